@@ -1,0 +1,200 @@
+/*
+ * xrt.h -- C ABI of the MI355X-native X-ray attenuation render path.
+ *
+ * This is the drop-in boundary for the reference's per-pixel render loop
+ * (Brandagot/SimpleRayTracing):
+ *
+ *   void renderLoop(Image&, const vector<TriangleMesh>&, RayTracerInfo&)
+ *       declared src/main.cxx:159-161, defined src/main.cxx:626-743,
+ *       called   src/main.cxx:237
+ *   void* renderLoopCallBack(void*)   (pixel-range twin)
+ *       src/main-pthreads-redo.cxx:660-771, PThreadData :184-213
+ *
+ * src/main-cuda.cxx (0 bytes) marks where the reference expected a GPU
+ * driver; this ABI fills that slot.  The C++ host library in
+ * simpleraytracing_amd/csrc/host keeps the reference's renderLoop signature and
+ * calls these entry points; INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions
+ *   - Plain C types only.  Every function returns an xrt_status (0 = OK);
+ *     xrt_last_error() gives the message.  Nothing throws across the ABI
+ *     (the reference throws std::runtime_error / std::out_of_range, which the
+ *     C++ host re-raises: main() exits 1 with "ERROR: ...", main.cxx:243-247).
+ *   - Image buffers are row-major, index (row - row_begin) * width + col, as
+ *     Image::setPixel (include/Image.inl:139-160) with a strip offset.
+ *   - One context per device; a context is not thread-safe (the reference's
+ *     threads write disjoint pixels of one Image, main-pthreads-redo.cxx:332).
+ *
+ * Output semantics (bit-exact with the reference):
+ *   image    f32  photonOut = 80 * expf(-(0.3971 * (float)(L * 0.1)))   main.cxx:725,739
+ *   lbuffer  f32  L = sum of sorted pair differences of the ray's hit
+ *                 distances (main.cxx:700-718); 0 for an odd hit count;
+ *                 +inf for a ray that hits nothing (z_buffer init, :646)
+ *   image_u8 u8   round(255 * image / 80), clamped -- Image::applyLUT's
+ *                 per-pixel formula (include/Image.inl:195-211), vmin 0, vmax 80
+ */
+#ifndef XRT_H
+#define XRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XRT_ABI_VERSION 1
+
+typedef enum xrt_status {
+    XRT_OK = 0,
+    XRT_ERR_ARGUMENT = 1,   /* bad pointer / size / row range (Image::setPixel's out_of_range) */
+    XRT_ERR_DEVICE = 2,     /* HIP runtime failure */
+    XRT_ERR_NO_MESH = 3,    /* render before xrt_upload_mesh */
+    XRT_ERR_OVERFLOW = 4,   /* internal capacity exceeded */
+    XRT_ERR_IO = 5,         /* file could not be read / written */
+    XRT_ERR_FORMAT = 6      /* malformed input file */
+} xrt_status;
+
+/* Kernel selection. */
+typedef enum xrt_kernel {
+    XRT_KERNEL_AUTO = 0,    /* = XRT_KERNEL_TILED */
+    XRT_KERNEL_BRUTE = 1,   /* every ray tests every triangle (renderLoop as written) */
+    XRT_KERNEL_TILED = 2    /* every 8x8 ray tile tests every triangle with a conservative
+                               edge-function cull, then exact Moller-Trumbore per ray */
+} xrt_kernel;
+
+/*
+ * Camera: RayTracerInfo (src/main.cxx:111-121, built by initialiseRayTracing
+ * :566-622) plus the pixel spacing computed in renderLoop's prologue
+ * (:634-641) and the image size.
+ */
+typedef struct xrt_camera {
+    float origin[3];        /* point source              RayTracerInfo::origin            */
+    float detector[3];      /* detector centre           RayTracerInfo::detector_position */
+    float up[3];            /* detector "v" axis         RayTracerInfo::up                */
+    float right[3];         /* detector "u" axis         RayTracerInfo::right             */
+    float pixel_spacing;    /* 2 * max(range_z / W, range_y / H)  main.cxx:639-641         */
+    uint32_t width;         /* Image::getWidth()                                           */
+    uint32_t height;        /* Image::getHeight()                                          */
+} xrt_camera;
+
+/* Per-render counters (the reference prints one line per odd ray, main.cxx:710). */
+typedef struct xrt_stats {
+    uint64_t rays;          /* rays rendered */
+    uint64_t hit_rays;      /* rays with >= 1 hit on mesh 0 */
+    uint64_t odd_rays;      /* rays with an odd hit count ("Only one intersect on this ray") */
+    uint64_t overflow_rays; /* rays whose hit list exceeded the register list (resolved exactly) */
+    uint64_t hits;          /* total recorded intersections */
+    uint32_t max_hits;      /* largest per-ray hit count */
+    uint32_t kernel;        /* xrt_kernel actually used */
+    double kernel_ms;       /* device time of the render kernels (HIP events) */
+} xrt_stats;
+
+typedef struct xrt_context xrt_context;
+
+/* --- lifetime ----------------------------------------------------------- */
+
+/* Creates a context on HIP device `device`. */
+int xrt_create(int device, xrt_context** out);
+void xrt_destroy(xrt_context* ctx);
+/* Last error message of `ctx` (or of the last failed xrt_create when ctx is NULL). */
+const char* xrt_last_error(const xrt_context* ctx);
+int xrt_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int xrt_device_count(void);
+
+/* --- mesh ---------------------------------------------------------------- */
+
+/*
+ * Uploads mesh 0 as a triangle soup: triangles[9*i .. 9*i+8] = p1, p2, p3 of
+ * TriangleMesh::getTriangle(i) (include/TriangleMesh.inl:208, Triangle.h:125-127).
+ * Only mesh 0 contributes to the image (the mesh filter at main.cxx:687), so the
+ * host uploads meshes[0] only.  Replaces any previous mesh; num_triangles may be 0.
+ */
+int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_triangles);
+
+/* --- camera (host-side arithmetic, no device needed) ---------------------- */
+
+/*
+ * Bounding box of a triangle soup: TriangleMesh::computeBoundingBox
+ * (src/TriangleMesh.cxx:192-228) / getBBox (src/main.cxx:538-563).
+ */
+int xrt_mesh_bbox(const float* triangles, uint64_t num_triangles, float lower[3], float upper[3]);
+
+/*
+ * Camera from the scene bounding box: initialiseRayTracing (main.cxx:566-622)
+ * and renderLoop's pixel spacing (main.cxx:634-641), f32/f64 rounding as written.
+ */
+int xrt_camera_from_bbox(const float lower[3], const float upper[3], uint32_t width,
+                         uint32_t height, xrt_camera* out);
+
+/* --- render --------------------------------------------------------------- */
+
+int xrt_set_kernel(xrt_context* ctx, int kernel);
+
+/*
+ * Renders image rows [row_begin, row_end) of camera->width x camera->height.
+ * HOST buffers (any may be NULL), each (row_end-row_begin)*width elements.
+ * Synchronous.  renderLoop == xrt_render_rows(ctx, cam, 0, H, image, ...).
+ */
+int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
+                    uint32_t row_end, float* image, float* lbuffer, uint8_t* image_u8,
+                    xrt_stats* stats);
+
+/*
+ * Same with DEVICE buffers on HIP stream `stream` (hipStream_t, NULL = default
+ * stream).  Asynchronous: returns after enqueueing.  Call xrt_read_stats()
+ * (which synchronises the stream) for counters and kernel time.
+ */
+int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
+                           uint32_t row_end, float* d_image, float* d_lbuffer,
+                           uint8_t* d_image_u8, void* stream);
+
+int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
+
+/*
+ * Kernel timing over a region of many renders without host synchronisation:
+ * after xrt_timing_begin, every render records a HIP event pair around its
+ * main render kernel on the render's stream; xrt_timing_end synchronises on the
+ * last event and returns the summed kernel time and the number of launches.
+ */
+int xrt_timing_begin(xrt_context* ctx);
+int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches);
+
+/* --- diagnostics (device probes of the exact device code paths) ----------- */
+
+/*
+ * Runs the kernel's Ray::intersect (src/Ray.cxx:72-124) on the device:
+ * rays[6*i] = origin xyz, unit direction xyz; triangles[9*i] = p1, p2, p3.
+ * hit[i] = 0/1, t[i] = distance (0 when no hit).  Host buffers.
+ */
+int xrt_probe_intersect(xrt_context* ctx, const float* rays, const float* triangles,
+                        uint64_t n, uint8_t* hit, float* t);
+
+typedef enum xrt_probe_op {
+    XRT_PROBE_EXPF = 0,     /* std::exp(float) == glibc expf                     */
+    XRT_PROBE_SQRTF = 1,    /* std::sqrt(float), correctly rounded               */
+    XRT_PROBE_RCP = 2,      /* (float)(1.0 / (double)x), src/Ray.cxx:99           */
+    XRT_PROBE_LUT_U8 = 3    /* 8-bit LUT of a photon value (out[i] = (float)u8)  */
+} xrt_probe_op;
+
+/* Evaluates one scalar device function elementwise.  Host buffers. */
+int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* out, uint64_t n);
+
+/*
+ * Host-side evaluation of the device expf restatement (the same source,
+ * compiled for the host): lets CPU-only tests check it against libm.
+ */
+void xrt_host_expf_batch(const float* in, float* out, uint64_t n);
+
+/*
+ * Test hook: caps the per-ray register hit list at `capacity` (1..16) so the
+ * exact overflow path runs.  0 restores the default (16).
+ */
+int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XRT_H */

@@ -1,0 +1,32 @@
+/*
+ * xrt_host.h -- C entry points of libxrt_host.so (the C++ drop-in host API,
+ * simpleraytracing_amd/csrc/host) that non-C++ callers use.
+ *
+ * xrt_host_load_ply replaces loadMeshes' Assimp import (src/main.cxx:427-510)
+ * followed by TriangleMesh::setGeometry(vertices, indices)
+ * (src/TriangleMesh.cxx:104-131): it returns mesh 0 as the triangle soup that
+ * xrt_upload_mesh takes.
+ */
+#ifndef XRT_HOST_H
+#define XRT_HOST_H
+
+#include <stdint.h>
+
+#include "xrt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Loads a PLY file; *triangles is malloc'd (free with xrt_host_free). */
+int xrt_host_load_ply(const char* path, float** triangles, uint64_t* num_triangles);
+void xrt_host_free(void* p);
+
+#ifdef __cplusplus
+}
+
+/* The process-wide context of `device` used by renderLoop / Ray::intersect. */
+xrt_context* xrt_host_device_context(int device);
+#endif
+
+#endif /* XRT_HOST_H */

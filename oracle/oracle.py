@@ -1,0 +1,190 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the CPU oracle.
+
+``liboracle.so`` is the plain-C restatement of the reference's render path
+(oracle/xrt_oracle.c); ``_ref/libxrt_ref.so`` is the reference's own
+src/Ray.cxx, src/Triangle.cxx and src/TriangleMesh.cxx compiled unmodified with
+a harness (oracle/ref_harness.cpp).  Both are built by oracle/Makefile.  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use them.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_F = ctypes.POINTER(ctypes.c_float)
+_U8 = ctypes.POINTER(ctypes.c_uint8)
+_I32 = ctypes.POINTER(ctypes.c_int32)
+_U32 = ctypes.POINTER(ctypes.c_uint32)
+
+_orc = None
+_ref = None
+
+
+def _fp(a):
+    return None if a is None else a.ctypes.data_as(_F)
+
+
+def lib():
+    global _orc
+    if _orc is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        L.orc_load_ply.argtypes = [ctypes.c_char_p, ctypes.POINTER(_F), ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_bbox.argtypes = [_F, ctypes.c_uint64, _F, _F]
+        L.orc_camera.argtypes = [_F, _F, ctypes.c_uint32, ctypes.c_uint32, _F]
+        L.orc_render_rows.restype = ctypes.c_int64
+        L.orc_render_rows.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, _F, _F, _U8, _I32, ctypes.c_int]
+        L.orc_render_row_list.restype = ctypes.c_int64
+        L.orc_render_row_list.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                          _U32, ctypes.c_uint32, _F, _F, _U8, _I32, ctypes.c_int]
+        L.orc_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
+        L.orc_save_text.argtypes = [_F, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+        L.orc_expf_batch.argtypes = [_F, _F, ctypes.c_uint64]
+        L.orc_lut_u8.restype = ctypes.c_uint8
+        L.orc_lut_u8.argtypes = [ctypes.c_float]
+        _orc = L
+    return _orc
+
+
+def ref_lib():
+    """The reference's own classes (oracle/_ref); None when not built."""
+    global _ref
+    if _ref is None:
+        path = os.path.join(HERE, "_ref", "libxrt_ref.so")
+        if not os.path.exists(path):
+            return None
+        R = ctypes.CDLL(path)
+        R.ref_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
+        R.ref_mesh_bbox.argtypes = [_F, ctypes.c_uint64, _F, _F]
+        R.ref_camera.argtypes = [_F, _F, ctypes.c_uint32, ctypes.c_uint32, _F]
+        R.ref_render_rows.restype = ctypes.c_int64
+        R.ref_render_rows.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, _F, _F]
+        _ref = R
+    return _ref
+
+
+def load_ply(path):
+    L = lib()
+    p = _F()
+    n = ctypes.c_uint64()
+    rc = L.orc_load_ply(str(path).encode(), ctypes.byref(p), ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oracle: cannot load {path} ({rc})")
+    T = n.value
+    out = np.ctypeslib.as_array(p, shape=(max(T, 1) * 9,))[: T * 9].copy()
+    L.orc_free(ctypes.cast(p, ctypes.c_void_p))
+    return out.reshape(T, 9)
+
+
+def bbox(tris):
+    tris = np.ascontiguousarray(tris, np.float32)
+    lo = np.zeros(3, np.float32)
+    hi = np.zeros(3, np.float32)
+    lib().orc_bbox(_fp(tris), len(tris), _fp(lo), _fp(hi))
+    return lo, hi
+
+
+def camera(lower, upper, width, height):
+    """13 floats: origin, detector, up, right, pixel spacing."""
+    lo = np.ascontiguousarray(lower, np.float32)
+    hi = np.ascontiguousarray(upper, np.float32)
+    cam = np.zeros(13, np.float32)
+    lib().orc_camera(_fp(lo), _fp(hi), width, height, _fp(cam))
+    return cam
+
+
+def camera_for_mesh(tris, width, height):
+    lo, hi = bbox(tris)
+    return camera(lo, hi, width, height)
+
+
+def render_rows(tris, cam13, width, height, row_begin=0, row_end=None, threads=None):
+    """(image f32, lbuffer f32, u8, nhits i32, odd) for rows [row_begin, row_end)."""
+    if row_end is None:
+        row_end = height
+    tris = np.ascontiguousarray(tris, np.float32)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    n = (row_end - row_begin) * width
+    img = np.empty(n, np.float32)
+    lb = np.empty(n, np.float32)
+    u8 = np.empty(n, np.uint8)
+    nh = np.empty(n, np.int32)
+    threads = threads or os.cpu_count() or 1
+    odd = lib().orc_render_rows(_fp(tris), len(tris), _fp(cam13), width, height, row_begin, row_end,
+                                _fp(img), _fp(lb), u8.ctypes.data_as(_U8), nh.ctypes.data_as(_I32),
+                                threads)
+    if odd < 0:
+        raise ValueError("bad row range")
+    return img, lb, u8, nh, odd
+
+
+def render_row_list(tris, cam13, width, height, rows, threads=None):
+    rows = np.ascontiguousarray(rows, np.uint32)
+    tris = np.ascontiguousarray(tris, np.float32)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    n = len(rows) * width
+    img = np.empty(n, np.float32)
+    lb = np.empty(n, np.float32)
+    u8 = np.empty(n, np.uint8)
+    nh = np.empty(n, np.int32)
+    threads = threads or os.cpu_count() or 1
+    odd = lib().orc_render_row_list(_fp(tris), len(tris), _fp(cam13), width, height,
+                                    rows.ctypes.data_as(_U32), len(rows), _fp(img), _fp(lb),
+                                    u8.ctypes.data_as(_U8), nh.ctypes.data_as(_I32), threads)
+    return img, lb, u8, nh, odd
+
+
+def intersect_batch(rays, tris):
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    hit = np.zeros(len(rays), np.uint8)
+    t = np.zeros(len(rays), np.float32)
+    lib().orc_intersect_batch(_fp(rays), _fp(tris), len(rays), hit.ctypes.data_as(_U8), _fp(t))
+    return hit, t
+
+
+def ref_intersect_batch(rays, tris):
+    R = ref_lib()
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    hit = np.zeros(len(rays), np.uint8)
+    t = np.zeros(len(rays), np.float32)
+    R.ref_intersect_batch(_fp(rays), _fp(tris), len(rays), hit.ctypes.data_as(_U8), _fp(t))
+    return hit, t
+
+
+def expf(x):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    lib().orc_expf_batch(_fp(x), _fp(out), x.size)
+    return out
+
+
+def save_text(img, width, height, path):
+    img = np.ascontiguousarray(img, np.float32)
+    return lib().orc_save_text(_fp(img), width, height, str(path).encode())
+
+
+def text_bytes(img, width, height):
+    """Image::saveTextFile's bytes for a float image (via a temp file)."""
+    import tempfile
+    with tempfile.NamedTemporaryFile(suffix=".txt", delete=False) as f:
+        path = f.name
+    try:
+        save_text(img, width, height, path)
+        with open(path, "rb") as f:
+            return f.read()
+    finally:
+        os.unlink(path)
+
+
+def lut_u8(v):
+    return lib().orc_lut_u8(float(v))

@@ -1,0 +1,188 @@
+"""simpleraytracing_amd -- MI355X-native X-ray attenuation render path.
+
+A drop-in for the reference's per-pixel ``renderLoop`` (Brandagot/
+SimpleRayTracing, src/main.cxx:626-743): ray generation -> brute-force
+Moller-Trumbore over the whole mesh -> L-buffer path length -> Beer-Lambert
+shade -> image store, bit-identical to the serial CPU program.
+
+The product is native: HIP kernels for gfx950 behind the C ABI of
+``include/xrt.h`` (``lib/libxrt.so``) and the C++ host API of
+``csrc/host`` (``lib/libxrt_host.so``, ``lib/xrt_main``).  This Python module is
+thin plumbing over that ABI for tests, ``bench.py`` and scripting; it never
+computes pixels itself.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BRUTE,  # noqa: F401
+                   XRT_KERNEL_TILED)
+
+__all__ = [
+    "Camera", "Stats", "Context", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
+    "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
+]
+
+
+class XrtError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__(f"xrt error {code}: {message}")
+        self.code = code
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _u8ptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def device_count() -> int:
+    return _abi.load().xrt_device_count()
+
+
+def load_ply(path: str) -> np.ndarray:
+    """Mesh 0 of a PLY file as a (T, 9) float32 triangle soup (p1, p2, p3)."""
+    host = _abi.load_host()
+    p = ctypes.POINTER(ctypes.c_float)()
+    n = ctypes.c_uint64()
+    rc = host.xrt_host_load_ply(str(path).encode(), ctypes.byref(p), ctypes.byref(n))
+    if rc != _abi.XRT_OK:
+        raise XrtError(rc, f"cannot load {path}")
+    try:
+        count = n.value
+        out = np.ctypeslib.as_array(p, shape=(max(count, 1) * 9,))[: count * 9].copy()
+    finally:
+        host.xrt_host_free(ctypes.cast(p, ctypes.c_void_p))
+    return out.reshape(count, 9)
+
+
+def mesh_bbox(tris: np.ndarray):
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    lo = np.zeros(3, np.float32)
+    hi = np.zeros(3, np.float32)
+    rc = _abi.load().xrt_mesh_bbox(_fptr(tris), len(tris), _fptr(lo), _fptr(hi))
+    if rc != _abi.XRT_OK:
+        raise XrtError(rc, "xrt_mesh_bbox")
+    return lo, hi
+
+
+def camera_from_bbox(lower, upper, width: int, height: int) -> Camera:
+    lo = np.ascontiguousarray(lower, dtype=np.float32)
+    hi = np.ascontiguousarray(upper, dtype=np.float32)
+    cam = Camera()
+    rc = _abi.load().xrt_camera_from_bbox(_fptr(lo), _fptr(hi), width, height, ctypes.byref(cam))
+    if rc != _abi.XRT_OK:
+        raise XrtError(rc, "xrt_camera_from_bbox")
+    return cam
+
+
+def camera_for_mesh(tris: np.ndarray, width: int, height: int) -> Camera:
+    lo, hi = mesh_bbox(tris)
+    return camera_from_bbox(lo, hi, width, height)
+
+
+class Context:
+    """One xrt_context (one device).  Not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _abi.load()
+        self._ctx = _abi._CtxP()
+        rc = self._lib.xrt_create(device, ctypes.byref(self._ctx))
+        if rc != _abi.XRT_OK:
+            raise XrtError(rc, self._lib.xrt_last_error(None).decode())
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self._lib.xrt_destroy(self._ctx)
+            self._ctx = _abi._CtxP()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != _abi.XRT_OK:
+            raise XrtError(rc, f"{what}: {self._lib.xrt_last_error(self._ctx).decode()}")
+
+    def upload_mesh(self, tris: np.ndarray):
+        tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        self._check(self._lib.xrt_upload_mesh(self._ctx, _fptr(tris), len(tris)), "xrt_upload_mesh")
+
+    def set_kernel(self, kernel: int):
+        self._check(self._lib.xrt_set_kernel(self._ctx, int(kernel)), "xrt_set_kernel")
+
+    def set_hit_capacity(self, capacity: int):
+        self._check(self._lib.xrt_set_hit_capacity(self._ctx, int(capacity)), "xrt_set_hit_capacity")
+
+    def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
+                    image=True, lbuffer=True, u8=True):
+        """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats)."""
+        if row_end is None:
+            row_end = cam.height
+        n = max(row_end - row_begin, 0) * cam.width
+        img = np.empty(n, np.float32) if image else None
+        lb = np.empty(n, np.float32) if lbuffer else None
+        u = np.empty(n, np.uint8) if u8 else None
+        st = Stats()
+        rc = self._lib.xrt_render_rows(
+            self._ctx, ctypes.byref(cam), row_begin, row_end,
+            _fptr(img) if img is not None else None,
+            _fptr(lb) if lb is not None else None,
+            _u8ptr(u) if u is not None else None, ctypes.byref(st))
+        self._check(rc, "xrt_render_rows")
+        return img, lb, u, st
+
+    def render_rows_device(self, cam: Camera, row_begin: int, row_end: int, d_image: int,
+                           d_lbuffer: int, d_u8: int, stream: int = 0):
+        """Device-buffer render (raw device pointers, hipStream_t as int); asynchronous."""
+        rc = self._lib.xrt_render_rows_device(self._ctx, ctypes.byref(cam), row_begin, row_end,
+                                              d_image or None, d_lbuffer or None, d_u8 or None,
+                                              stream or None)
+        self._check(rc, "xrt_render_rows_device")
+
+    def read_stats(self) -> Stats:
+        st = Stats()
+        self._check(self._lib.xrt_read_stats(self._ctx, ctypes.byref(st)), "xrt_read_stats")
+        return st
+
+    def timing_begin(self):
+        self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
+
+    def timing_end(self):
+        """(total kernel ms, launches) of the main render kernel since timing_begin."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        self._check(self._lib.xrt_timing_end(self._ctx, ctypes.byref(ms), ctypes.byref(n)),
+                    "xrt_timing_end")
+        return ms.value, n.value
+
+    def probe_intersect(self, rays: np.ndarray, tris: np.ndarray):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        n = len(rays)
+        hit = np.zeros(n, np.uint8)
+        t = np.zeros(n, np.float32)
+        self._check(self._lib.xrt_probe_intersect(self._ctx, _fptr(rays), _fptr(tris), n,
+                                                  _u8ptr(hit), _fptr(t)), "xrt_probe_intersect")
+        return hit, t
+
+    def probe_math(self, op: int, x: np.ndarray):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        out = np.empty_like(x)
+        self._check(self._lib.xrt_probe_math(self._ctx, int(op), _fptr(x), _fptr(out), x.size),
+                    "xrt_probe_math")
+        return out

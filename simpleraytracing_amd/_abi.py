@@ -1,0 +1,143 @@
+"""ctypes bindings of the C ABI (include/xrt.h, include/xrt_host.h).
+
+The shared libraries are built in-tree by ``simpleraytracing_amd/csrc/Makefile``
+into ``simpleraytracing_amd/lib/``.  Loading fails loudly when they are
+missing: there is no Python or CPU fallback for the render path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+
+XRT_OK = 0
+XRT_ERR_ARGUMENT = 1
+XRT_ERR_DEVICE = 2
+XRT_ERR_NO_MESH = 3
+XRT_ERR_OVERFLOW = 4
+XRT_ERR_IO = 5
+XRT_ERR_FORMAT = 6
+
+XRT_KERNEL_AUTO = 0
+XRT_KERNEL_BRUTE = 1
+XRT_KERNEL_TILED = 2
+
+XRT_PROBE_EXPF = 0
+XRT_PROBE_SQRTF = 1
+XRT_PROBE_RCP = 2
+XRT_PROBE_LUT_U8 = 3
+
+_f = ctypes.c_float
+_fp = ctypes.POINTER(ctypes.c_float)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+_vp = ctypes.c_void_p
+
+
+class Camera(ctypes.Structure):
+    """xrt_camera: RayTracerInfo (src/main.cxx:111-121) + pixel spacing + size."""
+
+    _fields_ = [
+        ("origin", _f * 3),
+        ("detector", _f * 3),
+        ("up", _f * 3),
+        ("right", _f * 3),
+        ("pixel_spacing", _f),
+        ("width", _u32),
+        ("height", _u32),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("rays", _u64),
+        ("hit_rays", _u64),
+        ("odd_rays", _u64),
+        ("overflow_rays", _u64),
+        ("hits", _u64),
+        ("max_hits", _u32),
+        ("kernel", _u32),
+        ("kernel_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class _Context(ctypes.Structure):
+    pass
+
+
+_CtxP = ctypes.POINTER(_Context)
+
+# name -> (restype, argtypes); every symbol declared in include/xrt.h
+XRT_SYMBOLS = {
+    "xrt_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_CtxP)]),
+    "xrt_destroy": (None, [_CtxP]),
+    "xrt_last_error": (ctypes.c_char_p, [_CtxP]),
+    "xrt_abi_version": (ctypes.c_int, []),
+    "xrt_device_count": (ctypes.c_int, []),
+    "xrt_upload_mesh": (ctypes.c_int, [_CtxP, _fp, _u64]),
+    "xrt_mesh_bbox": (ctypes.c_int, [_fp, _u64, _fp, _fp]),
+    "xrt_camera_from_bbox": (ctypes.c_int, [_fp, _fp, _u32, _u32, ctypes.POINTER(Camera)]),
+    "xrt_set_kernel": (ctypes.c_int, [_CtxP, ctypes.c_int]),
+    "xrt_render_rows": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _fp, _fp, _u8p,
+                                       ctypes.POINTER(Stats)]),
+    "xrt_render_rows_device": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _vp, _vp,
+                                              _vp, _vp]),
+    "xrt_read_stats": (ctypes.c_int, [_CtxP, ctypes.POINTER(Stats)]),
+    "xrt_timing_begin": (ctypes.c_int, [_CtxP]),
+    "xrt_timing_end": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
+    "xrt_probe_intersect": (ctypes.c_int, [_CtxP, _fp, _fp, _u64, _u8p, _fp]),
+    "xrt_probe_math": (ctypes.c_int, [_CtxP, ctypes.c_int, _fp, _fp, _u64]),
+    "xrt_host_expf_batch": (None, [_fp, _fp, _u64]),
+    "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
+}
+
+# every C symbol declared in include/xrt_host.h
+XRT_HOST_SYMBOLS = {
+    "xrt_host_load_ply": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_u64)]),
+    "xrt_host_free": (None, [_vp]),
+}
+
+_lib = None
+_host = None
+
+
+def _bind(lib, table):
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib_path(name="libxrt.so"):
+    return os.path.join(LIB_DIR, name)
+
+
+def load():
+    """Returns the bound libxrt.so; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        path = lib_path("libxrt.so")
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C simpleraytracing_amd/csrc` (there is no CPU fallback)")
+        _lib = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), XRT_SYMBOLS)
+    return _lib
+
+
+def load_host():
+    """Returns the bound libxrt_host.so (C++ host API's C entry points)."""
+    global _host
+    if _host is None:
+        load()
+        path = lib_path("libxrt_host.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: build simpleraytracing_amd/csrc first")
+        _host = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), XRT_HOST_SYMBOLS)
+    return _host

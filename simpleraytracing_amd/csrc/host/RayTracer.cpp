@@ -1,0 +1,257 @@
+// RayTracer.cpp -- see RayTracer.h.
+#include "RayTracer.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "PlyLoader.h"
+#include "xrt.h"
+#include "xrt_host.h"
+
+namespace {
+
+int g_kernel = -1;
+int g_device = -1;
+
+int kernel_choice()
+{
+    if (g_kernel >= 0) return g_kernel;
+    const char* k = std::getenv("XRT_KERNEL");
+    if (k && std::strcmp(k, "brute") == 0) return XRT_KERNEL_BRUTE;
+    if (k && std::strcmp(k, "tiled") == 0) return XRT_KERNEL_TILED;
+    return XRT_KERNEL_AUTO;
+}
+
+int device_choice()
+{
+    if (g_device >= 0) return g_device;
+    const char* d = std::getenv("XRT_DEVICE");
+    return d ? std::atoi(d) : 0;
+}
+
+void check(xrt_context* ctx, int rc, const char* what)
+{
+    if (rc != XRT_OK)
+        throw std::runtime_error(std::string(what) + ": " + xrt_last_error(ctx));
+}
+
+}  // namespace
+
+// One context per device for the process lifetime (contexts are not
+// thread-safe, so each is guarded by its own mutex).  Contexts are released by
+// process exit, not by static destructors that could run after the HIP
+// runtime has been torn down.
+struct DeviceSlot {
+    std::mutex lock;
+    xrt_context* ctx = nullptr;
+};
+
+static DeviceSlot& device_slot(int device)
+{
+    static std::mutex registry_lock;
+    static std::map<int, std::unique_ptr<DeviceSlot>> slots;
+    std::lock_guard<std::mutex> g(registry_lock);
+    auto& slot = slots[device];
+    if (!slot) slot.reset(new DeviceSlot());
+    if (!slot->ctx) {
+        xrt_context* ctx = nullptr;
+        int rc = xrt_create(device, &ctx);
+        if (rc != XRT_OK) throw std::runtime_error(std::string("xrt_create: ") + xrt_last_error(nullptr));
+        slot->ctx = ctx;
+    }
+    return *slot;
+}
+
+xrt_context* xrt_host_device_context(int device) { return device_slot(device).ctx; }
+
+void setRenderKernel(int kernel) { g_kernel = kernel; }
+void setRenderDevice(int device) { g_device = device; }
+
+// Assimp-free loadMeshes: one triangle mesh per file (main.cxx:455-508).
+void loadMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes)
+{
+    PlyMesh ply = loadPly(file_name);
+    meshes.clear();
+    TriangleMesh mesh;
+    mesh.setGeometry(ply.vertices, ply.indices);
+    meshes.push_back(mesh);
+}
+
+// main.cxx:538-563
+void getBBox(const std::vector<TriangleMesh>& meshes, Vec3& upper, Vec3& lower)
+{
+    const float inf = std::numeric_limits<float>::infinity();
+    lower = Vec3(inf, inf, inf);
+    upper = Vec3(-inf, -inf, -inf);
+    for (const TriangleMesh& m : meshes) {
+        for (unsigned k = 0; k < 3; ++k) {
+            lower[k] = std::min(lower[k], m.getLowerBBoxCorner()[k]);
+            upper[k] = std::max(upper[k], m.getUpperBBoxCorner()[k]);
+        }
+    }
+}
+
+// main.cxx:566-622; the arithmetic is xrt_camera_from_bbox's.
+RayTracerInfo initialiseRayTracing(std::vector<TriangleMesh>&, const Vec3& upper, const Vec3& lower,
+                                   unsigned int image_height, unsigned int image_width,
+                                   Image& output_image, float lut)
+{
+    float lo[3] = {lower[0], lower[1], lower[2]};
+    float hi[3] = {upper[0], upper[1], upper[2]};
+    xrt_camera cam;
+    if (xrt_camera_from_bbox(lo, hi, image_width, image_height, &cam) != XRT_OK)
+        throw std::runtime_error("initialiseRayTracing: invalid image size or bounding box");
+    output_image = Image(image_width, image_height, lut);
+    RayTracerInfo info;
+    info.detector_position = Vec3(cam.detector[0], cam.detector[1], cam.detector[2]);
+    info.origin = Vec3(cam.origin[0], cam.origin[1], cam.origin[2]);
+    info.up = Vec3(cam.up[0], cam.up[1], cam.up[2]);
+    info.right = Vec3(cam.right[0], cam.right[1], cam.right[2]);
+    info.upper_bbox_corner = upper;
+    info.lower_bbox_corner = lower;
+    info.range = upper - lower;
+    return info;
+}
+
+namespace {
+
+// Camera for a render: RayTracerInfo + the pixel spacing of renderLoop's
+// prologue (main.cxx:634-641), from the bbox of all meshes.
+xrt_camera camera_for(const Image& image, const std::vector<TriangleMesh>& meshes,
+                      const RayTracerInfo& info)
+{
+    Vec3 upper, lower;
+    getBBox(meshes, upper, lower);
+    Vec3 range = upper - lower;
+    float res1 = range[2] / image.getWidth();
+    float res2 = range[1] / image.getHeight();
+    xrt_camera cam;
+    for (unsigned k = 0; k < 3; ++k) {
+        cam.origin[k] = info.origin[k];
+        cam.detector[k] = info.detector_position[k];
+        cam.up[k] = info.up[k];
+        cam.right[k] = info.right[k];
+    }
+    cam.pixel_spacing = 2 * std::max(res1, res2);
+    cam.width = image.getWidth();
+    cam.height = image.getHeight();
+    return cam;
+}
+
+void render_strip(int device, const xrt_camera& cam, const std::vector<float>& soup,
+                  unsigned row_begin, unsigned row_end, float* image_strip, float* lbuffer_strip,
+                  unsigned char* u8_strip, xrt_stats* stats)
+{
+    DeviceSlot& slot = device_slot(device);
+    std::lock_guard<std::mutex> g(slot.lock);
+    xrt_context* ctx = slot.ctx;
+    check(ctx, xrt_set_kernel(ctx, kernel_choice()), "xrt_set_kernel");
+    check(ctx, xrt_upload_mesh(ctx, soup.data(), soup.size() / 9), "xrt_upload_mesh");
+    check(ctx, xrt_render_rows(ctx, &cam, row_begin, row_end, image_strip, lbuffer_strip, u8_strip, stats),
+          "xrt_render_rows");
+}
+
+std::vector<float> mesh0_soup(const std::vector<TriangleMesh>& meshes)
+{
+    // Only hits on meshes[0] count (main.cxx:687); other meshes cannot change
+    // the image, so only mesh 0 is sent to the device.
+    return meshes.empty() ? std::vector<float>() : meshes[0].flatten();
+}
+
+void report_odd(unsigned long long odd)
+{
+    for (unsigned long long i = 0; i < odd; ++i) std::cout << "Only one intersect on this ray" << std::endl;
+}
+
+}  // namespace
+
+void renderLoopRows(Image& image, const std::vector<TriangleMesh>& meshes, const RayTracerInfo& info,
+                    unsigned int row_begin, unsigned int row_end, float* lbuffer_strip,
+                    unsigned char* u8_strip, xrt_stats* stats)
+{
+    if (row_begin > row_end || row_end > image.getHeight())
+        throw std::out_of_range("renderLoopRows: row range outside the image");
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    render_strip(device_choice(), cam, soup, row_begin, row_end,
+                 image.getData() + (size_t)row_begin * image.getWidth(), lbuffer_strip, u8_strip, stats);
+}
+
+unsigned long long renderLoop(Image& image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info)
+{
+    xrt_stats stats;
+    renderLoopRows(image, meshes, info, 0, image.getHeight(), nullptr, nullptr, &stats);
+    report_odd(stats.odd_rays);
+    return stats.odd_rays;
+}
+
+unsigned long long renderLoopMultiGPU(Image& image, const std::vector<TriangleMesh>& meshes,
+                                      RayTracerInfo& info, int num_gpus)
+{
+    int available = xrt_device_count();
+    if (num_gpus < 1 || num_gpus > available)
+        throw std::runtime_error("renderLoopMultiGPU: " + std::to_string(num_gpus) + " GPUs requested, " +
+                                 std::to_string(available) + " available");
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    const unsigned H = image.getHeight();
+    std::vector<unsigned> begin(num_gpus), end(num_gpus);
+    unsigned rows_per = H / num_gpus, rem = H % num_gpus, next = 0;
+    for (int g = 0; g < num_gpus; ++g) {
+        begin[g] = next;
+        next += rows_per + (g < (int)rem ? 1u : 0u);
+        end[g] = next;
+    }
+    std::vector<xrt_stats> stats(num_gpus);
+    std::vector<std::exception_ptr> errors(num_gpus);
+    std::vector<std::thread> threads;
+    for (int g = 0; g < num_gpus; ++g) {
+        threads.emplace_back([&, g]() {
+            try {
+                render_strip(g, cam, soup, begin[g], end[g],
+                             image.getData() + (size_t)begin[g] * image.getWidth(), nullptr, nullptr,
+                             &stats[g]);
+            } catch (...) {
+                errors[g] = std::current_exception();
+            }
+        });
+    }
+    for (auto& t : threads) t.join();
+    for (auto& e : errors)
+        if (e) std::rethrow_exception(e);
+    unsigned long long odd = 0;
+    for (const auto& s : stats) odd += s.odd_rays;
+    report_odd(odd);
+    return odd;
+}
+
+// --- extern "C" helpers (include/xrt_host.h) --------------------------------
+extern "C" int xrt_host_load_ply(const char* path, float** triangles, uint64_t* num_triangles)
+{
+    if (!path || !triangles || !num_triangles) return XRT_ERR_ARGUMENT;
+    *triangles = nullptr;
+    *num_triangles = 0;
+    try {
+        std::vector<TriangleMesh> meshes;
+        loadMeshes(path, meshes);
+        std::vector<float> soup = mesh0_soup(meshes);
+        float* out = static_cast<float*>(std::malloc(sizeof(float) * (soup.size() ? soup.size() : 1)));
+        if (!out) return XRT_ERR_ARGUMENT;
+        std::memcpy(out, soup.data(), sizeof(float) * soup.size());
+        *triangles = out;
+        *num_triangles = soup.size() / 9;
+        return XRT_OK;
+    } catch (const std::exception& e) {
+        return std::string(e.what()).find("Cannot open") != std::string::npos ? XRT_ERR_IO : XRT_ERR_FORMAT;
+    }
+}
+
+extern "C" void xrt_host_free(void* p) { std::free(p); }

@@ -1,0 +1,60 @@
+// RayTracer.h -- scene set-up and the render loop of the drop-in host API.
+//
+// Same free functions and signatures as the reference's src/main.cxx:
+//   loadMeshes           main.cxx:139-140, 427-510
+//   getBBox              main.cxx:145-147, 538-563
+//   initialiseRayTracing main.cxx:149-157, 566-622
+//   renderLoop           main.cxx:159-161, 626-743  -> the GPU, via include/xrt.h
+// plus renderLoopRows (a row strip, the pthreads twin's pixel-range idea,
+// main-pthreads-redo.cxx:627-658) and renderLoopMultiGPU (row strips over
+// several GPUs).  Errors surface as exceptions, as in the reference.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "Image.h"
+#include "TriangleMesh.h"
+#include "Vec3.h"
+
+struct xrt_stats;
+
+// RayTracerInfo (main.cxx:111-121) without the Phong renderer's Light.
+struct RayTracerInfo {
+    Vec3 detector_position;
+    Vec3 origin;
+    Vec3 up;
+    Vec3 right;
+    Vec3 upper_bbox_corner;
+    Vec3 lower_bbox_corner;
+    Vec3 range;
+};
+
+// Render options (process-wide): kernel = 0 auto, 1 brute force, 2 tiled cull.
+// Defaults come from $XRT_KERNEL ("brute" / "tiled") and $XRT_DEVICE.
+void setRenderKernel(int kernel);
+void setRenderDevice(int device);
+
+void loadMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes);
+
+void getBBox(const std::vector<TriangleMesh>& meshes, Vec3& upper, Vec3& lower);
+
+RayTracerInfo initialiseRayTracing(std::vector<TriangleMesh>& meshes, const Vec3& upper,
+                                   const Vec3& lower, unsigned int image_height,
+                                   unsigned int image_width, Image& output_image, float lut);
+
+// Whole image; prints one "Only one intersect on this ray" line per odd ray
+// (main.cxx:710) and returns the number of such rays.
+unsigned long long renderLoop(Image& output_image, const std::vector<TriangleMesh>& meshes,
+                              RayTracerInfo& info);
+
+// Rows [row_begin, row_end) of output_image only; optional L-buffer / 8-bit
+// outputs of the same strip size.  Does not print.
+void renderLoopRows(Image& output_image, const std::vector<TriangleMesh>& meshes,
+                    const RayTracerInfo& info, unsigned int row_begin, unsigned int row_end,
+                    float* lbuffer_strip, unsigned char* u8_strip, xrt_stats* stats);
+
+// Row strips over `num_gpus` devices (rows_per = H / n, remainder to the first
+// strips), one host thread per device; returns the number of odd rays.
+unsigned long long renderLoopMultiGPU(Image& output_image, const std::vector<TriangleMesh>& meshes,
+                                      RayTracerInfo& info, int num_gpus);

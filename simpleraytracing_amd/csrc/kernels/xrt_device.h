@@ -1,0 +1,260 @@
+// xrt_device.h -- device-side arithmetic of the X-ray render path (gfx950).
+//
+// Every function here reproduces the reference's f32/f64 rounding sequence
+// exactly, so the GPU image is bit-identical to src/main.cxx's.  The numerical
+// contract (DESIGN.md "Numerical contract"):
+//   * no FMA contraction on the f32 path (built with -ffp-contract=off, and the
+//     pragma below); the only fused ops are the explicit fma() calls of
+//     glibc's expf, which are part of that function's definition;
+//   * f32 sqrt is correctly rounded (HIP's default
+//     -fhip-fp32-correctly-rounded-divide-sqrt); 1/det is computed as
+//     (float)(1.0/(double)det) exactly as src/Ray.cxx:99 writes it;
+//   * f32 denormals are preserved (no -fgpu-flush-denormals-to-zero).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace xrt {
+
+// Per-render triangle record: the ray-independent part of Ray::intersect
+// (src/Ray.cxx:86-122) for the shared ray origin.  64 bytes, read
+// wave-uniformly (one s_load_dwordx16 per triangle).
+struct alignas(16) TriRec {
+    float e1x, e1y, e1z;    // edge1 = P2 - P1                 Ray.cxx:86
+    float e2x, e2y, e2z;    // edge2 = P3 - P1                 Ray.cxx:87
+    float tvx, tvy, tvz;    // tvec  = origin - P1             Ray.cxx:102
+    float qvx, qvy, qvz;    // qvec  = tvec x edge1            Ray.cxx:112
+    float tnum;             // edge2 . qvec  (t * det)          Ray.cxx:122
+    float pad0, pad1, pad2;
+};
+static_assert(sizeof(TriRec) == 64, "TriRec must be 64 bytes");
+
+// Conservative screen-space footprint of a triangle (DESIGN.md "Tile cull"),
+// stored structure-of-arrays as four float4 planes of length T:
+//   plane 0  bbox  = (xmin, xmax, ymin, ymax) in pixel-centre coordinates
+//   plane 1..3 edge k = (a, b, c, 0):  a*col + b*row + c >= 0 holds at every
+//   pixel whose ray the reference's Ray::intersect can report as a hit with
+//   t > 1e-7.
+constexpr int kCullPlanes = 4;
+
+// Camera + strip parameters, passed by value.
+struct RenderParams {
+    float ox, oy, oz;       // RayTracerInfo::origin
+    float cx, cy, cz;       // RayTracerInfo::detector_position
+    float ux, uy, uz;       // RayTracerInfo::up
+    float rx, ry, rz;       // RayTracerInfo::right
+    float spacing;          // pixel_spacing, main.cxx:639-641
+    uint32_t width, height; // full image
+    uint32_t row_begin, row_end;
+    uint32_t num_triangles;
+    uint32_t hit_capacity;  // <= XRT_MAX_HITS
+};
+
+constexpr int kMaxHits = 16;
+
+// ---------------------------------------------------------------------------
+// Ray generation: src/main.cxx:652-661 and the Ray ctor, include/Ray.inl:74-85.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void make_ray(const RenderParams& p, uint32_t row, uint32_t col,
+                                         float& dx, float& dy, float& dz)
+{
+    // :655-656  float * (0.5 + unsigned - unsigned / 2.0) in double, narrowed once
+    float v_off = (float)((double)p.spacing * ((0.5 + (double)row) - (double)p.height / 2.0));
+    float u_off = (float)((double)p.spacing * ((0.5 + (double)col) - (double)p.width / 2.0));
+    // :659  detector + up*v + right*u - origin  (Vec3 ops left to right, f32)
+    float X = ((p.cx + p.ux * v_off) + p.rx * u_off) - p.ox;
+    float Y = ((p.cy + p.uy * v_off) + p.ry * u_off) - p.oy;
+    float Z = ((p.cz + p.uz * v_off) + p.rz * u_off) - p.oz;
+    // :660  Vec3::normalise (Vec3.inl:469-476)
+    float len = sqrtf((X * X + Y * Y) + Z * Z);
+    X = X / len;
+    Y = Y / len;
+    Z = Z / len;
+    // Ray ctor normalises again; a zero length keeps the default (0,0,0).
+    float len2 = sqrtf((X * X + Y * Y) + Z * Z);
+    if (len2 != 0.0f) {
+        dx = X / len2;
+        dy = Y / len2;
+        dz = Z / len2;
+    } else {
+        dx = 0.0f;
+        dy = 0.0f;
+        dz = 0.0f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Ray::intersect, src/Ray.cxx:72-124, with the ray-independent terms taken
+// from the TriRec.  A conservative pre-test rejects only when the reference's
+// `u < 0 || u > 1` test (Ray.cxx:106) provably rejects, so the f64 division
+// runs only for candidates (DESIGN.md "Early reject").
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool mt_intersect(float dx, float dy, float dz,
+                                             float e1x, float e1y, float e1z,
+                                             float e2x, float e2y, float e2z,
+                                             float tvx, float tvy, float tvz,
+                                             float qvx, float qvy, float qvz,
+                                             float tnum, float& t)
+{
+    // pvec = direction x edge2               Ray.cxx:90 (Vec3.inl:321-329)
+    float px = dy * e2z - dz * e2y;
+    float py = dz * e2x - dx * e2z;
+    float pz = dx * e2y - dy * e2x;
+    // det = edge1 . pvec                     Ray.cxx:93
+    float det = (e1x * px + e1y * py) + e1z * pz;
+    // tvec . pvec (u * det)                  Ray.cxx:105
+    float a = (tvx * px + tvy * py) + tvz * pz;
+
+    // Early reject.  With D = |det|, A = a*sign(det): u = RN(A * RN(1/D)).
+    //   A < -2^-20 D       =>  u <= -2^-20 (1 - 2^-21) < 0        (reference rejects)
+    //   A > RN(D (1+2^-20)) =>  u >= RN(1 + 2^-22 - tiny) > 1      (reference rejects)
+    // NaNs fail both compares and fall through to the exact test; det == +-0
+    // with a != 0 rejects here, as the reference does at Ray.cxx:94.
+    float D = fabsf(det);
+    float A = __int_as_float(__float_as_int(a) ^ (__float_as_int(det) & 0x80000000));
+    if (A < D * -0x1p-20f || A > D * 0x1.00001p0f) return false;
+
+    if (det == 0.0f) return false;                        // Ray.cxx:94 (fpclassify FP_ZERO)
+    float inv_det = (float)(1.0 / (double)det);           // Ray.cxx:99
+    float u = a * inv_det;                                // Ray.cxx:105
+    if (u < 0.0f || u > 1.0f) return false;               // Ray.cxx:106
+    float v = ((dx * qvx + dy * qvy) + dz * qvz) * inv_det;   // Ray.cxx:115
+    if (v < 0.0f || u + v > 1.0f) return false;           // Ray.cxx:116
+    t = tnum * inv_det;                                   // Ray.cxx:122
+    return true;
+}
+
+// t > 0.0000001 in double, main.cxx:687
+__device__ __forceinline__ bool accept_t(float t) { return (double)t > 0.0000001; }
+
+// ---------------------------------------------------------------------------
+// Per-ray sorted hit list in registers (static indices only).  Replaces the
+// per-pixel std::vector + std::sort of main.cxx:666-704.
+// ---------------------------------------------------------------------------
+struct HitList {
+    float h[kMaxHits];
+    uint32_t n;
+
+    __device__ __forceinline__ void init()
+    {
+#pragma unroll
+        for (int k = 0; k < kMaxHits; ++k) h[k] = __builtin_inff();
+        n = 0;
+    }
+
+    // Insertion keeps h[0..min(n,K)) ascending; +inf sentinels fill the rest.
+    __device__ __forceinline__ void push(float t)
+    {
+#pragma unroll
+        for (int k = 0; k < kMaxHits; ++k) {
+            float cur = h[k];
+            bool lt = t < cur;
+            h[k] = lt ? t : cur;
+            t = lt ? cur : t;
+        }
+        ++n;
+    }
+
+    // main.cxx:703-708: pairwise sum of the sorted list, sequential f32.
+    __device__ __forceinline__ float path_length() const
+    {
+        float distance = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kMaxHits / 2; ++k)
+            if (2u * k + 1u < n) distance += h[2 * k + 1] - h[2 * k];
+        return distance;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// glibc 2.35 expf (sysdeps/ieee754/flt-32/e_expf.c with e_exp2f_data.c,
+// EXP2F_TABLE_BITS = 5), as x86-64 glibc dispatches it on FMA hardware
+// (e_expf-fma.c: the compiler fuses InvLn2N*x into both uses and the
+// polynomial).  This is the function std::exp(float) binds to in
+// src/main.cxx:739.  Bit-identical to the system libm on all 2^32 inputs
+// (tools/gen_expf_table.py, tests/test_expf.py).
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ double xrt_u64_as_double(uint64_t u)
+{
+    double d;
+    __builtin_memcpy(&d, &u, 8);
+    return d;
+}
+
+__host__ __device__ __forceinline__ uint64_t xrt_double_as_u64(double d)
+{
+    uint64_t u;
+    __builtin_memcpy(&u, &d, 8);
+    return u;
+}
+
+__host__ __device__ __forceinline__ uint64_t xrt_exp2f_tab(uint32_t i)
+{
+    // tab[i] = asuint64(RN(2^(i/32))) - (i << 47)
+    constexpr uint64_t tab[32] = {
+        0x3ff0000000000000ULL, 0x3fefd9b0d3158574ULL, 0x3fefb5586cf9890fULL, 0x3fef9301d0125b51ULL,
+        0x3fef72b83c7d517bULL, 0x3fef54873168b9aaULL, 0x3fef387a6e756238ULL, 0x3fef1e9df51fdee1ULL,
+        0x3fef06fe0a31b715ULL, 0x3feef1a7373aa9cbULL, 0x3feedea64c123422ULL, 0x3feece086061892dULL,
+        0x3feebfdad5362a27ULL, 0x3feeb42b569d4f82ULL, 0x3feeab07dd485429ULL, 0x3feea47eb03a5585ULL,
+        0x3feea09e667f3bcdULL, 0x3fee9f75e8ec5f74ULL, 0x3feea11473eb0187ULL, 0x3feea589994cce13ULL,
+        0x3feeace5422aa0dbULL, 0x3feeb737b0cdc5e5ULL, 0x3feec49182a3f090ULL, 0x3feed503b23e255dULL,
+        0x3feee89f995ad3adULL, 0x3feeff76f2fb5e47ULL, 0x3fef199bdd85529cULL, 0x3fef3720dcef9069ULL,
+        0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL,
+    };
+    return tab[i & 31];
+}
+
+__host__ __device__ __forceinline__ float xrt_expf(float x)
+{
+    constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
+    constexpr double kShift = 0x1.8p+52;
+    constexpr double kC0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32;
+    constexpr double kC1 = 0x1.ebfce50fac4f3p-3 / 32 / 32;
+    constexpr double kC2 = 0x1.62e42ff0c52d6p-1 / 32;
+
+    uint32_t ix;
+    __builtin_memcpy(&ix, &x, 4);
+    uint32_t abstop = (ix >> 20) & 0x7ff;
+    if (abstop >= 0x42b) {                  // |x| >= 88 or NaN
+        if (ix == 0xff800000u) return 0.0f; // -inf
+        if (abstop >= 0x7f8) return x + x;  // +inf or NaN
+        if (x > 0x1.62e42ep6f) return __builtin_inff();   // overflow
+        if (x < -0x1.9fe368p6f) return 0.0f;              // underflow
+    }
+    double xd = (double)x;
+    double kd = __builtin_fma(kInvLn2N, xd, kShift);
+    uint64_t ki = xrt_double_as_u64(kd);
+    kd -= kShift;
+    double r = __builtin_fma(kInvLn2N, xd, -kd);
+    uint64_t t = xrt_exp2f_tab((uint32_t)(ki % 32)) + (ki << 47);
+    double s = xrt_u64_as_double(t);
+    double z = __builtin_fma(kC0, r, kC1);
+    double r2 = r * r;
+    double y = __builtin_fma(kC2, r, 1.0);
+    y = __builtin_fma(z, r2, y);
+    y = y * s;
+    return (float)y;
+}
+
+// Beer-Lambert shade, main.cxx:725 and :739.
+__host__ __device__ __forceinline__ float shade(float distance)
+{
+    float cm = (float)((double)distance * 0.1);
+    return 80.000f * xrt_expf(-(0.3971f * cm));
+}
+
+// 8-bit image: Image::applyLUT's per-pixel formula (include/Image.inl:195-211)
+// with vmin = 0, vmax = 80; NaN (undefined in the reference) maps to 0.
+__host__ __device__ __forceinline__ uint8_t lut_u8(float v)
+{
+    const float vmin = 0.0f, vmax = 80.0f;
+    if (v < vmin) return 0;
+    if (v > vmax) return 255;
+    if (v != v) return 0;
+    return (uint8_t)__builtin_round(255.0 * (double)(v - vmin) / (double)(vmax - vmin));
+}
+
+}  // namespace xrt

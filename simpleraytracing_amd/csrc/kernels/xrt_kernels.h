@@ -1,0 +1,530 @@
+// xrt_kernels.h -- HIP kernels of the X-ray render path for gfx950 (CDNA4).
+//
+// Kernels
+//   k_prep           one thread per triangle: TriRec (ray-independent part of
+//                    Ray::intersect for the shared origin) and the cull planes
+//                    (the conservative screen-space footprint, SoA float4).
+//   k_render_brute   renderLoop as written: one ray per lane, one 8x8 ray tile
+//                    per wavefront, every ray tests every triangle; triangle
+//                    records are wave-uniform scalar loads.
+//   k_render_tiled   one 32x32 pixel region per workgroup (4 waves, 4 tiles of
+//                    8x8 each).  Phase 1: all 256 lanes sweep the whole mesh's
+//                    footprint boxes (coalesced 16-B loads) and compact the
+//                    region's candidates into an LDS list.  Phase 2: per 8x8
+//                    tile, one lane per candidate evaluates the three relaxed
+//                    edge functions, a wave ballot keeps the survivors, and
+//                    every survivor runs the exact Moller-Trumbore test for all
+//                    64 rays.  Output is bit-identical to k_render_brute.
+//   k_overflow       exact fix-up for rays whose register hit list overflowed:
+//                    streams the sorted hit sequence by repeated minimum scans.
+//   k_probe_*        device probes of the exact device code paths (tests).
+#pragma once
+
+#include "xrt_device.h"
+
+namespace xrt {
+
+struct DevStats {
+    unsigned long long rays;
+    unsigned long long hit_rays;
+    unsigned long long odd_rays;
+    unsigned long long overflow_rays;
+    unsigned long long hits;
+    unsigned int max_hits;
+    unsigned int overflow_count;   // entries in the overflow list
+};
+
+// Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
+struct CullParams {
+    double dmax;      // upper bound of |D| (unnormalised ray direction) over the image
+    double mag;       // upper bound of the magnitudes summed while forming D
+    double width, height;
+};
+
+struct Outputs {
+    float* image;
+    float* lbuffer;
+    uint8_t* image_u8;
+    uint32_t* overflow_list;   // capacity = strip rays
+    DevStats* stats;
+};
+
+constexpr double kEps = 0x1p-24;
+
+__device__ __forceinline__ void cross_d(const double a[3], const double b[3], double o[3])
+{
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ double dot_d(const double a[3], const double b[3])
+{
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+__device__ __forceinline__ double l1_d(const double a[3])
+{
+    return fabs(a[0]) + fabs(a[1]) + fabs(a[2]);
+}
+
+// ---------------------------------------------------------------------------
+// k_prep
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
+                                              RenderParams p, CullParams cp,
+                                              TriRec* __restrict__ recs,
+                                              float4* __restrict__ culls)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T) return;
+    const float* P = tris + 9ull * i;
+    float p1x = P[0], p1y = P[1], p1z = P[2];
+    float p2x = P[3], p2y = P[4], p2z = P[5];
+    float p3x = P[6], p3y = P[7], p3z = P[8];
+
+    // Exactly the reference's f32 operations (Ray.cxx:86-87, 102, 112, 122).
+    TriRec r;
+    r.e1x = p2x - p1x; r.e1y = p2y - p1y; r.e1z = p2z - p1z;
+    r.e2x = p3x - p1x; r.e2y = p3y - p1y; r.e2z = p3z - p1z;
+    r.tvx = p.ox - p1x; r.tvy = p.oy - p1y; r.tvz = p.oz - p1z;
+    r.qvx = r.tvy * r.e1z - r.tvz * r.e1y;
+    r.qvy = r.tvz * r.e1x - r.tvx * r.e1z;
+    r.qvz = r.tvx * r.e1y - r.tvy * r.e1x;
+    r.tnum = (r.e2x * r.qvx + r.e2y * r.qvy) + r.e2z * r.qvz;
+    r.pad0 = r.pad1 = r.pad2 = 0.0f;
+    recs[i] = r;
+    if (!culls) return;
+
+    // --- conservative footprint (DESIGN.md "Tile cull") ---------------------
+    const float kInf = __builtin_inff();
+    struct {
+        float4 bbox, e0, e1, e2;
+    } c;
+    c.bbox = make_float4(-kInf, kInf, -kInf, kInf);   // never cull
+    c.e0 = make_float4(0.0f, 0.0f, kInf, 0.0f);
+    c.e1 = c.e0;
+    c.e2 = c.e0;
+    auto store = [&]() {
+        culls[i] = c.bbox;
+        culls[(size_t)T + i] = c.e0;
+        culls[2 * (size_t)T + i] = c.e1;
+        culls[3 * (size_t)T + i] = c.e2;
+    };
+
+    bool finite = isfinite(r.tnum) && isfinite(r.qvx) && isfinite(r.qvy) && isfinite(r.qvz);
+    if (finite && r.tnum == 0.0f) {
+        // t = 0 * inv_det is never > 1e-7: the triangle never contributes.
+        c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
+        c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
+        store();
+        return;
+    }
+    double E1[3] = {r.e1x, r.e1y, r.e1z};
+    double E2[3] = {r.e2x, r.e2y, r.e2z};
+    double TV[3] = {r.tvx, r.tvy, r.tvz};
+    double l1e1 = l1_d(E1), l1e2 = l1_d(E2), l1tv = l1_d(TV);
+    bool sane = finite && l1e1 > 0x1p-60 && l1e1 < 0x1p60 && l1e2 > 0x1p-60 && l1e2 < 0x1p60 &&
+                l1tv > 0x1p-60 && l1tv < 0x1p60;
+    if (!sane) {
+        store();
+        return;
+    }
+    double s = r.tnum > 0.0f ? 1.0 : -1.0;
+
+    double N[3][3];
+    cross_d(E2, TV, N[1]);     // a   = d . (edge2 x tvec)
+    cross_d(TV, E1, N[2]);     // b   = d . (tvec x edge1)
+    double Nd[3];
+    cross_d(E2, E1, Nd);       // det = d . (edge2 x edge1)
+    for (int k = 0; k < 3; ++k) N[0][k] = Nd[k] - N[1][k] - N[2][k];
+
+    double Ba = 32.0 * kEps * l1tv * l1e2;
+    double Bb = 32.0 * kEps * l1tv * l1e1;
+    double Bd = 32.0 * kEps * l1e1 * l1e2;
+    double Bx = 16.0 * kEps * l1e1 * l1e2;
+    double B[3] = {Bd + Ba + Bb + Bx, Ba + Bx, Bb + Bx};
+
+    double Cv[3] = {(double)p.cx - p.ox, (double)p.cy - p.oy, (double)p.cz - p.oz};
+    double Up[3] = {p.ux, p.uy, p.uz};
+    double Rt[3] = {p.rx, p.ry, p.rz};
+    double ps = p.spacing;
+    double cv = ps * (0.5 - cp.height / 2.0);
+    double cu = ps * (0.5 - cp.width / 2.0);
+
+    float ea[3], eb[3], ec[3];
+    bool constant_edge = false;
+    for (int k = 0; k < 3; ++k) {
+        double upn = dot_d(Up, N[k]);
+        double rtn = dot_d(Rt, N[k]);
+        double alpha = dot_d(Cv, N[k]) + cv * upn + cu * rtn;
+        double beta = ps * upn;    // per image row
+        double gamma = ps * rtn;   // per image column
+        double l1n = l1_d(N[k]);
+        double M = 4.0 * ((B[k] + 12.0 * kEps * l1n) * cp.dmax + 8.0 * kEps * cp.mag * l1n);
+        double nrm = sqrt(beta * beta + gamma * gamma);
+        if (!(nrm > 1e-30 * (fabs(alpha) + M + 1e-300))) {
+            // Edge function constant over the image plane.
+            if (s * alpha + M < 0.0) {
+                c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
+                c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
+                c.e1 = c.e2 = make_float4(0.0f, 0.0f, kInf, 0.0f);
+                store();
+                return;
+            }
+            ea[k] = 0.0f;
+            eb[k] = 0.0f;
+            ec[k] = kInf;
+            constant_edge = true;
+            continue;
+        }
+        double a = s * gamma / nrm;
+        double b = s * beta / nrm;
+        double cc = (s * alpha + M) / nrm;
+        cc += 0.05 + 64.0 * kEps * (cp.width + cp.height + fabs(cc));
+        ea[k] = (float)a;
+        eb[k] = (float)b;
+        ec[k] = (float)cc;
+    }
+    c.e0 = make_float4(ea[0], eb[0], ec[0], 0.0f);
+    c.e1 = make_float4(ea[1], eb[1], ec[1], 0.0f);
+    c.e2 = make_float4(ea[2], eb[2], ec[2], 0.0f);
+
+    if (!constant_edge) {
+        // Loosened triangle {a_k x + b_k y + c_k >= 0}: bounded iff the inward
+        // normals positively span the plane (cross products share a sign).
+        double A[3] = {ea[0], ea[1], ea[2]}, Bq[3] = {eb[0], eb[1], eb[2]}, Cq[3] = {ec[0], ec[1], ec[2]};
+        double x01 = A[0] * Bq[1] - A[1] * Bq[0];
+        double x12 = A[1] * Bq[2] - A[2] * Bq[1];
+        double x20 = A[2] * Bq[0] - A[0] * Bq[2];
+        const double tiny = 1e-9;
+        bool pos = x01 > tiny && x12 > tiny && x20 > tiny;
+        bool neg = x01 < -tiny && x12 < -tiny && x20 < -tiny;
+        if (pos || neg) {
+            double vx[3], vy[3];
+            const int pi[3] = {0, 1, 2}, pj[3] = {1, 2, 0};
+            const double cr[3] = {x01, x12, x20};
+            for (int q = 0; q < 3; ++q) {
+                int ii = pi[q], jj = pj[q];
+                vx[q] = (-Cq[ii] * Bq[jj] + Cq[jj] * Bq[ii]) / cr[q];
+                vy[q] = (-A[ii] * Cq[jj] + A[jj] * Cq[ii]) / cr[q];
+            }
+            double xmin = fmin(vx[0], fmin(vx[1], vx[2])), xmax = fmax(vx[0], fmax(vx[1], vx[2]));
+            double ymin = fmin(vy[0], fmin(vy[1], vy[2])), ymax = fmax(vy[0], fmax(vy[1], vy[2]));
+            double sx = 0.01 + 1e-4 * (fabs(xmin) + fabs(xmax));
+            double sy = 0.01 + 1e-4 * (fabs(ymin) + fabs(ymax));
+            if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax))
+                c.bbox = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy),
+                                     (float)(ymax + sy));
+        }
+    }
+    store();
+}
+
+// ---------------------------------------------------------------------------
+// Per-ray epilogue shared by the render kernels: L-buffer, shade, LUT, stores,
+// statistics.  Returns true if the ray overflowed (its outputs are then written
+// by k_overflow).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_stats(DevStats* st, bool active, uint32_t n, bool odd,
+                                           bool overflow)
+{
+    unsigned long long m_act = __ballot(active);
+    unsigned long long m_hit = __ballot(active && n > 0);
+    unsigned long long m_odd = __ballot(active && odd);
+    unsigned long long m_ovf = __ballot(active && overflow);
+    uint32_t hits = active ? n : 0u;
+    uint32_t mx = hits;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        hits += __shfl_xor(hits, off);
+        uint32_t o = __shfl_xor(mx, off);
+        mx = mx > o ? mx : o;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&st->rays, (unsigned long long)__popcll(m_act));
+        if (m_hit) atomicAdd(&st->hit_rays, (unsigned long long)__popcll(m_hit));
+        if (m_odd) atomicAdd(&st->odd_rays, (unsigned long long)__popcll(m_odd));
+        if (m_ovf) atomicAdd(&st->overflow_rays, (unsigned long long)__popcll(m_ovf));
+        if (hits) atomicAdd(&st->hits, (unsigned long long)hits);
+        if (mx) atomicMax(&st->max_hits, mx);
+    }
+}
+
+__device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
+                                           uint32_t row, uint32_t col, const HitList& hl)
+{
+    bool overflow = hl.n > p.hit_capacity;
+    bool odd = (hl.n & 1u) != 0u;
+    wave_stats(out.stats, active, hl.n, odd, overflow);
+    if (!active) return;
+    size_t o = (size_t)(row - p.row_begin) * p.width + col;
+    if (overflow) {
+        uint32_t slot = atomicAdd(&out.stats->overflow_count, 1u);
+        out.overflow_list[slot] = (uint32_t)o;
+        return;
+    }
+    // main.cxx:700-718
+    float distance = 0.0f;
+    float lval = __builtin_inff();
+    if (hl.n > 0) {
+        if (!odd) distance = hl.path_length();
+        lval = distance;
+    }
+    float photon = shade(distance);
+    if (out.image) out.image[o] = photon;
+    if (out.lbuffer) out.lbuffer[o] = lval;
+    if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+}
+
+// Loads one triangle record with a wave-uniform index (scalar loads).
+__device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
+                                            float dy, float dz, HitList& hl)
+{
+    const float4* q = reinterpret_cast<const float4*>(recs + j);
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    float t;
+    if (mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
+        accept_t(t))
+        hl.push(t);
+}
+
+// ---------------------------------------------------------------------------
+// k_render_brute: block = 256 lanes = 2x2 waves, each wave one 8x8 ray tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__ recs,
+                                                      RenderParams p, Outputs out)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t col = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
+    const uint32_t row = p.row_begin + (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    const bool active = col < p.width && row < p.row_end;
+
+    float dx, dy, dz;
+    make_ray(p, row, col, dx, dy, dz);
+    HitList hl;
+    hl.init();
+    const uint32_t T = p.num_triangles;
+    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
+    finish_ray(p, out, active, row, col, hl);
+}
+
+// ---------------------------------------------------------------------------
+// k_render_tiled
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRegion = 32;        // pixels per region side
+constexpr uint32_t kListCap = 4096;     // LDS candidate list capacity
+
+__device__ __forceinline__ bool edge_pass(const float4* __restrict__ culls, uint32_t T, uint32_t j,
+                                          float xc, float yc, float hx, float hy)
+{
+    float4 e0 = culls[(size_t)T + j], e1 = culls[2 * (size_t)T + j], e2 = culls[3 * (size_t)T + j];
+    float v0 = (e0.x * xc + e0.y * yc) + (e0.z + (fabsf(e0.x) * hx + fabsf(e0.y) * hy));
+    float v1 = (e1.x * xc + e1.y * yc) + (e1.z + (fabsf(e1.x) * hx + fabsf(e1.y) * hy));
+    float v2 = (e2.x * xc + e2.y * yc) + (e2.z + (fabsf(e2.x) * hx + fabsf(e2.y) * hy));
+    return v0 >= 0.0f && v1 >= 0.0f && v2 >= 0.0f;
+}
+
+__global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__ recs,
+                                                      const float4* __restrict__ culls,
+                                                      RenderParams p, Outputs out)
+{
+    __shared__ uint32_t s_list[kListCap];
+    __shared__ uint32_t s_count;
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = tid >> 6;
+    const uint32_t T = p.num_triangles;
+
+    const uint32_t rx0 = blockIdx.x * kRegion;
+    const uint32_t ry0 = p.row_begin + blockIdx.y * kRegion;
+    const uint32_t rx1 = min(rx0 + kRegion, p.width) - 1u;       // inclusive
+    const uint32_t ry1 = min(ry0 + kRegion, p.row_end) - 1u;
+
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+
+    // Phase 1: footprint boxes of the whole mesh vs the region (pixel centres).
+    const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
+    for (uint32_t base = 0; base < T; base += 256u) {
+        uint32_t j = base + tid;
+        bool pass = false;
+        if (j < T) {
+            float4 bb = culls[j];
+            pass = !(bb.y < fx0 || bb.x > fx1 || bb.w < fy0 || bb.z > fy1);
+        }
+        unsigned long long m = __ballot(pass);
+        if (m) {
+            uint32_t cnt = (uint32_t)__popcll(m);
+            uint32_t wbase = 0;
+            if (lane == 0) wbase = atomicAdd(&s_count, cnt);
+            wbase = __shfl(wbase, 0);
+            if (pass) {
+                uint32_t idx = wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (idx < kListCap) s_list[idx] = j;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n_cand = s_count;
+    const bool use_list = n_cand <= kListCap;
+    const uint32_t n_scan = use_list ? n_cand : T;
+
+    // Phase 2: each wave takes tiles wave, wave+4, wave+8, wave+12.
+    for (uint32_t tile = wave; tile < 16u; tile += 4u) {
+        const uint32_t tx0 = rx0 + (tile & 3u) * 8u;
+        const uint32_t ty0 = ry0 + (tile >> 2) * 8u;
+        if (tx0 >= p.width || ty0 >= p.row_end) continue;          // wave-uniform
+        const uint32_t col = tx0 + (lane & 7u);
+        const uint32_t row = ty0 + (lane >> 3);
+        const bool active = col < p.width && row < p.row_end;
+        const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
+        const float hx = 3.5f, hy = 3.5f;
+
+        float dx, dy, dz;
+        make_ray(p, row, col, dx, dy, dz);
+        HitList hl;
+        hl.init();
+
+        for (uint32_t base = 0; base < n_scan; base += 64u) {
+            uint32_t k = base + lane;
+            uint32_t j = 0;
+            bool pass = false;
+            if (k < n_scan) {
+                j = use_list ? s_list[k] : k;
+                pass = edge_pass(culls, T, j, xc, yc, hx, hy);
+            }
+            unsigned long long m = __ballot(pass);
+            while (m) {
+                uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                uint32_t jj = __builtin_amdgcn_readlane(j, b);
+                test_record(recs, jj, dx, dy, dz, hl);
+            }
+        }
+        finish_ray(p, out, active, row, col, hl);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_overflow: exact result for rays whose hit count exceeded the register
+// list.  The sorted hit sequence is streamed by repeated scans for the next
+// larger distance (with its multiplicity), so any hit count is handled with
+// O(1) state: main.cxx:703-708's sum in the same order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_overflow(const TriRec* __restrict__ recs, RenderParams p,
+                                                 Outputs out)
+{
+    const uint32_t count = out.stats->overflow_count;
+    const uint32_t T = p.num_triangles;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < count;
+         e += gridDim.x * blockDim.x) {
+        uint32_t o = out.overflow_list[e];
+        uint32_t row = p.row_begin + o / p.width;
+        uint32_t col = o % p.width;
+        float dx, dy, dz;
+        make_ray(p, row, col, dx, dy, dz);
+
+        // Scan 1: total count.
+        uint64_t n = 0;
+        for (uint32_t j = 0; j < T; ++j) {
+            const TriRec& r = recs[j];
+            float t;
+            if (mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx, r.tvy,
+                             r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
+                accept_t(t))
+                ++n;
+        }
+        float distance = 0.0f;
+        if (n % 2 == 0) {
+            uint64_t pos = 0;
+            float prev = -__builtin_inff();
+            bool first = true;
+            float pending = 0.0f;
+            while (pos < n) {
+                // next distinct value > prev (or >= -inf on the first pass) and its multiplicity
+                float cur = __builtin_inff();
+                uint64_t mult = 0;
+                for (uint32_t j = 0; j < T; ++j) {
+                    const TriRec& r = recs[j];
+                    float t;
+                    if (mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx,
+                                     r.tvy, r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
+                        accept_t(t) && (first || t > prev)) {
+                        if (t < cur) {
+                            cur = t;
+                            mult = 1;
+                        } else if (t == cur) {
+                            ++mult;
+                        }
+                    }
+                }
+                if (mult == 0) break;   // cannot happen; keeps the loop bounded
+                for (uint64_t q = 0; q < mult && pos < n; ++q, ++pos) {
+                    if ((pos & 1) == 0) pending = cur;
+                    else distance += cur - pending;
+                }
+                prev = cur;
+                first = false;
+            }
+        }
+        float photon = shade(distance);
+        if (out.image) out.image[o] = photon;
+        if (out.lbuffer) out.lbuffer[o] = distance;   // n > capacity >= 1, so the ray hit
+        if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Probes
+// ---------------------------------------------------------------------------
+__global__ void k_probe_intersect(const float* __restrict__ rays, const float* __restrict__ tris,
+                                  uint64_t n, uint8_t* __restrict__ hit, float* __restrict__ tout)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* R = rays + 6 * i;
+    const float* P = tris + 9 * i;
+    // The ray origin and the Ray ctor's re-normalisation (Ray.inl:80-84).
+    float ox = R[0], oy = R[1], oz = R[2];
+    float X = R[3], Y = R[4], Z = R[5];
+    float len = sqrtf((X * X + Y * Y) + Z * Z);
+    float dx = 0.0f, dy = 0.0f, dz = 0.0f;
+    if (len != 0.0f) {
+        dx = X / len;
+        dy = Y / len;
+        dz = Z / len;
+    }
+    float e1x = P[3] - P[0], e1y = P[4] - P[1], e1z = P[5] - P[2];
+    float e2x = P[6] - P[0], e2y = P[7] - P[1], e2z = P[8] - P[2];
+    float tvx = ox - P[0], tvy = oy - P[1], tvz = oz - P[2];
+    float qvx = tvy * e1z - tvz * e1y;
+    float qvy = tvz * e1x - tvx * e1z;
+    float qvz = tvx * e1y - tvy * e1x;
+    float tnum = (e2x * qvx + e2y * qvy) + e2z * qvz;
+    float t = 0.0f;
+    bool h = mt_intersect(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tvx, tvy, tvz, qvx, qvy, qvz,
+                          tnum, t);
+    hit[i] = h ? 1 : 0;
+    tout[i] = h ? t : 0.0f;
+}
+
+__global__ void k_probe_math(int op, const float* __restrict__ in, float* __restrict__ outp,
+                             uint64_t n)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x = in[i];
+    float y;
+    switch (op) {
+    case 0: y = xrt_expf(x); break;
+    case 1: y = sqrtf(x); break;
+    case 2: y = (float)(1.0 / (double)x); break;
+    default: y = (float)lut_u8(x); break;
+    }
+    outp[i] = y;
+}
+
+}  // namespace xrt

@@ -1,0 +1,536 @@
+// xrt_abi.hip -- the C ABI of include/xrt.h: device/context management,
+// launches and the host-side camera arithmetic.  Built into libxrt.so by
+// simpleraytracing_amd/csrc/Makefile (hipcc --offload-arch=gfx950).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/xrt.h"
+#include "kernels/xrt_kernels.h"
+
+using namespace xrt;
+
+struct xrt_context {
+    int device = 0;
+    std::string error;
+
+    float* d_tris = nullptr;       // raw triangle soup, 9 f32 per triangle
+    uint64_t num_tris = 0;
+    size_t tris_cap = 0;
+
+    TriRec* d_recs = nullptr;      // per-render records
+    size_t recs_cap = 0;
+    float4* d_cull = nullptr;      // per-render cull planes (4 x T float4)
+    size_t cull_cap = 0;
+
+    DevStats* d_stats = nullptr;
+    uint32_t* d_overflow = nullptr;
+    size_t overflow_cap = 0;
+
+    // staging for the host-pointer entry point
+    float* d_image = nullptr;
+    float* d_lbuffer = nullptr;
+    uint8_t* d_u8 = nullptr;
+    size_t stage_cap = 0;
+
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    // region timing (xrt_timing_begin/end)
+    bool timing = false;
+    std::vector<hipEvent_t> tev;      // pairs: [2i] before, [2i+1] after the main kernel
+    size_t tev_used = 0;
+    hipStream_t last_stream = nullptr;
+    bool pending = false;
+    int kernel = XRT_KERNEL_AUTO;
+    int last_kernel = XRT_KERNEL_TILED;
+    uint32_t hit_capacity = kMaxHits;
+};
+
+static std::string g_create_error;
+
+namespace {
+
+int fail(xrt_context* ctx, int code, const std::string& msg)
+{
+    if (ctx) ctx->error = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+#define XRT_HIP(ctx, expr)                                                                    \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail((ctx), XRT_ERR_DEVICE,                                                \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+    } while (0)
+
+template <typename T>
+int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
+{
+    if (need_elems <= cap && ptr) return XRT_OK;
+    if (ptr) {
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    size_t n = std::max<size_t>(need_elems, 1);
+    XRT_HIP(ctx, hipMalloc(&ptr, n * sizeof(T)));
+    cap = n;
+    return XRT_OK;
+}
+
+// The reference's stdmin / stdmax semantics (std::min(a,b) = b<a ? b : a).
+inline float stdmin(float a, float b) { return (b < a) ? b : a; }
+inline float stdmax(float a, float b) { return (a < b) ? b : a; }
+
+inline void cross3(const float a[3], const float b[3], float o[3])
+{
+    float x = a[1] * b[2] - a[2] * b[1];
+    float y = a[2] * b[0] - a[0] * b[2];
+    float z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+}
+
+inline float length3(const float a[3]) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+
+inline void normalise3(float a[3])
+{
+    float len = length3(a);
+    a[0] /= len;
+    a[1] /= len;
+    a[2] /= len;
+}
+
+RenderParams make_params(const xrt_camera& c, uint32_t row_begin, uint32_t row_end, uint64_t T,
+                         uint32_t capacity)
+{
+    RenderParams p;
+    p.ox = c.origin[0]; p.oy = c.origin[1]; p.oz = c.origin[2];
+    p.cx = c.detector[0]; p.cy = c.detector[1]; p.cz = c.detector[2];
+    p.ux = c.up[0]; p.uy = c.up[1]; p.uz = c.up[2];
+    p.rx = c.right[0]; p.ry = c.right[1]; p.rz = c.right[2];
+    p.spacing = c.pixel_spacing;
+    p.width = c.width;
+    p.height = c.height;
+    p.row_begin = row_begin;
+    p.row_end = row_end;
+    p.num_triangles = (uint32_t)T;
+    p.hit_capacity = capacity;
+    return p;
+}
+
+// Bounds used by the cull derivation (DESIGN.md "Tile cull"): over every pixel
+// of the image, |D| <= dmax and the terms summed into D are <= mag.
+CullParams make_cull_params(const xrt_camera& c)
+{
+    double ps = std::fabs((double)c.pixel_spacing);
+    double vmax = ps * ((double)c.height / 2.0 + 1.0);
+    double umax = ps * ((double)c.width / 2.0 + 1.0);
+    double d2 = 0.0, mag = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        double cterm = std::fabs((double)c.detector[k] - (double)c.origin[k]);
+        double spread = std::fabs((double)c.up[k]) * vmax + std::fabs((double)c.right[k]) * umax;
+        d2 += (cterm + spread) * (cterm + spread);
+        mag = std::max(mag, std::fabs((double)c.detector[k]) + spread + std::fabs((double)c.origin[k]));
+    }
+    CullParams cp;
+    cp.dmax = std::sqrt(d2) * (1.0 + 1e-6);
+    cp.mag = mag;
+    cp.width = c.width;
+    cp.height = c.height;
+    return cp;
+}
+
+int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end)
+{
+    if (!cam) return fail(ctx, XRT_ERR_ARGUMENT, "camera is NULL");
+    if (cam->width == 0 || cam->height == 0)
+        return fail(ctx, XRT_ERR_ARGUMENT, "image size must be non-zero");
+    if (row_begin > row_end || row_end > cam->height)
+        return fail(ctx, XRT_ERR_ARGUMENT,
+                    "row range [" + std::to_string(row_begin) + ", " + std::to_string(row_end) +
+                        ") outside image height " + std::to_string(cam->height));
+    if ((uint64_t)cam->width * cam->height > (1ull << 32) - 1)
+        return fail(ctx, XRT_ERR_ARGUMENT, "image larger than 2^32-1 pixels");
+    return XRT_OK;
+}
+
+int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
+                   float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream)
+{
+    int rc = check_camera(ctx, cam, row_begin, row_end);
+    if (rc) return rc;
+    if (!ctx->d_tris && ctx->num_tris) return fail(ctx, XRT_ERR_NO_MESH, "no mesh uploaded");
+    if (ctx->num_tris > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many triangles");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+
+    const uint64_t T = ctx->num_tris;
+    const uint32_t rows = row_end - row_begin;
+    const uint64_t rays = (uint64_t)rows * cam->width;
+    const int kernel = ctx->kernel == XRT_KERNEL_BRUTE ? XRT_KERNEL_BRUTE : XRT_KERNEL_TILED;
+
+    if ((rc = ensure(ctx, ctx->d_recs, ctx->recs_cap, T))) return rc;
+    if (kernel == XRT_KERNEL_TILED &&
+        (rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes)))
+        return rc;
+    if ((rc = ensure(ctx, ctx->d_overflow, ctx->overflow_cap, rays))) return rc;
+
+    RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
+    CullParams cp = make_cull_params(*cam);
+    Outputs out;
+    out.image = d_image;
+    out.lbuffer = d_lbuffer;
+    out.image_u8 = d_u8;
+    out.overflow_list = ctx->d_overflow;
+    out.stats = ctx->d_stats;
+
+    XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
+    if (T) {
+        dim3 pg((unsigned)((T + 255) / 256));
+        hipLaunchKernelGGL(k_prep, pg, dim3(256), 0, stream, ctx->d_tris, (uint32_t)T, p, cp,
+                           ctx->d_recs, kernel == XRT_KERNEL_TILED ? ctx->d_cull : nullptr);
+        XRT_HIP(ctx, hipGetLastError());
+    }
+    hipEvent_t t0 = ctx->ev_begin, t1 = ctx->ev_end;
+    if (ctx->timing) {
+        if (ctx->tev_used + 2 > ctx->tev.size()) {
+            for (int k = 0; k < 256; ++k) {
+                hipEvent_t e;
+                XRT_HIP(ctx, hipEventCreate(&e));
+                ctx->tev.push_back(e);
+            }
+        }
+        t0 = ctx->tev[ctx->tev_used];
+        t1 = ctx->tev[ctx->tev_used + 1];
+        ctx->tev_used += 2;
+    }
+    if (ctx->timing) XRT_HIP(ctx, hipEventRecord(ctx->ev_begin, stream));
+    XRT_HIP(ctx, hipEventRecord(t0, stream));
+    if (rows > 0) {
+        if (kernel == XRT_KERNEL_BRUTE) {
+            dim3 grid((cam->width + 15) / 16, (rows + 15) / 16);
+            hipLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, ctx->d_recs, p, out);
+        } else {
+            dim3 grid((cam->width + kRegion - 1) / kRegion, (rows + kRegion - 1) / kRegion);
+            hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs,
+                               ctx->d_cull, p, out);
+        }
+        XRT_HIP(ctx, hipGetLastError());
+    }
+    XRT_HIP(ctx, hipEventRecord(t1, stream));
+    if (ctx->timing) XRT_HIP(ctx, hipEventRecord(ctx->ev_end, stream));
+    if (rows > 0) {
+        hipLaunchKernelGGL(k_overflow, dim3(256), dim3(64), 0, stream, ctx->d_recs, p, out);
+        XRT_HIP(ctx, hipGetLastError());
+    }
+    ctx->last_stream = stream;
+    ctx->pending = true;
+    ctx->last_kernel = kernel;
+    return XRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xrt_abi_version(void) { return XRT_ABI_VERSION; }
+
+int xrt_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int xrt_create(int device, xrt_context** out)
+{
+    if (!out) return fail(nullptr, XRT_ERR_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(nullptr, XRT_ERR_DEVICE,
+                    std::string("no HIP device available: ") + hipGetErrorString(e));
+    if (device < 0 || device >= n)
+        return fail(nullptr, XRT_ERR_ARGUMENT, "device index out of range");
+    if ((e = hipSetDevice(device)) != hipSuccess)
+        return fail(nullptr, XRT_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    xrt_context* ctx = new xrt_context();
+    ctx->device = device;
+    if (hipMalloc(&ctx->d_stats, sizeof(DevStats)) != hipSuccess ||
+        hipEventCreate(&ctx->ev_begin) != hipSuccess || hipEventCreate(&ctx->ev_end) != hipSuccess) {
+        xrt_destroy(ctx);
+        return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
+    }
+    *out = ctx;
+    return XRT_OK;
+}
+
+void xrt_destroy(xrt_context* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ctx->d_tris);
+    (void)hipFree(ctx->d_recs);
+    (void)hipFree(ctx->d_cull);
+    (void)hipFree(ctx->d_stats);
+    (void)hipFree(ctx->d_overflow);
+    (void)hipFree(ctx->d_image);
+    (void)hipFree(ctx->d_lbuffer);
+    (void)hipFree(ctx->d_u8);
+    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+    if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
+    if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+    delete ctx;
+}
+
+const char* xrt_last_error(const xrt_context* ctx)
+{
+    return ctx ? ctx->error.c_str() : g_create_error.c_str();
+}
+
+int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_triangles)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (num_triangles && !triangles) return fail(ctx, XRT_ERR_ARGUMENT, "triangles is NULL");
+    if (num_triangles > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many triangles");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = ensure(ctx, ctx->d_tris, ctx->tris_cap, 9 * num_triangles);
+    if (rc) return rc;
+    if (num_triangles)
+        XRT_HIP(ctx, hipMemcpy(ctx->d_tris, triangles, 9 * num_triangles * sizeof(float),
+                               hipMemcpyHostToDevice));
+    ctx->num_tris = num_triangles;
+    return XRT_OK;
+}
+
+int xrt_mesh_bbox(const float* tris, uint64_t n, float lower[3], float upper[3])
+{
+    if ((n && !tris) || !lower || !upper) return XRT_ERR_ARGUMENT;
+    const float inf = std::numeric_limits<float>::infinity();
+    for (int k = 0; k < 3; ++k) {
+        lower[k] = inf;
+        upper[k] = -inf;
+    }
+    // TriangleMesh::computeBoundingBox, src/TriangleMesh.cxx:200-227 (p1, p2, p3 in turn)
+    for (uint64_t i = 0; i < n; ++i)
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) {
+                float x = tris[9 * i + 3 * v + k];
+                lower[k] = stdmin(lower[k], x);
+                upper[k] = stdmax(upper[k], x);
+            }
+    return XRT_OK;
+}
+
+int xrt_camera_from_bbox(const float lower[3], const float upper[3], uint32_t width,
+                         uint32_t height, xrt_camera* out)
+{
+    if (!lower || !upper || !out || !width || !height) return XRT_ERR_ARGUMENT;
+    // initialiseRayTracing, src/main.cxx:575-604
+    float range[3] = {upper[0] - lower[0], upper[1] - lower[1], upper[2] - lower[2]};
+    float centre[3];
+    for (int k = 0; k < 3; ++k) centre[k] = lower[k] + (float)((double)range[k] / 2.0);
+    float diagonal = length3(range);
+    float up[3] = {0.0f, 0.0f, -1.0f};
+    float origin[3] = {centre[0] - diagonal * 1, centre[1] - 0.0f, centre[2] - 0.0f};
+    float xoff = (float)((double)diagonal * 0.6);
+    float detector[3] = {centre[0] + xoff, centre[1] + 0.0f, centre[2] + 0.0f};
+    float direction[3] = {detector[0] - origin[0], detector[1] - origin[1], detector[2] - origin[2]};
+    normalise3(direction);
+    normalise3(direction);
+    float right[3];
+    cross3(direction, up, right);
+    // renderLoop prologue, src/main.cxx:637-641
+    float res1 = range[2] / (float)width;
+    float res2 = range[1] / (float)height;
+    float spacing = 2 * stdmax(res1, res2);
+    std::memcpy(out->origin, origin, sizeof origin);
+    std::memcpy(out->detector, detector, sizeof detector);
+    std::memcpy(out->up, up, sizeof up);
+    std::memcpy(out->right, right, sizeof right);
+    out->pixel_spacing = spacing;
+    out->width = width;
+    out->height = height;
+    return XRT_OK;
+}
+
+int xrt_set_kernel(xrt_context* ctx, int kernel)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (kernel < XRT_KERNEL_AUTO || kernel > XRT_KERNEL_TILED)
+        return fail(ctx, XRT_ERR_ARGUMENT, "unknown kernel");
+    ctx->kernel = kernel;
+    return XRT_OK;
+}
+
+int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (capacity > (uint32_t)kMaxHits) return fail(ctx, XRT_ERR_ARGUMENT, "capacity > 16");
+    ctx->hit_capacity = capacity ? capacity : (uint32_t)kMaxHits;
+    return XRT_OK;
+}
+
+int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
+                           uint32_t row_end, float* d_image, float* d_lbuffer, uint8_t* d_u8,
+                           void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    return enqueue_render(ctx, camera, row_begin, row_end, d_image, d_lbuffer, d_u8,
+                          (hipStream_t)stream);
+}
+
+int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
+{
+    if (!ctx || !stats) return XRT_ERR_ARGUMENT;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    if (ctx->pending) {
+        XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+        ctx->pending = false;
+    }
+    DevStats s;
+    XRT_HIP(ctx, hipMemcpy(&s, ctx->d_stats, sizeof s, hipMemcpyDeviceToHost));
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end) != hipSuccess) ms = 0.0f;
+    stats->rays = s.rays;
+    stats->hit_rays = s.hit_rays;
+    stats->odd_rays = s.odd_rays;
+    stats->overflow_rays = s.overflow_rays;
+    stats->hits = s.hits;
+    stats->max_hits = s.max_hits;
+    stats->kernel = (uint32_t)ctx->last_kernel;
+    stats->kernel_ms = ms;
+    return XRT_OK;
+}
+
+int xrt_timing_begin(xrt_context* ctx)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    ctx->timing = true;
+    ctx->tev_used = 0;
+    return XRT_OK;
+}
+
+int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches)
+{
+    if (!ctx || !total_ms || !launches) return XRT_ERR_ARGUMENT;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    double sum = 0.0;
+    for (size_t i = 0; i + 1 < ctx->tev_used; i += 2) {
+        XRT_HIP(ctx, hipEventSynchronize(ctx->tev[i + 1]));
+        float ms = 0.0f;
+        XRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->tev[i], ctx->tev[i + 1]));
+        sum += ms;
+    }
+    *total_ms = sum;
+    *launches = ctx->tev_used / 2;
+    ctx->timing = false;
+    ctx->tev_used = 0;
+    return XRT_OK;
+}
+
+int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
+                    uint32_t row_end, float* image, float* lbuffer, uint8_t* image_u8,
+                    xrt_stats* stats)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    int rc = check_camera(ctx, camera, row_begin, row_end);
+    if (rc) return rc;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)(row_end - row_begin) * camera->width;
+    size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
+    if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
+    ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
+    rc = enqueue_render(ctx, camera, row_begin, row_end, image ? ctx->d_image : nullptr,
+                        lbuffer ? ctx->d_lbuffer : nullptr, image_u8 ? ctx->d_u8 : nullptr, nullptr);
+    if (rc) return rc;
+    if (n) {
+        if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (lbuffer)
+            XRT_HIP(ctx, hipMemcpy(lbuffer, ctx->d_lbuffer, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
+    }
+    xrt_stats local;
+    rc = xrt_read_stats(ctx, stats ? stats : &local);
+    return rc;
+}
+
+int xrt_probe_intersect(xrt_context* ctx, const float* rays, const float* tris, uint64_t n,
+                        uint8_t* hit, float* t)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (n == 0) return XRT_OK;
+    if (!rays || !tris || !hit || !t) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    float *dr = nullptr, *dt = nullptr, *dout = nullptr;
+    uint8_t* dh = nullptr;
+    int rc = XRT_OK;
+    if (hipMalloc(&dr, n * 6 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&dt, n * 9 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&dout, n * sizeof(float)) != hipSuccess || hipMalloc(&dh, n) != hipSuccess) {
+        rc = fail(ctx, XRT_ERR_DEVICE, "probe allocation failed");
+    } else if (hipMemcpy(dr, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(dt, tris, n * 9 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(ctx, XRT_ERR_DEVICE, "probe upload failed");
+    } else {
+        hipLaunchKernelGGL(k_probe_intersect, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dr,
+                           dt, n, dh, dout);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpy(hit, dh, n, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(t, dout, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(ctx, XRT_ERR_DEVICE, "probe kernel failed");
+    }
+    (void)hipFree(dr);
+    (void)hipFree(dt);
+    (void)hipFree(dout);
+    (void)hipFree(dh);
+    return rc;
+}
+
+int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* outp, uint64_t n)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (op < XRT_PROBE_EXPF || op > XRT_PROBE_LUT_U8) return fail(ctx, XRT_ERR_ARGUMENT, "bad op");
+    if (n == 0) return XRT_OK;
+    if (!in || !outp) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    float *di = nullptr, *dout = nullptr;
+    int rc = XRT_OK;
+    if (hipMalloc(&di, n * sizeof(float)) != hipSuccess ||
+        hipMalloc(&dout, n * sizeof(float)) != hipSuccess) {
+        rc = fail(ctx, XRT_ERR_DEVICE, "probe allocation failed");
+    } else if (hipMemcpy(di, in, n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(ctx, XRT_ERR_DEVICE, "probe upload failed");
+    } else {
+        hipLaunchKernelGGL(k_probe_math, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, di,
+                           dout, n);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpy(outp, dout, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(ctx, XRT_ERR_DEVICE, "probe kernel failed");
+    }
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    return rc;
+}
+
+// Host evaluation of the device expf restatement (same source, host-compiled);
+// lets the CPU test suite check it exhaustively against libm without a GPU.
+void xrt_host_expf_batch(const float* in, float* outp, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) outp[i] = xrt_expf(in[i]);
+}
+
+}  // extern "C"

@@ -1,0 +1,132 @@
+"""CPU: the C-ABI libraries load, export every declared symbol, and their
+host-side arithmetic (bbox, camera, PLY ingestion, expf restatement) is
+bit-identical to the oracle.  No compute call touches a GPU here."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import simpleraytracing_amd as xrt
+from simpleraytracing_amd import _abi
+from oracle import oracle
+from conftest import DRAGON, ROOT, bits
+
+
+def declared_functions(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = text.split("#ifdef __cplusplus\n}")[0]        # C part only
+    return sorted(set(re.findall(r"\b(xrt_\w+)\s*\(", text)) - {"xrt_status"})
+
+
+def test_libxrt_exports_every_declared_symbol():
+    lib = _abi.load()
+    names = declared_functions("xrt.h")
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _abi.XRT_SYMBOLS, f"{n} declared in xrt.h but not bound in _abi.py"
+
+
+def test_libxrt_host_exports_every_declared_symbol():
+    host = _abi.load_host()
+    for n in declared_functions("xrt_host.h"):
+        assert hasattr(host, n), n
+
+
+def test_abi_version():
+    assert _abi.load().xrt_abi_version() == 1
+
+
+def test_create_without_gpu_fails_cleanly():
+    if xrt.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(xrt.XrtError) as e:
+        xrt.Context(0)
+    assert e.value.code == _abi.XRT_ERR_DEVICE
+
+
+def test_load_ply_matches_oracle(dragon):
+    soup = xrt.load_ply(DRAGON)
+    assert soup.shape == dragon.shape
+    assert np.array_equal(bits(soup), bits(dragon))
+
+
+def test_load_ply_errors(tmp_path):
+    with pytest.raises(xrt.XrtError) as e:
+        xrt.load_ply(str(tmp_path / "missing.ply"))
+    assert e.value.code == _abi.XRT_ERR_IO
+    bad = tmp_path / "bad.ply"
+    bad.write_bytes(b"ply\nformat binary_little_endian 1.0\nelement vertex 3\nproperty float x\nend_header\n")
+    with pytest.raises(xrt.XrtError):
+        xrt.load_ply(str(bad))
+
+
+def test_ascii_ply_and_quads(tmp_path):
+    p = tmp_path / "quad.ply"
+    p.write_text("ply\nformat ascii 1.0\nelement vertex 4\nproperty float x\nproperty float y\n"
+                 "property float z\nelement face 1\nproperty list uchar int vertex_indices\nend_header\n"
+                 "0 0 0\n1 0 0\n1 1 0\n0 1 0\n4 0 1 2 3\n")
+    soup = xrt.load_ply(str(p))
+    ref = oracle.load_ply(str(p))
+    assert soup.shape == (2, 9)
+    assert np.array_equal(soup, ref)
+
+
+def test_bbox_and_camera_match_oracle(dragon):
+    lo, hi = xrt.mesh_bbox(dragon)
+    lo2, hi2 = oracle.bbox(dragon)
+    assert np.array_equal(bits(lo), bits(lo2)) and np.array_equal(bits(hi), bits(hi2))
+    for (w, h) in [(128, 128), (2048, 2048), (4096, 4096), (8192, 8192), (640, 480), (3, 1000)]:
+        cam = xrt.camera_from_bbox(lo, hi, w, h)
+        c13 = oracle.camera(lo, hi, w, h)
+        got = np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) +
+                       [cam.pixel_spacing], np.float32)
+        assert np.array_equal(bits(got), bits(c13)), (w, h)
+        assert (cam.width, cam.height) == (w, h)
+
+
+def test_dragon_2048_camera_values(dragon):
+    # dragon 2048^2 camera
+    cam = xrt.camera_for_mesh(dragon, 2048, 2048)
+    assert np.float32(cam.pixel_spacing) == np.float32(0.151470721)
+    assert np.allclose(list(cam.origin), [-220.841003, -671.790405, 298.21048])
+    assert np.allclose(list(cam.detector), [115.792053, -671.790405, 298.21048])
+    assert list(cam.right)[1] == 1.0
+
+
+def test_host_expf_restatement_matches_libm():
+    """The device expf source (host-compiled) vs glibc expf: all floats in
+    [-0.5, 0] and a stride over [-104, 89] plus specials."""
+    lib = _abi.load()
+    ui = np.arange(0x80000000, 0xBF000001, 3, dtype=np.uint64).astype(np.uint32)   # -0 .. -0.5
+    x = np.concatenate([
+        ui.view(np.float32),
+        np.arange(0xBF000000, 0xC2D00000, 97, dtype=np.uint64).astype(np.uint32).view(np.float32),
+        np.arange(0x00000000, 0x42B20000, 997, dtype=np.uint64).astype(np.uint32).view(np.float32),
+        np.array([np.inf, -np.inf, np.nan, 88.0, 88.8, -103.9, -104.0, -1e-45, 1e-45, 0.0, -0.0],
+                 np.float32)])
+    got = np.empty_like(x)
+    lib.xrt_host_expf_batch(x.ctypes.data_as(_abi._fp), got.ctypes.data_as(_abi._fp), x.size)
+    want = oracle.expf(x)
+    same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), x[~same][:10]
+
+
+def test_cli_help_and_bad_option():
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and "--size" in r.stderr
+    r = subprocess.run([exe, "--bogus"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Usage" in r.stderr
+
+
+def test_cli_without_gpu_reports_error(tmp_path):
+    if xrt.device_count() > 0:
+        pytest.skip("a GPU is present")
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    r = subprocess.run([exe, "-s", "8", "8", "-i", DRAGON, "-f", "x.txt"], capture_output=True,
+                       text=True, cwd=tmp_path)
+    assert r.returncode == 1 and r.stderr.startswith("ERROR:")
