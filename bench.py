@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the X-ray render path (BASELINE.json metric).
+
+One step = one full frame of the configured size (default dragon.ply,
+2048x2048): every rank renders its contiguous row strip (rows_per = H/N,
+remainder to the first strips, as main-pthreads-rows.cxx:311-334 splits work)
+on its GPU, and for N > 1 the strips (f32 image, f32 L-buffer, u8 image) are
+gathered to rank 0 with one RCCL gather over xGMI.  The mesh is resident in HBM
+before the timed region; the per-frame triangle preparation (k_prep), the
+render kernel, the overflow fix-up and the gather are all inside it.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size W H]
+                    [--kernel tiled|brute] [--tile-mesh n] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BYTES_PER_TEST = 36            # 9 f32 vertex operands per ray-triangle test
+BYTES_OUT_PER_RAY = 9          # L f32 + image f32 + u8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, nargs=2, default=[2048, 2048], metavar=("W", "H"))
+    ap.add_argument("--kernel", choices=["tiled", "brute"], default="tiled")
+    ap.add_argument("--mesh", default=os.path.join(ROOT, "data", "dragon.ply"))
+    ap.add_argument("--tile-mesh", type=int, default=1,
+                    help="n x n tiled copies of the mesh (7 = the 1M-triangle config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU time of the bounded cpu_baseline sample")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 PMC runs (see DESIGN.md)")
+    return ap.parse_args()
+
+
+def cpu_baseline(tris, W, H, budget_s, gpu_rows):
+    """The oracle (a restatement of main.cxx's serial loop, threaded over pixel
+    blocks like main-pthreads-redo.cxx) timed on a bounded row sample of the same
+    frame; also checks those rows against the GPU frame."""
+    import numpy as np
+
+    from oracle import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 64))
+    cam = oracle.camera_for_mesh(tris, W, H)
+    # serial rate on a span of one row (the reference main.cxx is single-threaded),
+    # sized to about 1 s
+    mid = H // 2
+    span = int(max(8, min(W, 6.0e7 / max(len(tris), 1))))
+    c0 = (W - span) // 2
+    t0 = time.perf_counter()
+    oracle.render_span(tris, cam, W, H, mid, c0, c0 + span, threads=1)
+    serial_s = time.perf_counter() - t0
+    serial_rate = span / serial_s
+    # threaded sample sized to the budget
+    est_rate = serial_rate * threads
+    nrows = int(max(1, min(H, budget_s * est_rate / W)))
+    rows = np.unique(np.linspace(0, H - 1, nrows).astype(np.uint32))
+    t0 = time.perf_counter()
+    img, lb, u8, nh, odd = oracle.render_row_list(tris, cam, W, H, rows, threads=threads)
+    dt = time.perf_counter() - t0
+    g_img, g_lb, g_u8 = gpu_rows
+    parity = bool(np.array_equal(img.view(np.uint32), g_img.reshape(H, W)[rows].ravel().view(np.uint32))
+                  and np.array_equal(lb.view(np.uint32), g_lb.reshape(H, W)[rows].ravel().view(np.uint32))
+                  and np.array_equal(u8, g_u8.reshape(H, W)[rows].ravel()))
+    return {
+        "value": len(rows) * W / dt / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(rows)} rows x {W} px of the same {W}x{H} frame ({len(rows) * W} rays, "
+                  f"{dt:.1f} s), oracle/xrt_oracle.c threaded over 64-px blocks",
+        "serial_value": serial_rate / 1e6,
+        "serial_sample": f"{span} rays of row {mid}, 1 thread ({serial_s:.2f} s)",
+        "sample_bit_exact_vs_gpu": parity,
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import simpleraytracing_amd as xrt
+    from simpleraytracing_amd.scenes import tiled_mesh
+    from simpleraytracing_amd.strips import max_strip_pixels, strip_bounds, views
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H = args.size
+    tris = xrt.load_ply(args.mesh)
+    if args.tile_mesh > 1:
+        tris = tiled_mesh(tris, args.tile_mesh)
+    T = len(tris)
+    cam = xrt.camera_for_mesh(tris, W, H)
+    r0, r1 = strip_bounds(H, world, rank)
+    n_max = max_strip_pixels(W, H, world)
+
+    ctx = xrt.Context(local_rank)
+    ctx.set_kernel(xrt.XRT_KERNEL_BRUTE if args.kernel == "brute" else xrt.XRT_KERNEL_TILED)
+    ctx.upload_mesh(tris)
+
+    # one packed strip buffer: [image f32 | L-buffer f32 | u8], gathered in one collective
+    strip = torch.zeros(9 * n_max, dtype=torch.uint8, device=dev)
+    img, lb, u8 = views(strip, n_max)
+    gathered = [torch.empty_like(strip) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.render_rows_device(cam, r0, r1, img.data_ptr(), lb.data_ptr(), u8.data_ptr(),
+                               stream.cuda_stream)
+        if world > 1:
+            dist.gather(strip, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = ctx.timing_end()
+    stats = ctx.read_stats()
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    result = None
+    if rank == 0:
+        rays_total = W * H * args.steps
+        value = rays_total / elapsed_max / 1e6
+        rays_per_launch = (r1 - r0) * W
+        avg_kernel_s = kernel_ms / max(launches, 1) / 1e3
+        bytes_per_ray = BYTES_PER_TEST * T + BYTES_OUT_PER_RAY
+        achieved = rays_per_launch * bytes_per_ray / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+        workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
+                                                         if args.tile_mesh > 1 else "") + f" {W}x{H}"
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tr = json.load(f).get(f"{args.kernel}:{workload}:{world}")
+            if tr:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        result = {
+            "metric": "Mrays/s (dragon.ply render, whole job)",
+            "value": value,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "dragon.ply from the reference repo (deterministic mesh; no synthetic noise)"
+                    if args.tile_mesh == 1 else "tiled copies of dragon.ply (scenes.tiled_mesh)",
+            "config": {
+                "workload": workload,
+                "kernel": args.kernel,
+                "triangles": T,
+                "image": [W, H],
+                "rays_per_step": W * H,
+                "parallelism": f"row strips x{world}" + (", RCCL gather to rank 0" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_ray": bytes_per_ray,
+                "kernel": "k_render_tiled" if args.kernel == "tiled" else "k_render_brute",
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "launches": launches,
+            },
+            "render_stats": {
+                "hit_rays": stats.hit_rays, "odd_rays": stats.odd_rays, "max_hits": stats.max_hits,
+                "overflow_rays": stats.overflow_rays,
+            },
+            "cpu_baseline": None,
+        }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        full = ctx.render_rows(cam)     # the same frame, fetched to the host for the parity check
+        result["cpu_baseline"] = cpu_baseline(tris, W, H, args.cpu_seconds, full[:3])
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

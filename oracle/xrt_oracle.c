@@ -437,6 +437,7 @@ struct render_job {
     float* lbuffer;        /* may be NULL */
     uint8_t* image_u8;     /* may be NULL */
     int32_t* nhits;        /* may be NULL */
+    uint32_t col_begin, col_end;  /* columns rendered in every listed row */
     uint64_t next_unit;    /* work unit = 64 consecutive pixels of one row */
     uint64_t units_per_row;
     pthread_mutex_t lock;
@@ -524,9 +525,10 @@ static void* render_worker(void* arg)
         pthread_mutex_unlock(&job->lock);
         if (unit >= total) break;
         uint32_t i = (uint32_t)(unit / job->units_per_row);
-        uint32_t c0 = (uint32_t)(unit % job->units_per_row) * 64u;
-        uint32_t c1 = c0 + 64u < job->width ? c0 + 64u : job->width;
-        size_t base = (size_t)i * job->width;
+        uint32_t span = job->col_end - job->col_begin;
+        uint32_t c0 = job->col_begin + (uint32_t)(unit % job->units_per_row) * 64u;
+        uint32_t c1 = c0 + 64u < job->col_end ? c0 + 64u : job->col_end;
+        size_t base = (size_t)i * span - job->col_begin;
         for (uint32_t col = c0; col < c1; ++col) {
             size_t o = base + col;
             render_pixel(job, job->rows[i], col, &hits, &cap,
@@ -544,11 +546,13 @@ static void* render_worker(void* arg)
 }
 
 static int64_t render_list(const float* tris, uint64_t ntris, const float cam[13], uint32_t width,
-                           uint32_t height, const uint32_t* rows, uint32_t nrows, float* image,
+                           uint32_t height, const uint32_t* rows, uint32_t nrows,
+                           uint32_t col_begin, uint32_t col_end, float* image,
                            float* lbuffer, uint8_t* image_u8, int32_t* nhits, int nthreads)
 {
     for (uint32_t i = 0; i < nrows; ++i)
         if (rows[i] >= height) return -1;
+    if (col_begin > col_end || col_end > width) return -1;
     struct render_job job;
     memset(&job, 0, sizeof job);
     job.tris = tris;
@@ -562,7 +566,9 @@ static int64_t render_list(const float* tris, uint64_t ntris, const float cam[13
     job.lbuffer = lbuffer;
     job.image_u8 = image_u8;
     job.nhits = nhits;
-    job.units_per_row = (width + 63u) / 64u;
+    job.col_begin = col_begin;
+    job.col_end = col_end;
+    job.units_per_row = (col_end - col_begin + 63u) / 64u;
     pthread_mutex_init(&job.lock, NULL);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
@@ -589,8 +595,8 @@ int64_t orc_render_rows(const float* tris, uint64_t ntris, const float cam[13],
     uint32_t n = row_end - row_begin;
     uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
     for (uint32_t i = 0; i < n; ++i) rows[i] = row_begin + i;
-    int64_t odd = render_list(tris, ntris, cam, width, height, rows, n, image, lbuffer, image_u8,
-                              nhits, nthreads);
+    int64_t odd = render_list(tris, ntris, cam, width, height, rows, n, 0, width, image, lbuffer,
+                              image_u8, nhits, nthreads);
     free(rows);
     return odd;
 }
@@ -601,8 +607,18 @@ int64_t orc_render_row_list(const float* tris, uint64_t ntris, const float cam[1
                             uint32_t nrows, float* image, float* lbuffer,
                             uint8_t* image_u8, int32_t* nhits, int nthreads)
 {
-    return render_list(tris, ntris, cam, width, height, rows, nrows, image, lbuffer, image_u8,
-                       nhits, nthreads);
+    return render_list(tris, ntris, cam, width, height, rows, nrows, 0, width, image, lbuffer,
+                       image_u8, nhits, nthreads);
+}
+
+/* Columns [col_begin, col_end) of one row (bounded CPU timing samples). */
+int64_t orc_render_span(const float* tris, uint64_t ntris, const float cam[13], uint32_t width,
+                        uint32_t height, uint32_t row, uint32_t col_begin, uint32_t col_end,
+                        float* image, float* lbuffer, uint8_t* image_u8, int32_t* nhits,
+                        int nthreads)
+{
+    return render_list(tris, ntris, cam, width, height, &row, 1, col_begin, col_end, image,
+                       lbuffer, image_u8, nhits, nthreads);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -1,0 +1,304 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, the
+reference's golden text and size-independent properties.  Bit-exact on the
+f32 image, the f32 L-buffer and the 8-bit image (the north star's bar is
+bit-exact u8 and 1e-5 relative on the L-buffer; these tests demand 0 ULP)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import simpleraytracing_amd as xrt
+from simpleraytracing_amd import _abi
+from simpleraytracing_amd.scenes import tiled_mesh
+from oracle import oracle
+from conftest import DRAGON, GOLDEN, ROOT, bits
+from test_oracle import kat_vectors
+
+pytestmark = pytest.mark.gpu
+KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED]
+KNAME = {xrt.XRT_KERNEL_BRUTE: "brute", xrt.XRT_KERNEL_TILED: "tiled"}
+
+
+def cam13(cam):
+    return np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) +
+                    [cam.pixel_spacing], np.float32)
+
+
+def render(ctx, tris, W, H, kernel, r0=0, r1=None, cam=None):
+    ctx.set_kernel(kernel)
+    ctx.upload_mesh(tris)
+    cam = cam or xrt.camera_for_mesh(tris, W, H)
+    return ctx.render_rows(cam, r0, r1)
+
+
+def assert_same(gpu, ref, what=""):
+    img, lb, u8, st = gpu
+    rimg, rlb, ru8, rnh, rodd = ref
+    assert np.array_equal(bits(img), bits(rimg)), f"{what}: image differs at {np.nonzero(bits(img) != bits(rimg))[0][:8]}"
+    assert np.array_equal(bits(lb), bits(rlb)), f"{what}: L-buffer differs"
+    assert np.array_equal(u8, ru8), f"{what}: u8 differs"
+    assert st.odd_rays == rodd
+    assert st.hit_rays == int(np.count_nonzero(rnh))
+    assert st.hits == int(rnh.sum())
+    assert st.max_hits == (int(rnh.max()) if rnh.size else 0)
+
+
+# --------------------------------------------------------------------------- probes
+def test_probe_expf_matches_libm(ctx):
+    # every float in [-0.25, 0] plus strides over [-16, -0.25] and the full range
+    parts = [np.arange(0x80000000, 0xBE800001, 1, dtype=np.uint64),
+             np.arange(0xBE800000, 0xC1800000, 5, dtype=np.uint64),
+             np.arange(0xC1800000, 0xFF800001, 4099, dtype=np.uint64),
+             np.arange(0x00000000, 0x7F800001, 4099, dtype=np.uint64)]
+    for p in parts:
+        for c in range(0, p.size, 1 << 26):
+            x = p[c:c + (1 << 26)].astype(np.uint32).view(np.float32)
+            got = ctx.probe_math(_abi.XRT_PROBE_EXPF, x)
+            want = oracle.expf(x)
+            same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+            assert same.all(), x[~same][:8]
+
+
+def special_floats():
+    rng = np.random.default_rng(7)
+    r = rng.integers(0, 2**32, 1 << 22, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    den = rng.integers(1, 0x800000, 1 << 16, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, 2.0, 3.0, 1e-45, 1.17549435e-38,
+                   3.4028235e38, 0.5, 1e-38], np.float32)
+    return np.concatenate([r, den, -den, sp])
+
+
+def test_probe_sqrt_correctly_rounded(ctx):
+    x = np.abs(special_floats())
+    got = ctx.probe_math(_abi.XRT_PROBE_SQRTF, x)
+    want = np.sqrt(x)
+    same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), x[~same][:8]
+
+
+def test_probe_reciprocal_matches_double_division(ctx):
+    x = special_floats()
+    got = ctx.probe_math(_abi.XRT_PROBE_RCP, x)
+    with np.errstate(divide="ignore", over="ignore"):
+        want = (1.0 / x.astype(np.float64)).astype(np.float32)
+    same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), x[~same][:8]
+
+
+def test_probe_lut(ctx):
+    v = np.concatenate([np.linspace(-1, 81, 200001, dtype=np.float32),
+                        np.arange(0, 256, dtype=np.float32) * np.float32(80.0 / 255.0),
+                        (np.arange(0, 255, dtype=np.float64) + 0.5).astype(np.float32) * np.float32(80.0 / 255.0)])
+    got = ctx.probe_math(_abi.XRT_PROBE_LUT_U8, v)
+    want = np.array([oracle.lut_u8(float(a)) for a in v], np.float32)
+    assert np.array_equal(got, want)
+
+
+def test_probe_intersect_kat(ctx):
+    rays, tris = kat_vectors()
+    h1, t1 = ctx.probe_intersect(rays, tris)
+    h2, t2 = oracle.intersect_batch(rays, tris)
+    assert np.array_equal(h1, h2)
+    assert np.array_equal(bits(t1), bits(t2))
+
+
+# --------------------------------------------------------------------------- renders
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_golden_128(ctx, dragon, kernel):
+    """The reference's own golden, out/dragon-128x128-serial.txt, byte for byte."""
+    img, lb, u8, st = render(ctx, dragon, 128, 128, kernel)
+    want = open(os.path.join(GOLDEN, "dragon-128x128-serial.txt"), "rb").read()
+    assert oracle.text_bytes(img, 128, 128) == want
+    cam = oracle.camera_for_mesh(dragon, 128, 128)
+    assert_same((img, lb, u8, st), oracle.render_rows(dragon, cam, 128, 128), KNAME[kernel])
+    assert st.rays == 128 * 128 and st.kernel == kernel
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_full_256(ctx, dragon, kernel):
+    got = render(ctx, dragon, 256, 256, kernel)
+    cam = oracle.camera_for_mesh(dragon, 256, 256)
+    assert_same(got, oracle.render_rows(dragon, cam, 256, 256), KNAME[kernel])
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("W,H,r0,r1", [(1, 1, 0, 1), (7, 13, 0, 13), (33, 17, 0, 17), (100, 3, 0, 3),
+                                        (3, 100, 0, 100), (65, 65, 5, 50), (64, 64, 63, 64),
+                                        (97, 41, 40, 41), (50, 50, 20, 20)])
+def test_ragged_sizes_and_strips(ctx, dragon, kernel, W, H, r0, r1):
+    got = render(ctx, dragon, W, H, kernel, r0, r1)
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    assert_same(got, oracle.render_rows(dragon, cam, W, H, r0, r1), f"{KNAME[kernel]} {W}x{H}")
+
+
+def test_strips_assemble_to_full_image(ctx, dragon):
+    W = H = 160
+    full = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
+    for n in (2, 3, 8):
+        rows_per, rem = divmod(H, n)
+        parts, start = [], 0
+        for g in range(n):
+            end = start + rows_per + (1 if g < rem else 0)
+            parts.append(render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED, start, end)[0])
+            start = end
+        assert np.array_equal(bits(np.concatenate(parts)), bits(full[0]))
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_overflow_path_exact(ctx, dragon, kernel):
+    """Hit lists capped at 1 and 2 entries: the exact overflow kernel takes over."""
+    cam = oracle.camera_for_mesh(dragon, 96, 96)
+    ref = oracle.render_rows(dragon, cam, 96, 96)
+    for cap in (1, 2):
+        ctx.set_hit_capacity(cap)
+        try:
+            got = render(ctx, dragon, 96, 96, kernel)
+        finally:
+            ctx.set_hit_capacity(0)
+        assert got[3].overflow_rays == int(np.count_nonzero(ref[3] > cap))
+        assert_same(got, ref, f"{KNAME[kernel]} cap={cap}")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_empty_mesh(ctx, dragon, kernel):
+    cam = xrt.camera_for_mesh(dragon, 40, 30)
+    ctx.set_kernel(kernel)
+    ctx.upload_mesh(np.zeros((0, 9), np.float32))
+    img, lb, u8, st = ctx.render_rows(cam)
+    assert np.all(img == np.float32(80.0)) and np.all(np.isinf(lb)) and np.all(u8 == 255)
+    assert st.hits == 0
+
+
+def synthetic_soup(seed=11, n=3000):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-50, 50, (n, 1, 3))
+    t = (c + rng.normal(0, 6, (n, 3, 3))).astype(np.float32)
+    soup = t.reshape(n, 9)
+    k = n // 10
+    soup[:k, 6:9] = (soup[:k, 0:3] + 2 * (soup[:k, 3:6] - soup[:k, 0:3])).astype(np.float32)  # collinear
+    soup[k:2 * k] = soup[2 * k:3 * k]                                                    # duplicates (ties)
+    soup[3 * k:3 * k + 20, 3:6] = soup[3 * k:3 * k + 20, 0:3]                             # zero-length edge
+    return np.ascontiguousarray(soup)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_synthetic_soup_with_degenerates(ctx, kernel):
+    soup = synthetic_soup()
+    got = render(ctx, soup, 80, 72, kernel)
+    cam = oracle.camera_for_mesh(soup, 80, 72)
+    ref = oracle.render_rows(soup, cam, 80, 72)
+    assert ref[4] > 0      # odd rays occur (open soup)
+    assert_same(got, ref, KNAME[kernel])
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_custom_camera_triangles_around_source(ctx, kernel):
+    """Camera inside the scene: triangles behind, through and around the source."""
+    soup = synthetic_soup(seed=5, n=1500)
+    lo, hi = oracle.bbox(soup[:200])     # camera fitted to a sub-box: source lies inside the soup
+    cam = xrt.camera_from_bbox(lo, hi, 64, 48)
+    ctx.set_kernel(kernel)
+    ctx.upload_mesh(soup)
+    got = ctx.render_rows(cam)
+    ref = oracle.render_rows(soup, cam13(cam), 64, 48)
+    assert_same(got, ref, KNAME[kernel])
+
+
+def test_brute_equals_tiled_2048(ctx, dragon):
+    """Full 2048^2 frame: both kernels bit-identical; sampled rows vs the oracle;
+    SURVEY.md's dragon facts (hit rays, odd rays, max hits)."""
+    W = H = 2048
+    a = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
+    b = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BRUTE)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    st = a[3]
+    assert (st.hit_rays, st.odd_rays, st.max_hits) == (1365802, 24, 12)
+    rows = [0, 255, 256, 511, 512, 1023, 1024, 1535, 1536, 1792, 2047]
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    ref = oracle.render_row_list(dragon, cam, W, H, rows)
+    img = a[0].reshape(H, W)[rows].ravel()
+    lb = a[1].reshape(H, W)[rows].ravel()
+    u8 = a[2].reshape(H, W)[rows].ravel()
+    assert np.array_equal(bits(img), bits(ref[0]))
+    assert np.array_equal(bits(lb), bits(ref[1]))
+    assert np.array_equal(u8, ref[2])
+    # size-independent properties over the whole frame
+    miss = np.isinf(a[1])
+    assert np.all(a[0][miss] == np.float32(80.0)) and np.all(a[2][miss] == 255)
+    assert np.all(a[1][~miss] >= 0) and np.all(a[0] <= np.float32(80.0)) and np.all(a[0] > 0)
+
+
+def test_tiled_4096_rows_vs_oracle(ctx, dragon):
+    W = H = 4096
+    img, lb, u8, st = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
+    rows = [0, 511, 512, 2048, 3584, 4095]
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    ref = oracle.render_row_list(dragon, cam, W, H, rows)
+    assert np.array_equal(bits(img.reshape(H, W)[rows].ravel()), bits(ref[0]))
+    assert np.array_equal(bits(lb.reshape(H, W)[rows].ravel()), bits(ref[1]))
+
+
+def test_tiled_mesh_1m_parity(ctx, dragon):
+    """1,120,434-triangle tiled dragon: tiled == brute at 256^2, rows vs oracle."""
+    big = tiled_mesh(dragon, 7)
+    assert big.shape == (1120434, 9)
+    W = H = 256
+    a = render(ctx, big, W, H, xrt.XRT_KERNEL_TILED)
+    b = render(ctx, big, W, H, xrt.XRT_KERNEL_BRUTE)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    rows = [37, 128]
+    cam = oracle.camera_for_mesh(big, W, H)
+    ref = oracle.render_row_list(big, cam, W, H, rows)
+    assert np.array_equal(bits(a[0].reshape(H, W)[rows].ravel()), bits(ref[0]))
+    assert a[3].max_hits <= 16
+
+
+def test_device_buffers_and_timing(ctx, dragon):
+    """xrt_render_rows_device on torch-allocated device memory and a torch stream."""
+    import torch
+    W = H = 192
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    ctx.set_kernel(xrt.XRT_KERNEL_TILED)
+    ctx.upload_mesh(dragon)
+    dev = torch.device("cuda", ctx.device)
+    img = torch.empty(W * H, dtype=torch.float32, device=dev)
+    lb = torch.empty(W * H, dtype=torch.float32, device=dev)
+    u8 = torch.empty(W * H, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    ctx.timing_begin()
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            ctx.render_rows_device(cam, 0, H, img.data_ptr(), lb.data_ptr(), u8.data_ptr(),
+                                   stream.cuda_stream)
+    ms, launches = ctx.timing_end()
+    st = ctx.read_stats()
+    assert launches == 3 and ms > 0
+    ref = ctx.render_rows(cam)
+    assert np.array_equal(bits(img.cpu().numpy()), bits(ref[0]))
+    assert np.array_equal(u8.cpu().numpy(), ref[2])
+    assert st.rays == W * H
+
+
+def test_cli_golden_text(tmp_path):
+    """xrt_main (the reference's CLI over the GPU path) writes the golden text."""
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    (tmp_path / "out").mkdir()
+    for kernel in ("brute", "tiled"):
+        r = subprocess.run([exe, "-s", "128", "128", "-i", DRAGON, "-f", f"d-{kernel}.txt", "-k", kernel],
+                           capture_output=True, text=True, cwd=tmp_path, timeout=300)
+        assert r.returncode == 0, r.stderr
+        got = (tmp_path / "out" / f"d-{kernel}.txt").read_bytes()
+        assert got == open(os.path.join(GOLDEN, "dragon-128x128-serial.txt"), "rb").read()
+
+
+def test_cli_odd_ray_messages(tmp_path):
+    """The reference prints one line per odd-count ray (main.cxx:710): 24 at 2048^2."""
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    (tmp_path / "out").mkdir()
+    r = subprocess.run([exe, "-s", "2048", "2048", "-i", DRAGON, "-f", "d.txt"], capture_output=True,
+                       text=True, cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("Only one intersect on this ray") == 24
