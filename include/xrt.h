@@ -87,7 +87,9 @@ typedef struct xrt_stats {
     uint64_t hits;          /* total recorded intersections */
     uint32_t max_hits;      /* largest per-ray hit count */
     uint32_t kernel;        /* xrt_kernel actually used */
-    double kernel_ms;       /* device time of the render kernels (HIP events) */
+    double kernel_ms;       /* device time of the main render kernel (HIP events) */
+    uint64_t candidates;    /* TILED: triangles kept by the region footprint test, summed over regions */
+    uint64_t tile_tests;    /* triangle tests issued per 8x8 wave tile (64 ray-triangle tests each) */
 } xrt_stats;
 
 typedef struct xrt_context xrt_context;
@@ -180,6 +182,16 @@ typedef enum xrt_probe_op {
 
 /* Evaluates one scalar device function elementwise.  Host buffers. */
 int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* out, uint64_t n);
+
+/*
+ * Runs the per-render triangle preparation (k_prep) of the uploaded mesh for
+ * `camera` and copies its outputs to the host: records[16*i] = edge1, edge2,
+ * tvec, qvec, t*det, pad (the ray-independent terms of Ray::intersect,
+ * src/Ray.cxx:86-122) and footprint[16*i] = bbox (xmin, xmax, ymin, ymax) and
+ * the three relaxed edge functions (a, b, c, 0) of the tile cull.  Either
+ * output may be NULL.
+ */
+int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, float* footprint);
 
 /*
  * Host-side evaluation of the device expf restatement (the same source,

@@ -48,6 +48,9 @@ def lib():
         L.orc_render_span.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _F, _F, _U8,
                                       _I32, ctypes.c_int]
+        L.orc_hit_pairs.restype = ctypes.c_int64
+        L.orc_hit_pairs.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32, _U32,
+                                    ctypes.c_uint32, _U32, _U32, ctypes.c_uint64, ctypes.c_int]
         L.orc_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
         L.orc_save_text.argtypes = [_F, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
         L.orc_expf_batch.argtypes = [_F, _F, ctypes.c_uint64]
@@ -160,6 +163,21 @@ def render_span(tris, cam13, width, height, row, col_begin, col_end, threads=1):
     if odd < 0:
         raise ValueError("bad span")
     return img, lb, u8, nh, odd
+
+
+def hit_pairs(tris, cam13, width, height, rows, cap=1 << 24, threads=None):
+    """(pixel index within the row list, triangle index) of every hit with t > 1e-7."""
+    rows = np.ascontiguousarray(rows, np.uint32)
+    tris = np.ascontiguousarray(tris, np.float32)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    px = np.zeros(cap, np.uint32)
+    tr = np.zeros(cap, np.uint32)
+    n = lib().orc_hit_pairs(_fp(tris), len(tris), _fp(cam13), width, height, rows.ctypes.data_as(_U32),
+                            len(rows), px.ctypes.data_as(_U32), tr.ctypes.data_as(_U32), cap,
+                            threads or os.cpu_count() or 1)
+    if n > cap:
+        raise ValueError("capacity exceeded")
+    return px[:n], tr[:n]
 
 
 def intersect_batch(rays, tris):

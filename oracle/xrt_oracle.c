@@ -649,3 +649,91 @@ void orc_expf_batch(const float* in, float* out, uint64_t n)
 }
 
 uint8_t orc_lut_u8(float v) { return lut_u8(v); }
+
+/* ------------------------------------------------------------------------- */
+/* Hit pairs: every (pixel, triangle) whose Ray::intersect reports a hit with */
+/* t > 1e-7 (main.cxx:683-687), for the rows of a list.  Used to test that   */
+/* the GPU's conservative footprints contain every real hit.                 */
+/* ------------------------------------------------------------------------- */
+struct pairs_job {
+    const float* tris;
+    uint64_t ntris;
+    const float* cam;
+    uint32_t width, height;
+    const uint32_t* rows;
+    uint32_t nrows;
+    uint32_t* out_pixel;   /* (row index in list) * width + col */
+    uint32_t* out_tri;
+    uint64_t cap, count;
+    uint32_t next;
+    pthread_mutex_t lock;
+};
+
+static void* pairs_worker(void* arg)
+{
+    struct pairs_job* job = (struct pairs_job*)arg;
+    const float* cam = job->cam;
+    for (;;) {
+        pthread_mutex_lock(&job->lock);
+        uint32_t i = job->next++;
+        pthread_mutex_unlock(&job->lock);
+        if (i >= job->nrows) break;
+        uint32_t row = job->rows[i];
+        for (uint32_t col = 0; col < job->width; ++col) {
+            float v_offset = (float)((double)cam[12] * (0.5 + (double)row - (double)job->height / 2.0));
+            float u_offset = (float)((double)cam[12] * (0.5 + (double)col - (double)job->width / 2.0));
+            float dir[3];
+            for (int k = 0; k < 3; ++k)
+                dir[k] = ((cam[3 + k] + cam[6 + k] * v_offset) + cam[9 + k] * u_offset) - cam[k];
+            normalise3(dir);
+            float d[3] = {0.0f, 0.0f, 0.0f};
+            float len = length3(dir);
+            if (fpclassify(len) != FP_ZERO) {
+                d[0] = dir[0] / len;
+                d[1] = dir[1] / len;
+                d[2] = dir[2] / len;
+            }
+            for (uint64_t j = 0; j < job->ntris; ++j) {
+                const float* tr = job->tris + 9 * j;
+                float t;
+                if (orc_intersect(cam, d, tr, tr + 3, tr + 6, &t) && (double)t > 0.0000001) {
+                    pthread_mutex_lock(&job->lock);
+                    if (job->count < job->cap) {
+                        job->out_pixel[job->count] = i * job->width + col;
+                        job->out_tri[job->count] = (uint32_t)j;
+                    }
+                    ++job->count;
+                    pthread_mutex_unlock(&job->lock);
+                }
+            }
+        }
+    }
+    return NULL;
+}
+
+int64_t orc_hit_pairs(const float* tris, uint64_t ntris, const float cam[13], uint32_t width,
+                      uint32_t height, const uint32_t* rows, uint32_t nrows, uint32_t* out_pixel,
+                      uint32_t* out_tri, uint64_t cap, int nthreads)
+{
+    struct pairs_job job;
+    memset(&job, 0, sizeof job);
+    job.tris = tris;
+    job.ntris = ntris;
+    job.cam = cam;
+    job.width = width;
+    job.height = height;
+    job.rows = rows;
+    job.nrows = nrows;
+    job.out_pixel = out_pixel;
+    job.out_tri = out_tri;
+    job.cap = cap;
+    pthread_mutex_init(&job.lock, NULL);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int i = 1; i < nthreads; ++i) pthread_create(&th[i], NULL, pairs_worker, &job);
+    pairs_worker(&job);
+    for (int i = 1; i < nthreads; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&job.lock);
+    return (int64_t)job.count;
+}

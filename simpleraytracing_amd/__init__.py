@@ -180,6 +180,14 @@ class Context:
                                                   _u8ptr(hit), _fptr(t)), "xrt_probe_intersect")
         return hit, t
 
+    def probe_prep(self, cam: Camera, n: int):
+        """(records (n,16), footprint (n,16)) of the uploaded mesh (n triangles) for `cam`."""
+        rec = np.zeros((n, 16), np.float32)
+        fp = np.zeros((n, 16), np.float32)
+        self._check(self._lib.xrt_probe_prep(self._ctx, ctypes.byref(cam), _fptr(rec), _fptr(fp)),
+                    "xrt_probe_prep")
+        return rec, fp
+
     def probe_math(self, op: int, x: np.ndarray):
         x = np.ascontiguousarray(x, dtype=np.float32)
         out = np.empty_like(x)

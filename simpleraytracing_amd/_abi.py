@@ -60,6 +60,8 @@ class Stats(ctypes.Structure):
         ("max_hits", _u32),
         ("kernel", _u32),
         ("kernel_ms", ctypes.c_double),
+        ("candidates", _u64),
+        ("tile_tests", _u64),
     ]
 
     def as_dict(self):
@@ -92,6 +94,7 @@ XRT_SYMBOLS = {
     "xrt_timing_end": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
     "xrt_probe_intersect": (ctypes.c_int, [_CtxP, _fp, _fp, _u64, _u8p, _fp]),
     "xrt_probe_math": (ctypes.c_int, [_CtxP, ctypes.c_int, _fp, _fp, _u64]),
+    "xrt_probe_prep": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp]),
     "xrt_host_expf_batch": (None, [_fp, _fp, _u64]),
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
 }

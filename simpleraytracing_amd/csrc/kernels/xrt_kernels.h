@@ -32,6 +32,8 @@ struct DevStats {
     unsigned long long hits;
     unsigned int max_hits;
     unsigned int overflow_count;   // entries in the overflow list
+    unsigned long long candidates; // TILED: region candidates (phase 1), summed
+    unsigned long long tile_tests; // wave-level triangle tests (64 rays each)
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -41,12 +43,28 @@ struct CullParams {
     double width, height;
 };
 
+// Per-workgroup statistics, written with plain stores (one record per block)
+// and summed by k_stats_reduce: same-address global atomics from every wave
+// serialise in L2 and dominated short renders.
+struct BlockStats {
+    unsigned long long rays, hit_rays, odd_rays, overflow_rays, hits, tile_tests, candidates;
+    unsigned int max_hits, pad;
+};
+static_assert(sizeof(BlockStats) == 64, "BlockStats must be 64 bytes");
+
 struct Outputs {
     float* image;
     float* lbuffer;
     uint8_t* image_u8;
     uint32_t* overflow_list;   // capacity = strip rays
     DevStats* stats;
+    BlockStats* block_stats;   // one per workgroup of the render grid
+};
+
+// Running per-wave counters (wave-uniform values, kept in SGPRs).
+struct WaveStats {
+    uint32_t rays, hit_rays, odd_rays, overflow_rays, hits, max_hits;
+    uint32_t tile_tests;
 };
 
 constexpr double kEps = 0x1p-24;
@@ -226,13 +244,13 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
 // statistics.  Returns true if the ray overflowed (its outputs are then written
 // by k_overflow).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void wave_stats(DevStats* st, bool active, uint32_t n, bool odd,
+__device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t n, bool odd,
                                            bool overflow)
 {
-    unsigned long long m_act = __ballot(active);
-    unsigned long long m_hit = __ballot(active && n > 0);
-    unsigned long long m_odd = __ballot(active && odd);
-    unsigned long long m_ovf = __ballot(active && overflow);
+    ws.rays += (uint32_t)__popcll(__ballot(active));
+    ws.hit_rays += (uint32_t)__popcll(__ballot(active && n > 0));
+    ws.odd_rays += (uint32_t)__popcll(__ballot(active && odd));
+    ws.overflow_rays += (uint32_t)__popcll(__ballot(active && overflow));
     uint32_t hits = active ? n : 0u;
     uint32_t mx = hits;
 #pragma unroll
@@ -241,22 +259,81 @@ __device__ __forceinline__ void wave_stats(DevStats* st, bool active, uint32_t n
         uint32_t o = __shfl_xor(mx, off);
         mx = mx > o ? mx : o;
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&st->rays, (unsigned long long)__popcll(m_act));
-        if (m_hit) atomicAdd(&st->hit_rays, (unsigned long long)__popcll(m_hit));
-        if (m_odd) atomicAdd(&st->odd_rays, (unsigned long long)__popcll(m_odd));
-        if (m_ovf) atomicAdd(&st->overflow_rays, (unsigned long long)__popcll(m_ovf));
-        if (hits) atomicAdd(&st->hits, (unsigned long long)hits);
-        if (mx) atomicMax(&st->max_hits, mx);
+    ws.hits += hits;
+    ws.max_hits = ws.max_hits > mx ? ws.max_hits : mx;
+}
+
+// Combines the block's wave counters through LDS and stores one BlockStats.
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
+                                                  BlockStats* out)
+{
+    __shared__ WaveStats s_ws[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (lane == 0) s_ws[wave] = ws;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        BlockStats b = {};
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            b.rays += s_ws[w].rays;
+            b.hit_rays += s_ws[w].hit_rays;
+            b.odd_rays += s_ws[w].odd_rays;
+            b.overflow_rays += s_ws[w].overflow_rays;
+            b.hits += s_ws[w].hits;
+            b.tile_tests += s_ws[w].tile_tests;
+            b.max_hits = b.max_hits > s_ws[w].max_hits ? b.max_hits : s_ws[w].max_hits;
+        }
+        b.candidates = candidates;
+        out[blockIdx.y * gridDim.x + blockIdx.x] = b;
+    }
+}
+
+// Sums the per-block records into DevStats (one workgroup; n_blocks of them).
+__global__ __launch_bounds__(1024) void k_stats_reduce(const BlockStats* __restrict__ parts,
+                                                       uint32_t n_blocks, DevStats* __restrict__ st)
+{
+    __shared__ unsigned long long s_sum[7][16];
+    __shared__ unsigned int s_max[16];
+    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned int mx = 0;
+    for (uint32_t i = threadIdx.x; i < n_blocks; i += blockDim.x) {
+        const BlockStats& b = parts[i];
+        v[0] += b.rays; v[1] += b.hit_rays; v[2] += b.odd_rays; v[3] += b.overflow_rays;
+        v[4] += b.hits; v[5] += b.tile_tests; v[6] += b.candidates;
+        mx = mx > b.max_hits ? mx : b.max_hits;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v[k] += __shfl_xor(v[k], off);
+        unsigned int o = __shfl_xor(mx, off);
+        mx = mx > o ? mx : o;
+    }
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        for (int k = 0; k < 7; ++k) s_sum[k][wave] = v[k];
+        s_max[wave] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t[7] = {0, 0, 0, 0, 0, 0, 0};
+        unsigned int m = 0;
+        for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+            for (int k = 0; k < 7; ++k) t[k] += s_sum[k][w];
+            m = m > s_max[w] ? m : s_max[w];
+        }
+        st->rays = t[0]; st->hit_rays = t[1]; st->odd_rays = t[2]; st->overflow_rays = t[3];
+        st->hits = t[4]; st->tile_tests = t[5]; st->candidates = t[6]; st->max_hits = m;
     }
 }
 
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
-                                           uint32_t row, uint32_t col, const HitList& hl)
+                                           uint32_t row, uint32_t col, const HitList& hl,
+                                           WaveStats& ws)
 {
     bool overflow = hl.n > p.hit_capacity;
     bool odd = (hl.n & 1u) != 0u;
-    wave_stats(out.stats, active, hl.n, odd, overflow);
+    wave_stats(ws, active, hl.n, odd, overflow);
     if (!active) return;
     size_t o = (size_t)(row - p.row_begin) * p.width + col;
     if (overflow) {
@@ -307,7 +384,10 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     hl.init();
     const uint32_t T = p.num_triangles;
     for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
-    finish_ray(p, out, active, row, col, hl);
+    WaveStats ws = {};
+    ws.tile_tests = T;
+    finish_ray(p, out, active, row, col, hl, ws);
+    store_block_stats(ws, 0u, out.block_stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -347,28 +427,41 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
     __syncthreads();
 
     // Phase 1: footprint boxes of the whole mesh vs the region (pixel centres).
+    // The sweep is cut into chunks of 1024 boxes (4 independent 16-B loads per
+    // lane in flight) and every workgroup starts at a different chunk, so the
+    // grid's concurrent reads spread over all L2 channels instead of hitting
+    // the same lines in lockstep.
     const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
-    for (uint32_t base = 0; base < T; base += 256u) {
-        uint32_t j = base + tid;
-        bool pass = false;
-        if (j < T) {
-            float4 bb = culls[j];
-            pass = !(bb.y < fx0 || bb.x > fx1 || bb.w < fy0 || bb.z > fy1);
+    const uint32_t nchunks = (T + 1023u) / 1024u;
+    uint32_t chunk = nchunks ? (uint32_t)(((uint64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 2654435761u) % nchunks) : 0u;
+    for (uint32_t c = 0; c < nchunks; ++c, chunk = (chunk + 1u == nchunks) ? 0u : chunk + 1u) {
+        const uint32_t base = chunk * 1024u + tid;
+        float4 bb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t j = base + 256u * u;
+            bb[u] = j < T ? culls[j] : make_float4(1.0f, -1.0f, 1.0f, -1.0f);
         }
-        unsigned long long m = __ballot(pass);
-        if (m) {
-            uint32_t cnt = (uint32_t)__popcll(m);
-            uint32_t wbase = 0;
-            if (lane == 0) wbase = atomicAdd(&s_count, cnt);
-            wbase = __shfl(wbase, 0);
-            if (pass) {
-                uint32_t idx = wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (idx < kListCap) s_list[idx] = j;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t j = base + 256u * u;
+            bool pass = j < T && !(bb[u].y < fx0 || bb[u].x > fx1 || bb[u].w < fy0 || bb[u].z > fy1);
+            unsigned long long m = __ballot(pass);
+            if (m) {
+                uint32_t cnt = (uint32_t)__popcll(m);
+                uint32_t wbase = 0;
+                if (lane == 0) wbase = atomicAdd(&s_count, cnt);
+                wbase = __shfl(wbase, 0);
+                if (pass) {
+                    uint32_t idx = wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    if (idx < kListCap) s_list[idx] = j;
+                }
             }
         }
     }
     __syncthreads();
     const uint32_t n_cand = s_count;
+    WaveStats ws = {};
     const bool use_list = n_cand <= kListCap;
     const uint32_t n_scan = use_list ? n_cand : T;
 
@@ -388,6 +481,7 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
         HitList hl;
         hl.init();
 
+        uint32_t tests = 0;
         for (uint32_t base = 0; base < n_scan; base += 64u) {
             uint32_t k = base + lane;
             uint32_t j = 0;
@@ -397,6 +491,7 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
                 pass = edge_pass(culls, T, j, xc, yc, hx, hy);
             }
             unsigned long long m = __ballot(pass);
+            tests += (uint32_t)__popcll(m);
             while (m) {
                 uint32_t b = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1ull;
@@ -404,8 +499,10 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
                 test_record(recs, jj, dx, dy, dz, hl);
             }
         }
-        finish_ray(p, out, active, row, col, hl);
+        ws.tile_tests += tests;
+        finish_ray(p, out, active, row, col, hl, ws);
     }
+    store_block_stats(ws, n_cand, out.block_stats);
 }
 
 // ---------------------------------------------------------------------------

@@ -30,6 +30,8 @@ struct xrt_context {
     size_t cull_cap = 0;
 
     DevStats* d_stats = nullptr;
+    BlockStats* d_block_stats = nullptr;
+    size_t block_stats_cap = 0;
     uint32_t* d_overflow = nullptr;
     size_t overflow_cap = 0;
 
@@ -191,6 +193,12 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.image_u8 = d_u8;
     out.overflow_list = ctx->d_overflow;
     out.stats = ctx->d_stats;
+    dim3 grid = kernel == XRT_KERNEL_BRUTE
+                    ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
+                    : dim3((cam->width + kRegion - 1) / kRegion, (rows + kRegion - 1) / kRegion);
+    const uint32_t n_blocks = rows ? grid.x * grid.y : 0u;
+    if ((rc = ensure(ctx, ctx->d_block_stats, ctx->block_stats_cap, n_blocks))) return rc;
+    out.block_stats = ctx->d_block_stats;
 
     XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
     if (T) {
@@ -216,10 +224,8 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     XRT_HIP(ctx, hipEventRecord(t0, stream));
     if (rows > 0) {
         if (kernel == XRT_KERNEL_BRUTE) {
-            dim3 grid((cam->width + 15) / 16, (rows + 15) / 16);
             hipLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, ctx->d_recs, p, out);
         } else {
-            dim3 grid((cam->width + kRegion - 1) / kRegion, (rows + kRegion - 1) / kRegion);
             hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs,
                                ctx->d_cull, p, out);
         }
@@ -229,6 +235,9 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (ctx->timing) XRT_HIP(ctx, hipEventRecord(ctx->ev_end, stream));
     if (rows > 0) {
         hipLaunchKernelGGL(k_overflow, dim3(256), dim3(64), 0, stream, ctx->d_recs, p, out);
+        XRT_HIP(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, ctx->d_block_stats,
+                           n_blocks, ctx->d_stats);
         XRT_HIP(ctx, hipGetLastError());
     }
     ctx->last_stream = stream;
@@ -284,6 +293,7 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_recs);
     (void)hipFree(ctx->d_cull);
     (void)hipFree(ctx->d_stats);
+    (void)hipFree(ctx->d_block_stats);
     (void)hipFree(ctx->d_overflow);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
@@ -411,6 +421,8 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     stats->max_hits = s.max_hits;
     stats->kernel = (uint32_t)ctx->last_kernel;
     stats->kernel_ms = ms;
+    stats->candidates = s.candidates;
+    stats->tile_tests = s.tile_tests;
     return XRT_OK;
 }
 
@@ -524,6 +536,35 @@ int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* outp, uint6
     (void)hipFree(di);
     (void)hipFree(dout);
     return rc;
+}
+
+int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, float* footprint)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    int rc = check_camera(ctx, camera, 0, camera ? camera->height : 0);
+    if (rc) return rc;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t T = ctx->num_tris;
+    if (!T) return XRT_OK;
+    if ((rc = ensure(ctx, ctx->d_recs, ctx->recs_cap, T))) return rc;
+    if ((rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes))) return rc;
+    RenderParams p = make_params(*camera, 0, camera->height, T, ctx->hit_capacity);
+    CullParams cp = make_cull_params(*camera);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
+                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull);
+    XRT_HIP(ctx, hipGetLastError());
+    if (records)
+        XRT_HIP(ctx, hipMemcpy(records, ctx->d_recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));
+    if (footprint) {
+        // planes [bbox | e0 | e1 | e2] of T float4 -> per triangle 16 floats
+        std::vector<float4> planes((size_t)T * kCullPlanes);
+        XRT_HIP(ctx, hipMemcpy(planes.data(), ctx->d_cull, planes.size() * sizeof(float4),
+                               hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < T; ++i)
+            for (int k = 0; k < kCullPlanes; ++k)
+                std::memcpy(footprint + 16 * i + 4 * k, &planes[(size_t)k * T + i], sizeof(float4));
+    }
+    return XRT_OK;
 }
 
 // Host evaluation of the device expf restatement (same source, host-compiled);

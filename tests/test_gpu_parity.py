@@ -302,3 +302,26 @@ def test_cli_odd_ray_messages(tmp_path):
                        text=True, cwd=tmp_path, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.count("Only one intersect on this ray") == 24
+
+
+@pytest.mark.parametrize("W,rows", [(256, list(range(256))), (2048, [0, 700, 1024, 1025, 1400, 2047])])
+def test_footprints_contain_every_hit(ctx, dragon, W, rows):
+    """Direct check of the tile cull's conservativeness: every (pixel, triangle)
+    pair the reference's Ray::intersect reports (t > 1e-7) lies inside that
+    triangle's footprint box and satisfies its three relaxed edge functions."""
+    H = W
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    ctx.upload_mesh(dragon)
+    _, fp = ctx.probe_prep(cam, len(dragon))
+    px, tri = oracle.hit_pairs(dragon, cam13(cam), W, H, rows)
+    assert len(px) > 0
+    row = np.asarray(rows, np.float32)[px // W]
+    col = (px % W).astype(np.float32)
+    f = fp[tri]
+    assert np.all((f[:, 0] <= col) & (col <= f[:, 1]) & (f[:, 2] <= row) & (row <= f[:, 3]))
+    for k in range(3):
+        a, b, c = f[:, 4 + 4 * k], f[:, 5 + 4 * k], f[:, 6 + 4 * k]
+        assert np.all(a * col + b * row + c >= 0), k
+    # the footprints are tight: median box no wider than the triangle's projection + 2 px
+    w = fp[:, 1] - fp[:, 0]
+    assert np.median(w[np.isfinite(w)]) < W / 16
