@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
 """bench.py -- Mrays/s of the X-ray render path (BASELINE.json metric).
 
-One step = one full frame of the configured size (default dragon.ply,
-2048x2048): every rank renders its contiguous row strip (rows_per = H/N,
-remainder to the first strips, as main-pthreads-rows.cxx:311-334 splits work)
-on its GPU, and for N > 1 the strips (f32 image, f32 L-buffer, u8 image) are
-gathered to rank 0 with one RCCL gather over xGMI.  The mesh is resident in HBM
-before the timed region; the per-frame triangle preparation (k_prep), the
-render kernel, the overflow fix-up and the gather are all inside it.
+A step renders frames of the configured size (default dragon.ply, 2048x2048,
+every ray tested against the mesh, outputs f32 image + f32 L-buffer + u8
+image).  The mesh is resident in HBM before the timed region; the per-frame
+triangle preparation, the render kernel and its fix-up kernel are inside it.
+
+  --mode frames  (default) weak scaling: every rank renders one whole frame per
+                 step on its own GPU; no collective in the timed loop (the path
+                 shards by frame and by row, with no exchange step).  With
+                 N > 1 an untimed frame is also rendered as row strips and
+                 gathered to rank 0 with RCCL; it must equal rank 0's frame
+                 bit for bit ("gather_check").
+  --mode strips  strong scaling: one frame per step split into row strips
+                 (rows_per = H/N, remainder to the first, as
+                 main-pthreads-rows.cxx:311-334) and gathered to rank 0 with
+                 one RCCL gather over xGMI inside the timed loop.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size W H]
-                    [--kernel tiled|brute] [--tile-mesh n] [--no-cpu-baseline]
+                    [--kernel auto|binned|tiled|brute] [--mode frames|strips]
+                    [--tile-mesh n] [--no-cpu-baseline]
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -36,11 +45,17 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, nargs=2, default=[2048, 2048], metavar=("W", "H"))
-    ap.add_argument("--kernel", choices=["tiled", "brute"], default="tiled")
+    ap.add_argument("--kernel", choices=["auto", "binned", "tiled", "brute"], default="auto")
+    ap.add_argument("--mode", choices=["frames", "strips"], default="frames")
     ap.add_argument("--mesh", default=os.path.join(ROOT, "data", "dragon.ply"))
     ap.add_argument("--tile-mesh", type=int, default=1,
                     help="n x n tiled copies of the mesh (7 = the 1M-triangle config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
+                         "N ranks on fewer GPUs")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank uses device 0 (with --dist-backend gloo)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the bounded cpu_baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -106,10 +121,24 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    device_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(device_index)
+    dev = torch.device("cuda", device_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    def gather_to_root(t, out_list):
+        """dist.gather of a device tensor (RCCL), or staged through the host for gloo."""
+        if args.dist_backend == "nccl":
+            dist.gather(t, out_list, dst=0)
+            return out_list
+        host = t.cpu()
+        lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+        dist.gather(host, lst, dst=0)
+        return lst
 
     W, H = args.size
     tris = xrt.load_ply(args.mesh)
@@ -117,24 +146,26 @@ def main():
         tris = tiled_mesh(tris, args.tile_mesh)
     T = len(tris)
     cam = xrt.camera_for_mesh(tris, W, H)
-    r0, r1 = strip_bounds(H, world, rank)
-    n_max = max_strip_pixels(W, H, world)
+    strips = args.mode == "strips"
+    r0, r1 = strip_bounds(H, world, rank) if strips else (0, H)
+    n_max = max_strip_pixels(W, H, world) if strips else W * H
 
-    ctx = xrt.Context(local_rank)
-    ctx.set_kernel(xrt.XRT_KERNEL_BRUTE if args.kernel == "brute" else xrt.XRT_KERNEL_TILED)
+    ctx = xrt.Context(device_index)
+    ctx.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
+                    "tiled": xrt.XRT_KERNEL_TILED, "binned": xrt.XRT_KERNEL_BINNED}[args.kernel])
     ctx.upload_mesh(tris)
 
-    # one packed strip buffer: [image f32 | L-buffer f32 | u8], gathered in one collective
+    # one packed buffer: [image f32 | L-buffer f32 | u8]
     strip = torch.zeros(9 * n_max, dtype=torch.uint8, device=dev)
     img, lb, u8 = views(strip, n_max)
-    gathered = [torch.empty_like(strip) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gathered = [torch.empty_like(strip) for _ in range(world)] if (strips and world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
 
     def step():
         ctx.render_rows_device(cam, r0, r1, img.data_ptr(), lb.data_ptr(), u8.data_ptr(),
                                stream.cuda_stream)
-        if world > 1:
-            dist.gather(strip, gathered, dst=0)
+        if strips and world > 1:
+            gather_to_root(strip, gathered)
 
     for _ in range(args.warmup):
         step()
@@ -159,20 +190,44 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
+    # untimed: the row-strip + RCCL gather path must reproduce rank 0's frame
+    gather = None
+    if world > 1 and not strips:
+        from simpleraytracing_amd.strips import assemble
+        g0, g1 = strip_bounds(H, world, rank)
+        gn = max_strip_pixels(W, H, world)
+        gbuf = torch.zeros(9 * gn, dtype=torch.uint8, device=dev)
+        gi, gl, gu = views(gbuf, gn)
+        glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        ctx.render_rows_device(cam, g0, g1, gi.data_ptr(), gl.data_ptr(), gu.data_ptr(), stream.cuda_stream)
+        glist = gather_to_root(gbuf, glist)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            full = assemble([x.cpu().numpy() for x in glist], W, H)
+            mine = (img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy())
+            ok = all(np.array_equal(a.view(np.uint8), b.view(np.uint8)) for a, b in zip(full, mine))
+            gather = {"bit_exact_vs_rank0_frame": bool(ok), "striped_frame_plus_gather_ms": gather_ms,
+                      "bytes_gathered": 9 * W * H}
+
     result = None
     if rank == 0:
-        rays_total = W * H * args.steps
+        rays_total = W * H * args.steps * (1 if strips else world)
         value = rays_total / elapsed_max / 1e6
         rays_per_launch = (r1 - r0) * W
         avg_kernel_s = kernel_ms / max(launches, 1) / 1e3
         bytes_per_ray = BYTES_PER_TEST * T + BYTES_OUT_PER_RAY
         achieved = rays_per_launch * bytes_per_ray / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+        result_kernel = {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel]
         workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
                                                          if args.tile_mesh > 1 else "") + f" {W}x{H}"
         traffic = None
         try:
             with open(args.traffic_json) as f:
-                tr = json.load(f).get(f"{args.kernel}:{workload}:{world}")
+                tr = json.load(f).get(f"{result_kernel}:{workload}")
             if tr:
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
@@ -186,18 +241,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if strips else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "dragon.ply from the reference repo (deterministic mesh; no synthetic noise)"
                     if args.tile_mesh == 1 else "tiled copies of dragon.ply (scenes.tiled_mesh)",
             "config": {
                 "workload": workload,
-                "kernel": args.kernel,
+                "kernel": {0: "auto", 1: "brute", 2: "tiled", 3: "binned"}[stats.kernel],
+                "mode": args.mode,
                 "triangles": T,
                 "image": [W, H],
-                "rays_per_step": W * H,
-                "parallelism": f"row strips x{world}" + (", RCCL gather to rank 0" if world > 1 else ""),
+                "rays_per_step": W * H * (1 if strips else world),
+                "parallelism": (f"row strips x{world}, RCCL gather to rank 0" if strips
+                                else f"one frame per rank x{world} (weak)"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -207,7 +264,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "algorithmic_bytes_per_ray": bytes_per_ray,
-                "kernel": "k_render_tiled" if args.kernel == "tiled" else "k_render_brute",
+                "kernel": "k_render_" + {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel],
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "launches": launches,
             },
@@ -218,6 +275,8 @@ def main():
                 "ray_triangle_tests_per_ray": stats.tile_tests * 64 / max(stats.rays, 1),
             },
             "cpu_baseline": None,
+            "gather_check": gather,
+            "dist_backend": args.dist_backend if world > 1 else None,
         }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

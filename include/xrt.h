@@ -57,10 +57,13 @@ typedef enum xrt_status {
 
 /* Kernel selection. */
 typedef enum xrt_kernel {
-    XRT_KERNEL_AUTO = 0,    /* = XRT_KERNEL_TILED */
+    XRT_KERNEL_AUTO = 0,    /* TILED, or BINNED when T x regions > 2e8 */
     XRT_KERNEL_BRUTE = 1,   /* every ray tests every triangle (renderLoop as written) */
-    XRT_KERNEL_TILED = 2    /* every 8x8 ray tile tests every triangle with a conservative
-                               edge-function cull, then exact Moller-Trumbore per ray */
+    XRT_KERNEL_TILED = 2,   /* every 32x32 region sweeps every triangle's conservative
+                               footprint; per 8x8 ray tile the survivors of a relaxed
+                               edge-function test get the exact Moller-Trumbore test */
+    XRT_KERNEL_BINNED = 3   /* as TILED, but footprints are binned to regions once per
+                               frame (count, scan, fill) instead of swept per region */
 } xrt_kernel;
 
 /*
@@ -204,6 +207,12 @@ void xrt_host_expf_batch(const float* in, float* out, uint64_t n);
  * exact overflow path runs.  0 restores the default (16).
  */
 int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
+
+/*
+ * Test hook: caps the BINNED kernel's region-list capacity at `entries` so the
+ * whole-mesh fallback runs.  0 restores automatic sizing.
+ */
+int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
 
 #ifdef __cplusplus
 }

@@ -18,12 +18,13 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BRUTE,  # noqa: F401
-                   XRT_KERNEL_TILED)
+from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
+                   XRT_KERNEL_BRUTE, XRT_KERNEL_TILED)
 
 __all__ = [
     "Camera", "Stats", "Context", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
+    "XRT_KERNEL_BINNED",
 ]
 
 
@@ -127,6 +128,9 @@ class Context:
 
     def set_hit_capacity(self, capacity: int):
         self._check(self._lib.xrt_set_hit_capacity(self._ctx, int(capacity)), "xrt_set_hit_capacity")
+
+    def set_bin_capacity(self, entries: int):
+        self._check(self._lib.xrt_set_bin_capacity(self._ctx, int(entries)), "xrt_set_bin_capacity")
 
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
                     image=True, lbuffer=True, u8=True):

@@ -22,6 +22,7 @@ XRT_ERR_FORMAT = 6
 XRT_KERNEL_AUTO = 0
 XRT_KERNEL_BRUTE = 1
 XRT_KERNEL_TILED = 2
+XRT_KERNEL_BINNED = 3
 
 XRT_PROBE_EXPF = 0
 XRT_PROBE_SQRTF = 1
@@ -97,6 +98,7 @@ XRT_SYMBOLS = {
     "xrt_probe_prep": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp]),
     "xrt_host_expf_batch": (None, [_fp, _fp, _u64]),
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
+    "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
 }
 
 # every C symbol declared in include/xrt_host.h

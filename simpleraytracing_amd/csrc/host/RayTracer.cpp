@@ -27,6 +27,7 @@ int kernel_choice()
     const char* k = std::getenv("XRT_KERNEL");
     if (k && std::strcmp(k, "brute") == 0) return XRT_KERNEL_BRUTE;
     if (k && std::strcmp(k, "tiled") == 0) return XRT_KERNEL_TILED;
+    if (k && std::strcmp(k, "binned") == 0) return XRT_KERNEL_BINNED;
     return XRT_KERNEL_AUTO;
 }
 

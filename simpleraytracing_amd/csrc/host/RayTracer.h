@@ -30,8 +30,9 @@ struct RayTracerInfo {
     Vec3 range;
 };
 
-// Render options (process-wide): kernel = 0 auto, 1 brute force, 2 tiled cull.
-// Defaults come from $XRT_KERNEL ("brute" / "tiled") and $XRT_DEVICE.
+// Render options (process-wide): kernel = 0 auto, 1 brute force, 2 tiled cull,
+// 3 binned cull.  Defaults come from $XRT_KERNEL ("brute" / "tiled" / "binned")
+// and $XRT_DEVICE.
 void setRenderKernel(int kernel);
 void setRenderDevice(int device);
 

@@ -9,7 +9,7 @@
 //   -i, --input FILE           mesh (default ./dragon.ply)
 // additions:
 //   -g, --gpus N               row strips over N GPUs (default 1)
-//   -k, --kernel brute|tiled   render kernel (default tiled)
+//   -k, --kernel brute|tiled|binned  render kernel (default binned)
 //   -t, --threads N            accepted for main-pthreads*.cxx compatibility (ignored)
 //       --lbuffer FILE         also write the L-buffer as raw little-endian f32
 //       --u8 FILE              also write the 8-bit image (LUT 0..80) as PGM
@@ -38,7 +38,7 @@ void showUsage(const std::string& prog)
               << "\t-f,--filename FILENAME\t\tName of the output text file, written to ./out/ (default: test.jpg)\n"
               << "\t-i,--input FILENAME\t\tInput mesh (default: ./dragon.ply)\n"
               << "\t-g,--gpus N\t\t\tRender row strips on N GPUs (default: 1)\n"
-              << "\t-k,--kernel brute|tiled\t\tRender kernel (default: tiled)\n"
+              << "\t-k,--kernel brute|tiled|binned\tRender kernel (default: binned)\n"
               << "\t--lbuffer FILE\t\t\tWrite the L-buffer as raw float32\n"
               << "\t--u8 FILE\t\t\tWrite the 8-bit image (0..80 keV LUT) as PGM\n"
               << "\t--time\t\t\t\tPrint render time and Mrays/s\n"
@@ -98,6 +98,7 @@ Options processCmd(int argc, char** argv)
             std::string k = parse_str(argv[0], argc, argv, i);
             if (k == "brute") o.kernel = XRT_KERNEL_BRUTE;
             else if (k == "tiled") o.kernel = XRT_KERNEL_TILED;
+            else if (k == "binned") o.kernel = XRT_KERNEL_BINNED;
             else {
                 showUsage(argv[0]);
                 std::exit(EXIT_FAILURE);

@@ -51,7 +51,15 @@ struct RenderParams {
     uint32_t row_begin, row_end;
     uint32_t num_triangles;
     uint32_t hit_capacity;  // <= XRT_MAX_HITS
+    uint32_t ablate;        // diagnostics only ($XRT_ABLATE bits, kAblate*); 0 in production
 };
+
+// Ablation bits (timing studies; outputs are wrong when any is set).
+constexpr uint32_t kAblateCandidates = 1;   // phase 2 sees no candidates
+constexpr uint32_t kAblateSweep = 2;        // tiled: no phase-1 footprint sweep
+constexpr uint32_t kAblateRayGen = 4;       // constant ray direction
+constexpr uint32_t kAblateStores = 8;       // no output stores
+constexpr uint32_t kAblateShade = 16;       // no expf / LUT
 
 constexpr int kMaxHits = 16;
 
@@ -146,15 +154,38 @@ struct HitList {
     }
 
     // Insertion keeps h[0..min(n,K)) ascending; +inf sentinels fill the rest.
-    __device__ __forceinline__ void push(float t)
+    // `bound` is a wave-uniform upper bound of n (the number of pushes the
+    // wave has issued): entries at or above it are still sentinels, so the
+    // compare-exchange chain stops there (the chains are unrolled statically).
+    __device__ __forceinline__ void insert_upto(float t, uint32_t bound)
+    {
+        if (bound < 4u) {
+            insert_n<4>(t);
+        } else if (bound < 8u) {
+            insert_n<8>(t);
+        } else if (bound < 12u) {
+            insert_n<12>(t);
+        } else {
+            insert_n<kMaxHits>(t);
+        }
+        ++n;
+    }
+
+    template <int N>
+    __device__ __forceinline__ void insert_n(float t)
     {
 #pragma unroll
-        for (int k = 0; k < kMaxHits; ++k) {
+        for (int k = 0; k < N; ++k) {
             float cur = h[k];
             bool lt = t < cur;
             h[k] = lt ? t : cur;
             t = lt ? cur : t;
         }
+    }
+
+    __device__ __forceinline__ void push(float t)
+    {
+        insert_n<kMaxHits>(t);
         ++n;
     }
 

@@ -22,7 +22,20 @@
 
 #include "xrt_device.h"
 
+// Compile-time variants for A/B timing (tools/ab.py); the defaults are the
+// measured-faster choices.
+#ifndef XRT_BOUNDED_PUSH
+#define XRT_BOUNDED_PUSH 0   // wave-bounded insertion network: measured slower
+#endif
+
 namespace xrt {
+
+struct BinState {            // zeroed per frame with DevStats
+    unsigned int global_count;
+    unsigned int total;
+    unsigned int overflow;   // total > list_cap: regions fall back to the whole mesh
+    unsigned int pad;
+};
 
 struct DevStats {
     unsigned long long rays;
@@ -34,6 +47,7 @@ struct DevStats {
     unsigned int overflow_count;   // entries in the overflow list
     unsigned long long candidates; // TILED: region candidates (phase 1), summed
     unsigned long long tile_tests; // wave-level triangle tests (64 rays each)
+    BinState bin;
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -61,9 +75,11 @@ struct Outputs {
     BlockStats* block_stats;   // one per workgroup of the render grid
 };
 
-// Running per-wave counters (wave-uniform values, kept in SGPRs).
+// Running counters of one wave: ballot counts (wave-uniform), per-lane hit sum
+// and maximum (reduced across the wave once, in store_block_stats).
 struct WaveStats {
-    uint32_t rays, hit_rays, odd_rays, overflow_rays, hits, max_hits;
+    uint32_t rays, hit_rays, odd_rays, overflow_rays;
+    uint32_t lane_hits, lane_max;   // per lane
     uint32_t tile_tests;
 };
 
@@ -87,12 +103,423 @@ __device__ __forceinline__ double l1_d(const double a[3])
 }
 
 // ---------------------------------------------------------------------------
+// Per-ray epilogue shared by the render kernels: L-buffer, shade, LUT, stores,
+// statistics.  Returns true if the ray overflowed (its outputs are then written
+// by k_overflow).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t n, bool odd,
+                                           bool overflow)
+{
+    ws.rays += (uint32_t)__popcll(__ballot(active));
+    ws.hit_rays += (uint32_t)__popcll(__ballot(active && n > 0));
+    ws.odd_rays += (uint32_t)__popcll(__ballot(active && odd));
+    ws.overflow_rays += (uint32_t)__popcll(__ballot(active && overflow));
+    const uint32_t h = active ? n : 0u;
+    ws.lane_hits += h;
+    ws.lane_max = ws.lane_max > h ? ws.lane_max : h;
+}
+
+// Combines the block's wave counters through LDS and stores one BlockStats.
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
+                                                  BlockStats* out)
+{
+    __shared__ WaveStats s_ws[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t hits = ws.lane_hits, mx = ws.lane_max;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        hits += __shfl_xor(hits, off);
+        const uint32_t o = __shfl_xor(mx, off);
+        mx = mx > o ? mx : o;
+    }
+    if (lane == 0) {
+        s_ws[wave] = ws;
+        s_ws[wave].lane_hits = hits;
+        s_ws[wave].lane_max = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        BlockStats b = {};
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            b.rays += s_ws[w].rays;
+            b.hit_rays += s_ws[w].hit_rays;
+            b.odd_rays += s_ws[w].odd_rays;
+            b.overflow_rays += s_ws[w].overflow_rays;
+            b.hits += s_ws[w].lane_hits;
+            b.tile_tests += s_ws[w].tile_tests;
+            b.max_hits = b.max_hits > s_ws[w].lane_max ? b.max_hits : s_ws[w].lane_max;
+        }
+        b.candidates = candidates;
+        out[blockIdx.y * gridDim.x + blockIdx.x] = b;
+    }
+}
+
+__device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
+                                           uint32_t row, uint32_t col, const HitList& hl,
+                                           WaveStats& ws)
+{
+    bool overflow = hl.n > p.hit_capacity;
+    bool odd = (hl.n & 1u) != 0u;
+    wave_stats(ws, active, hl.n, odd, overflow);
+    if (!active) return;
+    size_t o = (size_t)(row - p.row_begin) * p.width + col;
+    if (overflow) {
+        uint32_t slot = atomicAdd(&out.stats->overflow_count, 1u);
+        out.overflow_list[slot] = (uint32_t)o;
+        return;
+    }
+    // main.cxx:700-718
+    float distance = 0.0f;
+    float lval = __builtin_inff();
+    if (hl.n > 0) {
+        if (!odd) distance = hl.path_length();
+        lval = distance;
+    }
+    if (p.ablate & (kAblateStores | kAblateShade)) {
+        if (!(p.ablate & kAblateStores)) {
+            if (out.image) out.image[o] = distance;
+            if (out.lbuffer) out.lbuffer[o] = lval;
+        }
+        return;
+    }
+    float photon = shade(distance);
+    if (out.image) out.image[o] = photon;
+    if (out.lbuffer) out.lbuffer[o] = lval;
+    if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+}
+
+// Loads one triangle record with a wave-uniform index (scalar loads).
+__device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
+                                            float dy, float dz, HitList& hl, uint32_t& pushes)
+{
+    const float4* q = reinterpret_cast<const float4*>(recs + j);
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    float t;
+    const bool hit =
+        mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
+        accept_t(t);
+#if XRT_BOUNDED_PUSH
+    if (hit) hl.insert_upto(t, pushes);
+    pushes += __ballot(hit) != 0ull ? 1u : 0u;
+#else
+    if (hit) hl.push(t);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_render_brute: block = 256 lanes = 2x2 waves, each wave one 8x8 ray tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__ recs,
+                                                      RenderParams p, Outputs out)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t col = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
+    const uint32_t row = p.row_begin + (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    const bool active = col < p.width && row < p.row_end;
+
+    float dx, dy, dz;
+    make_ray(p, row, col, dx, dy, dz);
+    HitList hl;
+    hl.init();
+    const uint32_t T = p.num_triangles;
+    uint32_t pushes = 0;
+    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl, pushes);
+    WaveStats ws = {};
+    ws.tile_tests = T;
+    finish_ray(p, out, active, row, col, hl, ws);
+    store_block_stats(ws, 0u, out.block_stats);
+}
+
+// ---------------------------------------------------------------------------
+// Tile cull (k_render_tiled, k_render_binned)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
+constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
+constexpr uint32_t kGlobalRegions = 64; // footprints over more regions go to the global list
+
+// Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
+// function a*col + b*row + c.
+__device__ __forceinline__ float edge_max(float4 e, float xc, float yc, float hx, float hy)
+{
+    return (e.x * xc + e.y * yc) + (e.z + (fabsf(e.x) * hx + fabsf(e.y) * hy));
+}
+
+__device__ __forceinline__ bool edges_pass(float4 e0, float4 e1, float4 e2, float xc, float yc,
+                                           float hx, float hy)
+{
+    return edge_max(e0, xc, yc, hx, hy) >= 0.0f && edge_max(e1, xc, yc, hx, hy) >= 0.0f &&
+           edge_max(e2, xc, yc, hx, hy) >= 0.0f;
+}
+
+__device__ __forceinline__ bool edge_pass(const float4* __restrict__ culls, uint32_t T, uint32_t j,
+                                          float xc, float yc, float hx, float hy)
+{
+    return edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j], xc,
+                      yc, hx, hy);
+}
+
+// Phase 2, shared by the tiled and binned kernels.
+//
+// The region's candidates (fetch(k) = triangle of the k-th candidate) are
+// staged into LDS in chunks of kStage: their three relaxed edge functions and
+// their Moller-Trumbore record, structure-of-arrays, loaded by all 256 lanes
+// in one parallel round trip.  Each wave then renders its four 8x8 tiles from
+// LDS only: one lane per staged candidate tests the tile rectangle against
+// the relaxed edges, a ballot keeps the survivors, and each survivor's record
+// is read with a wave-uniform (broadcast) LDS read and tested exactly for all
+// 64 rays.  A region with more than kStage candidates re-stages per chunk
+// (every wave reaches every barrier: the loop trip counts are block-uniform).
+constexpr uint32_t kStage = 128;
+
+struct StageLDS {
+    float4 e0[kStage], e1[kStage], e2[kStage];
+    float4 r0[kStage], r1[kStage], r2[kStage];
+    float tnum[kStage];
+};
+
+template <typename Fetch>
+__device__ __forceinline__ void stage_candidates(StageLDS& st, const TriRec* __restrict__ recs,
+                                                 const float4* __restrict__ culls, uint32_t T,
+                                                 uint32_t first, uint32_t count, Fetch fetch)
+{
+    for (uint32_t k = threadIdx.x; k < count; k += blockDim.x) {
+        const uint32_t j = fetch(first + k);
+        const float4* q = reinterpret_cast<const float4*>(recs + j);
+        float4 e0 = culls[(size_t)T + j], e1 = culls[2 * (size_t)T + j], e2 = culls[3 * (size_t)T + j];
+        float4 r0 = q[0], r1 = q[1], r2 = q[2];
+        float tn = recs[j].tnum;
+        st.e0[k] = e0; st.e1[k] = e1; st.e2[k] = e2;
+        st.r0[k] = r0; st.r1[k] = r1; st.r2[k] = r2;
+        st.tnum[k] = tn;
+    }
+}
+
+__device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t count, float xc,
+                                                float yc, float dx, float dy, float dz, HitList& hl,
+                                                uint32_t& pushes)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t tests = 0;
+    for (uint32_t base = 0; base < count; base += 64u) {
+        const uint32_t k = base + lane;
+        const bool pass = k < count && edges_pass(st.e0[k], st.e1[k], st.e2[k], xc, yc, 3.5f, 3.5f);
+        unsigned long long m = __ballot(pass);
+        tests += (uint32_t)__popcll(m);
+        while (m) {
+            const uint32_t kk = base + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            const float4 a = st.r0[kk], b = st.r1[kk], c = st.r2[kk];
+            const float tn = st.tnum[kk];
+            float t;
+            const bool hit = mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x,
+                                          c.y, c.z, c.w, tn, t) &&
+                             accept_t(t);
+#if XRT_BOUNDED_PUSH
+            if (hit) hl.insert_upto(t, pushes);
+            pushes += __ballot(hit) != 0ull ? 1u : 0u;
+#else
+            if (hit) hl.push(t);
+#endif
+        }
+    }
+    return tests;
+}
+
+template <typename Fetch>
+__device__ __forceinline__ void render_region_tiles(const RenderParams& p, const Outputs& out,
+                                                    const TriRec* __restrict__ recs,
+                                                    const float4* __restrict__ culls,
+                                                    uint32_t rx0, uint32_t ry0, uint32_t n_cand,
+                                                    Fetch fetch, WaveStats& ws, StageLDS& st)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t T = p.num_triangles;
+    if (p.ablate & kAblateCandidates) n_cand = 0;
+    const bool once = n_cand <= kStage;
+    if (once) {
+        stage_candidates(st, recs, culls, T, 0u, n_cand, fetch);
+        __syncthreads();
+    }
+    for (uint32_t tile = wave; tile < 16u; tile += 4u) {
+        const uint32_t tx0 = rx0 + (tile & 3u) * 8u;
+        const uint32_t ty0 = ry0 + (tile >> 2) * 8u;
+        const bool tile_live = tx0 < p.width && ty0 < p.row_end;   // wave-uniform
+        const uint32_t col = tx0 + (lane & 7u);
+        const uint32_t row = ty0 + (lane >> 3);
+        const bool active = tile_live && col < p.width && row < p.row_end;
+        const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
+
+        float dx = 0.0f, dy = 0.0f, dz = 0.0f;
+        if (tile_live && !(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+        else dx = 1.0f;
+        HitList hl;
+        hl.init();
+        uint32_t tests = 0, pushes = 0;
+        if (once) {
+            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, pushes);
+        } else {
+            for (uint32_t first = 0; first < n_cand; first += kStage) {
+                const uint32_t count = min(kStage, n_cand - first);
+                __syncthreads();
+                stage_candidates(st, recs, culls, T, first, count, fetch);
+                __syncthreads();
+                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, pushes);
+            }
+        }
+        if (tile_live) {
+            ws.tile_tests += tests;
+            finish_ray(p, out, active, row, col, hl, ws);
+        }
+    }
+}
+
+// k_render_tiled: one 32x32 region per workgroup.  Phase 1: the 256 lanes
+// sweep the footprint boxes of the whole mesh (every region sees every
+// triangle) and compact the region's candidates into an LDS list.
+__global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__ recs,
+                                                      const float4* __restrict__ culls,
+                                                      RenderParams p, Outputs out)
+{
+    __shared__ uint32_t s_list[kListCap];
+    __shared__ uint32_t s_count;
+    __shared__ StageLDS st;
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t T = p.num_triangles;
+    const uint32_t rx0 = blockIdx.x * kRegion;
+    const uint32_t ry0 = p.row_begin + blockIdx.y * kRegion;
+    const uint32_t rx1 = min(rx0 + kRegion, p.width) - 1u;       // inclusive
+    const uint32_t ry1 = min(ry0 + kRegion, p.row_end) - 1u;
+
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+
+    // Chunks of 1024 boxes (4 independent 16-B loads per lane in flight); every
+    // workgroup starts at a different chunk so concurrent reads spread over
+    // the L2 channels.
+    const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
+    const uint32_t nchunks = (p.ablate & kAblateSweep) ? 0u : (T + 1023u) / 1024u;
+    uint32_t chunk =
+        nchunks ? (uint32_t)(((uint64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 2654435761u) % nchunks) : 0u;
+    for (uint32_t c = 0; c < nchunks; ++c, chunk = (chunk + 1u == nchunks) ? 0u : chunk + 1u) {
+        const uint32_t base = chunk * 1024u + tid;
+        float4 bb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t j = base + 256u * u;
+            bb[u] = j < T ? culls[j] : make_float4(1.0f, -1.0f, 1.0f, -1.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t j = base + 256u * u;
+            bool pass = j < T && !(bb[u].y < fx0 || bb[u].x > fx1 || bb[u].w < fy0 || bb[u].z > fy1);
+            unsigned long long m = __ballot(pass);
+            if (m) {
+                uint32_t cnt = (uint32_t)__popcll(m);
+                uint32_t wbase = 0;
+                if (lane == 0) wbase = atomicAdd(&s_count, cnt);
+                wbase = __shfl(wbase, 0);
+                if (pass) {
+                    uint32_t idx = wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    if (idx < kListCap) s_list[idx] = j;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n_cand = s_count;
+    WaveStats ws = {};
+    if (n_cand <= kListCap)
+        render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand,
+                            [&](uint32_t k) { return s_list[k]; }, ws, st);
+    else   // list overflow: every triangle is a candidate (still exact)
+        render_region_tiles(p, out, recs, culls, rx0, ry0, T, [](uint32_t k) { return k; }, ws, st);
+    store_block_stats(ws, n_cand, out.block_stats);
+}
+
+// ---------------------------------------------------------------------------
+// Binning (k_render_binned): footprints are assigned to 32x32 regions once per
+// frame -- count (in k_prep), scan, fill -- so each region's workgroup reads
+// only its own candidates.  Footprints covering more than kGlobalRegions
+// regions (or unbounded ones) go to a global list every region reads.
+// ---------------------------------------------------------------------------
+struct BinBuffers {
+    uint32_t* counts;        // [n_regions]            zeroed before k_prep
+    uint32_t* offsets;       // [n_regions + 1]        exclusive scan of counts
+    uint32_t* cursor;        // [n_regions]            fill cursors
+    uint32_t* list;          // [list_cap]             region candidate lists
+    uint32_t* global_list;   // [T]
+    uint32_t list_cap;
+    uint32_t regions_x, regions_y;
+};
+
+// Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
+// footprint box may touch; false when it touches none.
+__device__ __forceinline__ bool footprint_regions(float4 bb, const RenderParams& p,
+                                                  const BinBuffers& bins, uint32_t& x0,
+                                                  uint32_t& x1, uint32_t& y0, uint32_t& y1)
+{
+    if (!(bb.x <= bb.y) || !(bb.z <= bb.w)) return false;           // empty or NaN
+    const float rows = (float)(p.row_end - p.row_begin);
+    float xmin = fmaxf(bb.x, -64.0f), xmax = fminf(bb.y, (float)p.width + 64.0f);
+    float ymin = fmaxf(bb.z - (float)p.row_begin, -64.0f), ymax = fminf(bb.w - (float)p.row_begin, rows + 64.0f);
+    if (xmax < 0.0f || ymax < 0.0f || xmin > (float)p.width || ymin > rows) return false;
+    int ix0 = (int)floorf((xmin - 31.0f) * (1.0f / 32.0f));
+    int ix1 = (int)floorf(xmax * (1.0f / 32.0f));
+    int iy0 = (int)floorf((ymin - 31.0f) * (1.0f / 32.0f));
+    int iy1 = (int)floorf(ymax * (1.0f / 32.0f));
+    ix0 = max(ix0, 0);
+    iy0 = max(iy0, 0);
+    ix1 = min(ix1, (int)bins.regions_x - 1);
+    iy1 = min(iy1, (int)bins.regions_y - 1);
+    if (ix0 > ix1 || iy0 > iy1) return false;
+    x0 = (uint32_t)ix0; x1 = (uint32_t)ix1; y0 = (uint32_t)iy0; y1 = (uint32_t)iy1;
+    return true;
+}
+
+// Calls f(region) for every region of the rectangle whose 32x32 pixel-centre
+// square passes the relaxed edge functions.
+template <typename F>
+__device__ __forceinline__ void for_each_region(const RenderParams& p, const BinBuffers& bins,
+                                                uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1,
+                                                float4 e0, float4 e1, float4 e2, F f)
+{
+    for (uint32_t ry = y0; ry <= y1; ++ry) {
+        const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
+        for (uint32_t rx = x0; rx <= x1; ++rx) {
+            const float xc = (float)(rx * kRegion) + 15.5f;
+            if (edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f)) f(ry * bins.regions_x + rx);
+        }
+    }
+}
+
+// Counting pass, run per triangle right after its footprint is known.
+__device__ __forceinline__ void bin_count(uint32_t j, float4 bb, float4 e0, float4 e1, float4 e2,
+                                          const RenderParams& p, const BinBuffers& bins,
+                                          BinState* bs)
+{
+    uint32_t x0, x1, y0, y1;
+    if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return;
+    if ((uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1) > kGlobalRegions) {
+        bins.global_list[atomicAdd(&bs->global_count, 1u)] = j;
+        return;
+    }
+    for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2,
+                    [&](uint32_t r) { atomicAdd(&bins.counts[r], 1u); });
+}
+
+// ---------------------------------------------------------------------------
 // k_prep
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
-                                              float4* __restrict__ culls)
+                                              float4* __restrict__ culls, BinBuffers bins,
+                                              BinState* __restrict__ bs)
 {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T) return;
@@ -128,6 +555,7 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
         culls[(size_t)T + i] = c.e0;
         culls[2 * (size_t)T + i] = c.e1;
         culls[3 * (size_t)T + i] = c.e2;
+        if (bins.counts) bin_count(i, c.bbox, c.e0, c.e1, c.e2, p, bins, bs);
     };
 
     bool finite = isfinite(r.tnum) && isfinite(r.qvx) && isfinite(r.qvy) && isfinite(r.qvz);
@@ -239,64 +667,95 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     store();
 }
 
-// ---------------------------------------------------------------------------
-// Per-ray epilogue shared by the render kernels: L-buffer, shade, LUT, stores,
-// statistics.  Returns true if the ray overflowed (its outputs are then written
-// by k_overflow).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t n, bool odd,
-                                           bool overflow)
+// Single-workgroup exclusive scan of the region counts.
+__global__ __launch_bounds__(1024) void k_bin_scan(BinBuffers bins, BinState* __restrict__ bs)
 {
-    ws.rays += (uint32_t)__popcll(__ballot(active));
-    ws.hit_rays += (uint32_t)__popcll(__ballot(active && n > 0));
-    ws.odd_rays += (uint32_t)__popcll(__ballot(active && odd));
-    ws.overflow_rays += (uint32_t)__popcll(__ballot(active && overflow));
-    uint32_t hits = active ? n : 0u;
-    uint32_t mx = hits;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        hits += __shfl_xor(hits, off);
-        uint32_t o = __shfl_xor(mx, off);
-        mx = mx > o ? mx : o;
-    }
-    ws.hits += hits;
-    ws.max_hits = ws.max_hits > mx ? ws.max_hits : mx;
-}
-
-// Combines the block's wave counters through LDS and stores one BlockStats.
-// Must be reached by every thread of the block.
-__device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
-                                                  BlockStats* out)
-{
-    __shared__ WaveStats s_ws[4];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (lane == 0) s_ws[wave] = ws;
+    __shared__ uint32_t s_part[1024];
+    const uint32_t n = bins.regions_x * bins.regions_y;
+    const uint32_t per = (n + 1023u) / 1024u;
+    const uint32_t b = threadIdx.x * per, e = min(b + per, n);
+    uint32_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += bins.counts[i];
+    s_part[threadIdx.x] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        BlockStats b = {};
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-            b.rays += s_ws[w].rays;
-            b.hit_rays += s_ws[w].hit_rays;
-            b.odd_rays += s_ws[w].odd_rays;
-            b.overflow_rays += s_ws[w].overflow_rays;
-            b.hits += s_ws[w].hits;
-            b.tile_tests += s_ws[w].tile_tests;
-            b.max_hits = b.max_hits > s_ws[w].max_hits ? b.max_hits : s_ws[w].max_hits;
-        }
-        b.candidates = candidates;
-        out[blockIdx.y * gridDim.x + blockIdx.x] = b;
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {     // Hillis-Steele inclusive scan
+        uint32_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_part[threadIdx.x] - sum;
+    for (uint32_t i = b; i < e; ++i) {
+        bins.offsets[i] = run;
+        bins.cursor[i] = run;
+        run += bins.counts[i];
+    }
+    if (threadIdx.x == 1023u) {
+        bins.offsets[n] = s_part[1023];
+        bs->total = s_part[1023];
+        bs->overflow = s_part[1023] > bins.list_cap ? 1u : 0u;
     }
 }
 
-// Sums the per-block records into DevStats (one workgroup; n_blocks of them).
-__global__ __launch_bounds__(1024) void k_stats_reduce(const BlockStats* __restrict__ parts,
-                                                       uint32_t n_blocks, DevStats* __restrict__ st)
+// Fill pass: one thread per triangle appends it to its regions' lists.
+__global__ __launch_bounds__(256) void k_bin_fill(const float4* __restrict__ culls, RenderParams p,
+                                                  BinBuffers bins, const BinState* __restrict__ bs)
 {
-    __shared__ unsigned long long s_sum[7][16];
-    __shared__ unsigned int s_max[16];
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = p.num_triangles;
+    if (j >= T || bs->overflow) return;
+    float4 bb = culls[j];
+    uint32_t x0, x1, y0, y1;
+    if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return;
+    if ((uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1) > kGlobalRegions) return;   // in the global list
+    float4 e0 = culls[(size_t)T + j], e1 = culls[2 * (size_t)T + j], e2 = culls[3 * (size_t)T + j];
+    for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2,
+                    [&](uint32_t r) { bins.list[atomicAdd(&bins.cursor[r], 1u)] = j; });
+}
+
+__global__ __launch_bounds__(256) void k_render_binned(const TriRec* __restrict__ recs,
+                                                       const float4* __restrict__ culls,
+                                                       RenderParams p, Outputs out, BinBuffers bins,
+                                                       const BinState* __restrict__ bs)
+{
+    __shared__ StageLDS st;
+    const uint32_t region = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t rx0 = blockIdx.x * kRegion;
+    const uint32_t ry0 = p.row_begin + blockIdx.y * kRegion;
+    WaveStats ws = {};
+    uint32_t n_cand;
+    if (bs->overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
+        n_cand = p.num_triangles;
+        render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand, [](uint32_t k) { return k; }, ws, st);
+    } else {
+        const uint32_t lo = bins.offsets[region];
+        const uint32_t n_local = bins.offsets[region + 1] - lo;
+        const uint32_t* __restrict__ local = bins.list + lo;
+        const uint32_t* __restrict__ glob = bins.global_list;
+        n_cand = n_local + bs->global_count;
+        render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand,
+                            [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws, st);
+    }
+    store_block_stats(ws, n_cand, out.block_stats);
+}
+
+// ---------------------------------------------------------------------------
+// k_finish: (1) exact result for rays whose hit count exceeded the register
+// list -- the sorted hit sequence is streamed by repeated scans for the next
+// larger distance (with its multiplicity), so any hit count is handled with
+// O(1) state and main.cxx:703-708's sum runs in the same order; (2) workgroup
+// 0 sums the per-workgroup statistics.
+// ---------------------------------------------------------------------------
+// Every k_finish workgroup sums a slice of the per-workgroup records and adds
+// it to DevStats (a handful of atomics per workgroup, spread over 8 words).
+__device__ void stats_reduce_slice(const BlockStats* __restrict__ parts, uint32_t n_blocks,
+                                   DevStats* __restrict__ st)
+{
+    __shared__ unsigned long long s_sum[7][4];
+    __shared__ unsigned int s_max[4];
     unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
     unsigned int mx = 0;
-    for (uint32_t i = threadIdx.x; i < n_blocks; i += blockDim.x) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_blocks; i += gridDim.x * blockDim.x) {
         const BlockStats& b = parts[i];
         v[0] += b.rays; v[1] += b.hit_rays; v[2] += b.odd_rays; v[3] += b.overflow_rays;
         v[4] += b.hits; v[5] += b.tile_tests; v[6] += b.candidates;
@@ -315,205 +774,26 @@ __global__ __launch_bounds__(1024) void k_stats_reduce(const BlockStats* __restr
         s_max[wave] = mx;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t[7] = {0, 0, 0, 0, 0, 0, 0};
-        unsigned int m = 0;
-        for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
-            for (int k = 0; k < 7; ++k) t[k] += s_sum[k][w];
-            m = m > s_max[w] ? m : s_max[w];
-        }
-        st->rays = t[0]; st->hit_rays = t[1]; st->odd_rays = t[2]; st->overflow_rays = t[3];
-        st->hits = t[4]; st->tile_tests = t[5]; st->candidates = t[6]; st->max_hits = m;
-    }
-}
-
-__device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
-                                           uint32_t row, uint32_t col, const HitList& hl,
-                                           WaveStats& ws)
-{
-    bool overflow = hl.n > p.hit_capacity;
-    bool odd = (hl.n & 1u) != 0u;
-    wave_stats(ws, active, hl.n, odd, overflow);
-    if (!active) return;
-    size_t o = (size_t)(row - p.row_begin) * p.width + col;
-    if (overflow) {
-        uint32_t slot = atomicAdd(&out.stats->overflow_count, 1u);
-        out.overflow_list[slot] = (uint32_t)o;
-        return;
-    }
-    // main.cxx:700-718
-    float distance = 0.0f;
-    float lval = __builtin_inff();
-    if (hl.n > 0) {
-        if (!odd) distance = hl.path_length();
-        lval = distance;
-    }
-    float photon = shade(distance);
-    if (out.image) out.image[o] = photon;
-    if (out.lbuffer) out.lbuffer[o] = lval;
-    if (out.image_u8) out.image_u8[o] = lut_u8(photon);
-}
-
-// Loads one triangle record with a wave-uniform index (scalar loads).
-__device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
-                                            float dy, float dz, HitList& hl)
-{
-    const float4* q = reinterpret_cast<const float4*>(recs + j);
-    float4 a = q[0], b = q[1], c = q[2], d = q[3];
-    float t;
-    if (mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
-        accept_t(t))
-        hl.push(t);
-}
-
-// ---------------------------------------------------------------------------
-// k_render_brute: block = 256 lanes = 2x2 waves, each wave one 8x8 ray tile.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__ recs,
-                                                      RenderParams p, Outputs out)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t col = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
-    const uint32_t row = p.row_begin + (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
-    const bool active = col < p.width && row < p.row_end;
-
-    float dx, dy, dz;
-    make_ray(p, row, col, dx, dy, dz);
-    HitList hl;
-    hl.init();
-    const uint32_t T = p.num_triangles;
-    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
-    WaveStats ws = {};
-    ws.tile_tests = T;
-    finish_ray(p, out, active, row, col, hl, ws);
-    store_block_stats(ws, 0u, out.block_stats);
-}
-
-// ---------------------------------------------------------------------------
-// k_render_tiled
-// ---------------------------------------------------------------------------
-constexpr uint32_t kRegion = 32;        // pixels per region side
-constexpr uint32_t kListCap = 4096;     // LDS candidate list capacity
-
-__device__ __forceinline__ bool edge_pass(const float4* __restrict__ culls, uint32_t T, uint32_t j,
-                                          float xc, float yc, float hx, float hy)
-{
-    float4 e0 = culls[(size_t)T + j], e1 = culls[2 * (size_t)T + j], e2 = culls[3 * (size_t)T + j];
-    float v0 = (e0.x * xc + e0.y * yc) + (e0.z + (fabsf(e0.x) * hx + fabsf(e0.y) * hy));
-    float v1 = (e1.x * xc + e1.y * yc) + (e1.z + (fabsf(e1.x) * hx + fabsf(e1.y) * hy));
-    float v2 = (e2.x * xc + e2.y * yc) + (e2.z + (fabsf(e2.x) * hx + fabsf(e2.y) * hy));
-    return v0 >= 0.0f && v1 >= 0.0f && v2 >= 0.0f;
-}
-
-__global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__ recs,
-                                                      const float4* __restrict__ culls,
-                                                      RenderParams p, Outputs out)
-{
-    __shared__ uint32_t s_list[kListCap];
-    __shared__ uint32_t s_count;
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = tid >> 6;
-    const uint32_t T = p.num_triangles;
-
-    const uint32_t rx0 = blockIdx.x * kRegion;
-    const uint32_t ry0 = p.row_begin + blockIdx.y * kRegion;
-    const uint32_t rx1 = min(rx0 + kRegion, p.width) - 1u;       // inclusive
-    const uint32_t ry1 = min(ry0 + kRegion, p.row_end) - 1u;
-
-    if (tid == 0) s_count = 0;
-    __syncthreads();
-
-    // Phase 1: footprint boxes of the whole mesh vs the region (pixel centres).
-    // The sweep is cut into chunks of 1024 boxes (4 independent 16-B loads per
-    // lane in flight) and every workgroup starts at a different chunk, so the
-    // grid's concurrent reads spread over all L2 channels instead of hitting
-    // the same lines in lockstep.
-    const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
-    const uint32_t nchunks = (T + 1023u) / 1024u;
-    uint32_t chunk = nchunks ? (uint32_t)(((uint64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 2654435761u) % nchunks) : 0u;
-    for (uint32_t c = 0; c < nchunks; ++c, chunk = (chunk + 1u == nchunks) ? 0u : chunk + 1u) {
-        const uint32_t base = chunk * 1024u + tid;
-        float4 bb[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint32_t j = base + 256u * u;
-            bb[u] = j < T ? culls[j] : make_float4(1.0f, -1.0f, 1.0f, -1.0f);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint32_t j = base + 256u * u;
-            bool pass = j < T && !(bb[u].y < fx0 || bb[u].x > fx1 || bb[u].w < fy0 || bb[u].z > fy1);
-            unsigned long long m = __ballot(pass);
-            if (m) {
-                uint32_t cnt = (uint32_t)__popcll(m);
-                uint32_t wbase = 0;
-                if (lane == 0) wbase = atomicAdd(&s_count, cnt);
-                wbase = __shfl(wbase, 0);
-                if (pass) {
-                    uint32_t idx = wbase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                    if (idx < kListCap) s_list[idx] = j;
-                }
-            }
+    if (threadIdx.x < 8u) {
+        const uint32_t k = threadIdx.x;
+        if (k < 7) {
+            unsigned long long t = 0;
+            for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) t += s_sum[k][w];
+            unsigned long long* dst[7] = {&st->rays, &st->hit_rays, &st->odd_rays, &st->overflow_rays,
+                                          &st->hits, &st->tile_tests, &st->candidates};
+            if (t) atomicAdd(dst[k], t);
+        } else {
+            unsigned int m = 0;
+            for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) m = m > s_max[w] ? m : s_max[w];
+            if (m) atomicMax(&st->max_hits, m);
         }
     }
-    __syncthreads();
-    const uint32_t n_cand = s_count;
-    WaveStats ws = {};
-    const bool use_list = n_cand <= kListCap;
-    const uint32_t n_scan = use_list ? n_cand : T;
-
-    // Phase 2: each wave takes tiles wave, wave+4, wave+8, wave+12.
-    for (uint32_t tile = wave; tile < 16u; tile += 4u) {
-        const uint32_t tx0 = rx0 + (tile & 3u) * 8u;
-        const uint32_t ty0 = ry0 + (tile >> 2) * 8u;
-        if (tx0 >= p.width || ty0 >= p.row_end) continue;          // wave-uniform
-        const uint32_t col = tx0 + (lane & 7u);
-        const uint32_t row = ty0 + (lane >> 3);
-        const bool active = col < p.width && row < p.row_end;
-        const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
-        const float hx = 3.5f, hy = 3.5f;
-
-        float dx, dy, dz;
-        make_ray(p, row, col, dx, dy, dz);
-        HitList hl;
-        hl.init();
-
-        uint32_t tests = 0;
-        for (uint32_t base = 0; base < n_scan; base += 64u) {
-            uint32_t k = base + lane;
-            uint32_t j = 0;
-            bool pass = false;
-            if (k < n_scan) {
-                j = use_list ? s_list[k] : k;
-                pass = edge_pass(culls, T, j, xc, yc, hx, hy);
-            }
-            unsigned long long m = __ballot(pass);
-            tests += (uint32_t)__popcll(m);
-            while (m) {
-                uint32_t b = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1ull;
-                uint32_t jj = __builtin_amdgcn_readlane(j, b);
-                test_record(recs, jj, dx, dy, dz, hl);
-            }
-        }
-        ws.tile_tests += tests;
-        finish_ray(p, out, active, row, col, hl, ws);
-    }
-    store_block_stats(ws, n_cand, out.block_stats);
 }
 
-// ---------------------------------------------------------------------------
-// k_overflow: exact result for rays whose hit count exceeded the register
-// list.  The sorted hit sequence is streamed by repeated scans for the next
-// larger distance (with its multiplicity), so any hit count is handled with
-// O(1) state: main.cxx:703-708's sum in the same order.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_overflow(const TriRec* __restrict__ recs, RenderParams p,
-                                                 Outputs out)
+__global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs, RenderParams p,
+                                                Outputs out, uint32_t n_blocks)
 {
+    stats_reduce_slice(out.block_stats, n_blocks, out.stats);
     const uint32_t count = out.stats->overflow_count;
     const uint32_t T = p.num_triangles;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < count;
@@ -541,7 +821,7 @@ __global__ __launch_bounds__(64) void k_overflow(const TriRec* __restrict__ recs
             bool first = true;
             float pending = 0.0f;
             while (pos < n) {
-                // next distinct value > prev (or >= -inf on the first pass) and its multiplicity
+                // next distinct value > prev (any value on the first pass) and its multiplicity
                 float cur = __builtin_inff();
                 uint64_t mult = 0;
                 for (uint32_t j = 0; j < T; ++j) {

@@ -6,12 +6,13 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
 #include <vector>
 
-#include "../../include/xrt.h"
+#include "xrt.h"
 #include "kernels/xrt_kernels.h"
 
 using namespace xrt;
@@ -32,6 +33,16 @@ struct xrt_context {
     DevStats* d_stats = nullptr;
     BlockStats* d_block_stats = nullptr;
     size_t block_stats_cap = 0;
+
+    // binning (XRT_KERNEL_BINNED)
+    uint32_t* d_bin_counts = nullptr;   // counts | offsets | cursor, 3 * (regions + 1)
+    size_t bin_counts_cap = 0;
+    uint32_t* d_bin_list = nullptr;
+    size_t bin_list_cap = 0;
+    uint32_t* d_global_list = nullptr;
+    size_t global_list_cap = 0;
+    size_t bin_list_want = 0;          // grown after a frame overflowed its lists
+    size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     uint32_t* d_overflow = nullptr;
     size_t overflow_cap = 0;
 
@@ -49,7 +60,7 @@ struct xrt_context {
     hipStream_t last_stream = nullptr;
     bool pending = false;
     int kernel = XRT_KERNEL_AUTO;
-    int last_kernel = XRT_KERNEL_TILED;
+    int last_kernel = XRT_KERNEL_BINNED;
     uint32_t hit_capacity = kMaxHits;
 };
 
@@ -126,6 +137,8 @@ RenderParams make_params(const xrt_camera& c, uint32_t row_begin, uint32_t row_e
     p.row_end = row_end;
     p.num_triangles = (uint32_t)T;
     p.hit_capacity = capacity;
+    const char* ab = std::getenv("XRT_ABLATE");   // timing studies only
+    p.ablate = ab ? (uint32_t)std::strtoul(ab, nullptr, 0) : 0u;
     return p;
 }
 
@@ -177,12 +190,17 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     const uint64_t T = ctx->num_tris;
     const uint32_t rows = row_end - row_begin;
     const uint64_t rays = (uint64_t)rows * cam->width;
-    const int kernel = ctx->kernel == XRT_KERNEL_BRUTE ? XRT_KERNEL_BRUTE : XRT_KERNEL_TILED;
+    // AUTO: the per-region footprint sweep costs T x regions box tests; past
+    // ~2e8 of them binning once per frame is cheaper (DESIGN.md "Kernels").
+    const uint64_t sweep = T * (uint64_t)((cam->width + kRegion - 1) / kRegion) * ((rows + kRegion - 1) / kRegion);
+    const int kernel = ctx->kernel != XRT_KERNEL_AUTO ? ctx->kernel
+                       : sweep > 200000000ull       ? XRT_KERNEL_BINNED
+                                                    : XRT_KERNEL_TILED;
+    const bool culled = kernel != XRT_KERNEL_BRUTE;
+    const bool binned = kernel == XRT_KERNEL_BINNED;
 
     if ((rc = ensure(ctx, ctx->d_recs, ctx->recs_cap, T))) return rc;
-    if (kernel == XRT_KERNEL_TILED &&
-        (rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes)))
-        return rc;
+    if (culled && (rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes))) return rc;
     if ((rc = ensure(ctx, ctx->d_overflow, ctx->overflow_cap, rays))) return rc;
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
@@ -200,13 +218,42 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if ((rc = ensure(ctx, ctx->d_block_stats, ctx->block_stats_cap, n_blocks))) return rc;
     out.block_stats = ctx->d_block_stats;
 
+    BinBuffers bins = {};
+    const uint32_t n_regions = rows ? grid.x * grid.y : 0u;
+    if (binned && rows) {
+        const size_t want = std::max<size_t>({ctx->bin_list_want, 4 * (size_t)T, (size_t)n_regions, 65536});
+        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, 3 * ((size_t)n_regions + 1)))) return rc;
+        if ((rc = ensure(ctx, ctx->d_bin_list, ctx->bin_list_cap, want))) return rc;
+        if ((rc = ensure(ctx, ctx->d_global_list, ctx->global_list_cap, T))) return rc;
+        bins.counts = ctx->d_bin_counts;
+        bins.offsets = ctx->d_bin_counts + (n_regions + 1);
+        bins.cursor = ctx->d_bin_counts + 2 * (n_regions + 1);
+        bins.list = ctx->d_bin_list;
+        bins.global_list = ctx->d_global_list;
+        bins.list_cap = (uint32_t)std::min<size_t>(ctx->bin_list_cap, 0xFFFFFFFFu);
+        if (ctx->bin_force_cap) bins.list_cap = (uint32_t)std::min<size_t>(bins.list_cap, ctx->bin_force_cap);
+        bins.regions_x = grid.x;
+        bins.regions_y = grid.y;
+        XRT_HIP(ctx, hipMemsetAsync(bins.counts, 0, sizeof(uint32_t) * n_regions, stream));
+    }
+
     XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
     if (T) {
         dim3 pg((unsigned)((T + 255) / 256));
         hipLaunchKernelGGL(k_prep, pg, dim3(256), 0, stream, ctx->d_tris, (uint32_t)T, p, cp,
-                           ctx->d_recs, kernel == XRT_KERNEL_TILED ? ctx->d_cull : nullptr);
+                           ctx->d_recs, culled ? ctx->d_cull : nullptr, bins, &ctx->d_stats->bin);
         XRT_HIP(ctx, hipGetLastError());
     }
+    if (binned && rows) {
+        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, stream, bins, &ctx->d_stats->bin);
+        XRT_HIP(ctx, hipGetLastError());
+        if (T) {
+            hipLaunchKernelGGL(k_bin_fill, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream,
+                               ctx->d_cull, p, bins, &ctx->d_stats->bin);
+            XRT_HIP(ctx, hipGetLastError());
+        }
+    }
+
     hipEvent_t t0 = ctx->ev_begin, t1 = ctx->ev_end;
     if (ctx->timing) {
         if (ctx->tev_used + 2 > ctx->tev.size()) {
@@ -223,21 +270,19 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (ctx->timing) XRT_HIP(ctx, hipEventRecord(ctx->ev_begin, stream));
     XRT_HIP(ctx, hipEventRecord(t0, stream));
     if (rows > 0) {
-        if (kernel == XRT_KERNEL_BRUTE) {
+        if (kernel == XRT_KERNEL_BRUTE)
             hipLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, ctx->d_recs, p, out);
-        } else {
-            hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs,
-                               ctx->d_cull, p, out);
-        }
+        else if (kernel == XRT_KERNEL_TILED)
+            hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p, out);
+        else
+            hipLaunchKernelGGL(k_render_binned, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p,
+                               out, bins, &ctx->d_stats->bin);
         XRT_HIP(ctx, hipGetLastError());
     }
     XRT_HIP(ctx, hipEventRecord(t1, stream));
     if (ctx->timing) XRT_HIP(ctx, hipEventRecord(ctx->ev_end, stream));
     if (rows > 0) {
-        hipLaunchKernelGGL(k_overflow, dim3(256), dim3(64), 0, stream, ctx->d_recs, p, out);
-        XRT_HIP(ctx, hipGetLastError());
-        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, ctx->d_block_stats,
-                           n_blocks, ctx->d_stats);
+        hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, stream, ctx->d_recs, p, out, n_blocks);
         XRT_HIP(ctx, hipGetLastError());
     }
     ctx->last_stream = stream;
@@ -294,6 +339,9 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_cull);
     (void)hipFree(ctx->d_stats);
     (void)hipFree(ctx->d_block_stats);
+    (void)hipFree(ctx->d_bin_counts);
+    (void)hipFree(ctx->d_bin_list);
+    (void)hipFree(ctx->d_global_list);
     (void)hipFree(ctx->d_overflow);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
@@ -378,7 +426,7 @@ int xrt_camera_from_bbox(const float lower[3], const float upper[3], uint32_t wi
 int xrt_set_kernel(xrt_context* ctx, int kernel)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
-    if (kernel < XRT_KERNEL_AUTO || kernel > XRT_KERNEL_TILED)
+    if (kernel < XRT_KERNEL_AUTO || kernel > XRT_KERNEL_BINNED)
         return fail(ctx, XRT_ERR_ARGUMENT, "unknown kernel");
     ctx->kernel = kernel;
     return XRT_OK;
@@ -389,6 +437,13 @@ int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity)
     if (!ctx) return XRT_ERR_ARGUMENT;
     if (capacity > (uint32_t)kMaxHits) return fail(ctx, XRT_ERR_ARGUMENT, "capacity > 16");
     ctx->hit_capacity = capacity ? capacity : (uint32_t)kMaxHits;
+    return XRT_OK;
+}
+
+int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    ctx->bin_force_cap = (size_t)entries;
     return XRT_OK;
 }
 
@@ -423,6 +478,8 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     stats->kernel_ms = ms;
     stats->candidates = s.candidates;
     stats->tile_tests = s.tile_tests;
+    if (s.bin.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
+        ctx->bin_list_want = std::max(ctx->bin_list_want, (size_t)s.bin.total + s.bin.total / 4 + 1024);
     return XRT_OK;
 }
 
@@ -550,8 +607,9 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     if ((rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes))) return rc;
     RenderParams p = make_params(*camera, 0, camera->height, T, ctx->hit_capacity);
     CullParams cp = make_cull_params(*camera);
+    BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull);
+                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull, nobins, &ctx->d_stats->bin);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, ctx->d_recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));

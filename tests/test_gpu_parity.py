@@ -16,8 +16,8 @@ from conftest import DRAGON, GOLDEN, ROOT, bits
 from test_oracle import kat_vectors
 
 pytestmark = pytest.mark.gpu
-KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED]
-KNAME = {xrt.XRT_KERNEL_BRUTE: "brute", xrt.XRT_KERNEL_TILED: "tiled"}
+KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED]
+KNAME = {xrt.XRT_KERNEL_BRUTE: "brute", xrt.XRT_KERNEL_TILED: "tiled", xrt.XRT_KERNEL_BINNED: "binned"}
 
 
 def cam13(cam):
@@ -132,17 +132,34 @@ def test_ragged_sizes_and_strips(ctx, dragon, kernel, W, H, r0, r1):
     assert_same(got, oracle.render_rows(dragon, cam, W, H, r0, r1), f"{KNAME[kernel]} {W}x{H}")
 
 
-def test_strips_assemble_to_full_image(ctx, dragon):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_strips_assemble_to_full_image(ctx, dragon, kernel):
     W = H = 160
-    full = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
+    full = render(ctx, dragon, W, H, kernel)
     for n in (2, 3, 8):
         rows_per, rem = divmod(H, n)
         parts, start = [], 0
         for g in range(n):
             end = start + rows_per + (1 if g < rem else 0)
-            parts.append(render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED, start, end)[0])
+            parts.append(render(ctx, dragon, W, H, kernel, start, end)[0])
             start = end
         assert np.array_equal(bits(np.concatenate(parts)), bits(full[0]))
+
+
+def test_binned_list_overflow_falls_back_exactly(ctx, dragon):
+    """Region lists capped at 16 entries: every region takes the whole-mesh path."""
+    cam = oracle.camera_for_mesh(dragon, 96, 96)
+    ref = oracle.render_rows(dragon, cam, 96, 96)
+    ctx.set_bin_capacity(16)
+    try:
+        got = render(ctx, dragon, 96, 96, xrt.XRT_KERNEL_BINNED)
+    finally:
+        ctx.set_bin_capacity(0)
+    assert got[3].candidates == 9 * len(dragon)     # 3x3 regions, each the whole mesh
+    assert_same(got, ref, "binned overflow")
+    again = render(ctx, dragon, 96, 96, xrt.XRT_KERNEL_BINNED)
+    assert again[3].candidates < 9 * len(dragon)
+    assert_same(again, ref, "binned")
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -205,14 +222,15 @@ def test_custom_camera_triangles_around_source(ctx, kernel):
     assert_same(got, ref, KNAME[kernel])
 
 
-def test_brute_equals_tiled_2048(ctx, dragon):
-    """Full 2048^2 frame: both kernels bit-identical; sampled rows vs the oracle;
-    SURVEY.md's dragon facts (hit rays, odd rays, max hits)."""
+def test_all_kernels_equal_2048(ctx, dragon):
+    """Full 2048^2 frame: the three kernels bit-identical; sampled rows vs the
+    oracle; SURVEY.md's dragon facts (hit rays, odd rays, max hits)."""
     W = H = 2048
-    a = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
-    b = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BRUTE)
-    for x, y in zip(a[:3], b[:3]):
-        assert np.array_equal(bits(x), bits(y))
+    a = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED)
+    for k in (xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BRUTE):
+        b = render(ctx, dragon, W, H, k)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(bits(x), bits(y)), KNAME[k]
     st = a[3]
     assert (st.hit_rays, st.odd_rays, st.max_hits) == (1365802, 24, 12)
     rows = [0, 255, 256, 511, 512, 1023, 1024, 1535, 1536, 1792, 2047]
@@ -230,9 +248,10 @@ def test_brute_equals_tiled_2048(ctx, dragon):
     assert np.all(a[1][~miss] >= 0) and np.all(a[0] <= np.float32(80.0)) and np.all(a[0] > 0)
 
 
-def test_tiled_4096_rows_vs_oracle(ctx, dragon):
+@pytest.mark.parametrize("kernel", [xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED])
+def test_culled_4096_rows_vs_oracle(ctx, dragon, kernel):
     W = H = 4096
-    img, lb, u8, st = render(ctx, dragon, W, H, xrt.XRT_KERNEL_TILED)
+    img, lb, u8, st = render(ctx, dragon, W, H, kernel)
     rows = [0, 511, 512, 2048, 3584, 4095]
     cam = oracle.camera_for_mesh(dragon, W, H)
     ref = oracle.render_row_list(dragon, cam, W, H, rows)
@@ -245,10 +264,11 @@ def test_tiled_mesh_1m_parity(ctx, dragon):
     big = tiled_mesh(dragon, 7)
     assert big.shape == (1120434, 9)
     W = H = 256
-    a = render(ctx, big, W, H, xrt.XRT_KERNEL_TILED)
-    b = render(ctx, big, W, H, xrt.XRT_KERNEL_BRUTE)
-    for x, y in zip(a[:3], b[:3]):
-        assert np.array_equal(bits(x), bits(y))
+    a = render(ctx, big, W, H, xrt.XRT_KERNEL_BINNED)
+    for k in (xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BRUTE):
+        b = render(ctx, big, W, H, k)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(bits(x), bits(y)), KNAME[k]
     rows = [37, 128]
     cam = oracle.camera_for_mesh(big, W, H)
     ref = oracle.render_row_list(big, cam, W, H, rows)
@@ -286,7 +306,7 @@ def test_cli_golden_text(tmp_path):
     """xrt_main (the reference's CLI over the GPU path) writes the golden text."""
     exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
     (tmp_path / "out").mkdir()
-    for kernel in ("brute", "tiled"):
+    for kernel in ("brute", "tiled", "binned"):
         r = subprocess.run([exe, "-s", "128", "128", "-i", DRAGON, "-f", f"d-{kernel}.txt", "-k", kernel],
                            capture_output=True, text=True, cwd=tmp_path, timeout=300)
         assert r.returncode == 0, r.stderr
