@@ -17,7 +17,13 @@
 
 #pragma clang fp contract(off)
 
-namespace xrt {
+// Variant builds (tools/build_variants.sh) get their own kernel namespace so
+// several can be loaded side by side without kernel-name collisions.
+#ifndef XRT_KERNEL_NS
+#define XRT_KERNEL_NS xrt
+#endif
+
+namespace XRT_KERNEL_NS {
 
 // Per-render triangle record: the ray-independent part of Ray::intersect
 // (src/Ray.cxx:86-122) for the shared ray origin.  64 bytes, read
@@ -288,4 +294,4 @@ __host__ __device__ __forceinline__ uint8_t lut_u8(float v)
     return (uint8_t)__builtin_round(255.0 * (double)(v - vmin) / (double)(vmax - vmin));
 }
 
-}  // namespace xrt
+}  // namespace XRT_KERNEL_NS

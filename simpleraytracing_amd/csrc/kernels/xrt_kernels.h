@@ -28,13 +28,15 @@
 #define XRT_BOUNDED_PUSH 0   // wave-bounded insertion network: measured slower
 #endif
 
-namespace xrt {
+namespace XRT_KERNEL_NS {
 
-struct BinState {            // zeroed per frame with DevStats
-    unsigned int global_count;
-    unsigned int total;
-    unsigned int overflow;   // total > list_cap: regions fall back to the whole mesh
-    unsigned int pad;
+// Binning control block (zeroed per binned frame, in front of the counts) and
+// the copy reported in DevStats.
+struct BinState {
+    unsigned int ticket;        // k_prep workgroups done
+    unsigned int global_count;  // triangles in the global list
+    unsigned int total;         // sum of the region counts
+    unsigned int overflow;      // total > list_cap: regions fall back to the whole mesh
 };
 
 struct DevStats {
@@ -441,6 +443,126 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
     store_block_stats(ws, n_cand, out.block_stats);
 }
 
+// Conservative footprint of one triangle (DESIGN.md "Tile cull").
+struct Footprint {
+    float4 bbox, e0, e1, e2;
+};
+
+__device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, const CullParams& cp)
+{
+    const float kInf = __builtin_inff();
+    Footprint c;
+    c.bbox = make_float4(-kInf, kInf, -kInf, kInf);   // never cull
+    c.e0 = make_float4(0.0f, 0.0f, kInf, 0.0f);
+    c.e1 = c.e0;
+    c.e2 = c.e0;
+
+    bool finite = isfinite(r.tnum) && isfinite(r.qvx) && isfinite(r.qvy) && isfinite(r.qvz);
+    if (finite && r.tnum == 0.0f) {
+        // t = 0 * inv_det is never > 1e-7: the triangle never contributes.
+        c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
+        c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
+        return c;
+    }
+    double E1[3] = {r.e1x, r.e1y, r.e1z};
+    double E2[3] = {r.e2x, r.e2y, r.e2z};
+    double TV[3] = {r.tvx, r.tvy, r.tvz};
+    double l1e1 = l1_d(E1), l1e2 = l1_d(E2), l1tv = l1_d(TV);
+    bool sane = finite && l1e1 > 0x1p-60 && l1e1 < 0x1p60 && l1e2 > 0x1p-60 && l1e2 < 0x1p60 &&
+                l1tv > 0x1p-60 && l1tv < 0x1p60;
+    if (!sane) {
+        return c;
+    }
+    double s = r.tnum > 0.0f ? 1.0 : -1.0;
+
+    double N[3][3];
+    cross_d(E2, TV, N[1]);     // a   = d . (edge2 x tvec)
+    cross_d(TV, E1, N[2]);     // b   = d . (tvec x edge1)
+    double Nd[3];
+    cross_d(E2, E1, Nd);       // det = d . (edge2 x edge1)
+    for (int k = 0; k < 3; ++k) N[0][k] = Nd[k] - N[1][k] - N[2][k];
+
+    double Ba = 32.0 * kEps * l1tv * l1e2;
+    double Bb = 32.0 * kEps * l1tv * l1e1;
+    double Bd = 32.0 * kEps * l1e1 * l1e2;
+    double Bx = 16.0 * kEps * l1e1 * l1e2;
+    double B[3] = {Bd + Ba + Bb + Bx, Ba + Bx, Bb + Bx};
+
+    double Cv[3] = {(double)p.cx - p.ox, (double)p.cy - p.oy, (double)p.cz - p.oz};
+    double Up[3] = {p.ux, p.uy, p.uz};
+    double Rt[3] = {p.rx, p.ry, p.rz};
+    double ps = p.spacing;
+    double cv = ps * (0.5 - cp.height / 2.0);
+    double cu = ps * (0.5 - cp.width / 2.0);
+
+    float ea[3], eb[3], ec[3];
+    bool constant_edge = false;
+    for (int k = 0; k < 3; ++k) {
+        double upn = dot_d(Up, N[k]);
+        double rtn = dot_d(Rt, N[k]);
+        double alpha = dot_d(Cv, N[k]) + cv * upn + cu * rtn;
+        double beta = ps * upn;    // per image row
+        double gamma = ps * rtn;   // per image column
+        double l1n = l1_d(N[k]);
+        double M = 4.0 * ((B[k] + 12.0 * kEps * l1n) * cp.dmax + 8.0 * kEps * cp.mag * l1n);
+        double nrm = sqrt(beta * beta + gamma * gamma);
+        if (!(nrm > 1e-30 * (fabs(alpha) + M + 1e-300))) {
+            // Edge function constant over the image plane.
+            if (s * alpha + M < 0.0) {
+                c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
+                c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
+                c.e1 = c.e2 = make_float4(0.0f, 0.0f, kInf, 0.0f);
+                return c;
+            }
+            ea[k] = 0.0f;
+            eb[k] = 0.0f;
+            ec[k] = kInf;
+            constant_edge = true;
+            continue;
+        }
+        double a = s * gamma / nrm;
+        double b = s * beta / nrm;
+        double cc = (s * alpha + M) / nrm;
+        cc += 0.05 + 64.0 * kEps * (cp.width + cp.height + fabs(cc));
+        ea[k] = (float)a;
+        eb[k] = (float)b;
+        ec[k] = (float)cc;
+    }
+    c.e0 = make_float4(ea[0], eb[0], ec[0], 0.0f);
+    c.e1 = make_float4(ea[1], eb[1], ec[1], 0.0f);
+    c.e2 = make_float4(ea[2], eb[2], ec[2], 0.0f);
+
+    if (!constant_edge) {
+        // Loosened triangle {a_k x + b_k y + c_k >= 0}: bounded iff the inward
+        // normals positively span the plane (cross products share a sign).
+        double A[3] = {ea[0], ea[1], ea[2]}, Bq[3] = {eb[0], eb[1], eb[2]}, Cq[3] = {ec[0], ec[1], ec[2]};
+        double x01 = A[0] * Bq[1] - A[1] * Bq[0];
+        double x12 = A[1] * Bq[2] - A[2] * Bq[1];
+        double x20 = A[2] * Bq[0] - A[0] * Bq[2];
+        const double tiny = 1e-9;
+        bool pos = x01 > tiny && x12 > tiny && x20 > tiny;
+        bool neg = x01 < -tiny && x12 < -tiny && x20 < -tiny;
+        if (pos || neg) {
+            double vx[3], vy[3];
+            const int pi[3] = {0, 1, 2}, pj[3] = {1, 2, 0};
+            const double cr[3] = {x01, x12, x20};
+            for (int q = 0; q < 3; ++q) {
+                int ii = pi[q], jj = pj[q];
+                vx[q] = (-Cq[ii] * Bq[jj] + Cq[jj] * Bq[ii]) / cr[q];
+                vy[q] = (-A[ii] * Cq[jj] + A[jj] * Cq[ii]) / cr[q];
+            }
+            double xmin = fmin(vx[0], fmin(vx[1], vx[2])), xmax = fmax(vx[0], fmax(vx[1], vx[2]));
+            double ymin = fmin(vy[0], fmin(vy[1], vy[2])), ymax = fmax(vy[0], fmax(vy[1], vy[2]));
+            double sx = 0.01 + 1e-4 * (fabs(xmin) + fabs(xmax));
+            double sy = 0.01 + 1e-4 * (fabs(ymin) + fabs(ymax));
+            if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax))
+                c.bbox = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy),
+                                     (float)(ymax + sy));
+        }
+    }
+    return c;
+}
+
 // ---------------------------------------------------------------------------
 // Binning (k_render_binned): footprints are assigned to 32x32 regions once per
 // frame -- count (in k_prep), scan, fill -- so each region's workgroup reads
@@ -497,189 +619,86 @@ __device__ __forceinline__ void for_each_region(const RenderParams& p, const Bin
     }
 }
 
-// Counting pass, run per triangle right after its footprint is known.
-__device__ __forceinline__ void bin_count(uint32_t j, float4 bb, float4 e0, float4 e1, float4 e2,
-                                          const RenderParams& p, const BinBuffers& bins,
-                                          BinState* bs)
+// ---------------------------------------------------------------------------
+// Binning with workgroup-local aggregation.  A workgroup's 256 consecutive
+// triangles are spatially coherent, so their (region, triangle) pairs fall in
+// a few regions: they are counted (and later given list slots) in an LDS hash
+// table, and each distinct region costs one global atomic per workgroup
+// instead of one per pair -- same-address global atomics serialise in L2.
+// Keys that do not find a slot within kProbe probes take the direct global
+// path (consistently in both passes: slots are never freed).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHash = 1024;
+constexpr uint32_t kProbe = 32;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+struct BinHash {
+    uint32_t key[kHash];
+    uint32_t cnt[kHash];
+    uint32_t base[kHash];
+    uint32_t last;          // this workgroup took the last ticket
+};
+
+__device__ __forceinline__ uint32_t hash_insert(BinHash& h, uint32_t key)
 {
-    uint32_t x0, x1, y0, y1;
-    if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return;
+    uint32_t s = (key * 2654435761u) >> 22;
+    for (uint32_t probe = 0; probe < kProbe; ++probe) {
+        const uint32_t old = atomicCAS(&h.key[s], kEmpty, key);
+        if (old == kEmpty || old == key) return s;
+        s = (s + 1u) & (kHash - 1u);
+    }
+    return kEmpty;
+}
+
+__device__ __forceinline__ uint32_t hash_find(const BinHash& h, uint32_t key)
+{
+    uint32_t s = (key * 2654435761u) >> 22;
+    for (uint32_t probe = 0; probe < kProbe; ++probe) {
+        const uint32_t k = h.key[s];
+        if (k == key) return s;
+        if (k == kEmpty) return kEmpty;
+        s = (s + 1u) & (kHash - 1u);
+    }
+    return kEmpty;
+}
+
+__device__ __forceinline__ void hash_clear(BinHash& h)
+{
+    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) {
+        h.key[k] = kEmpty;
+        h.cnt[k] = 0u;
+    }
+}
+
+// Region rectangle of a footprint; false when the triangle is in no region
+// list (no region, or in the global list -- `global` tells which).
+__device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const BinBuffers& bins,
+                                         uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1,
+                                         bool& global)
+{
+    global = false;
+    if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return false;
     if ((uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1) > kGlobalRegions) {
-        bins.global_list[atomicAdd(&bs->global_count, 1u)] = j;
-        return;
+        global = true;
+        return false;
     }
-    for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2,
-                    [&](uint32_t r) { atomicAdd(&bins.counts[r], 1u); });
+    return true;
 }
 
-// ---------------------------------------------------------------------------
-// k_prep
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
-                                              RenderParams p, CullParams cp,
-                                              TriRec* __restrict__ recs,
-                                              float4* __restrict__ culls, BinBuffers bins,
-                                              BinState* __restrict__ bs)
+// Exclusive scan of the region counts by one workgroup (the last k_prep one).
+__device__ void scan_regions(const BinBuffers& bins, BinState* __restrict__ bs, DevStats* __restrict__ st,
+                             uint32_t* s_part)
 {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= T) return;
-    const float* P = tris + 9ull * i;
-    float p1x = P[0], p1y = P[1], p1z = P[2];
-    float p2x = P[3], p2y = P[4], p2z = P[5];
-    float p3x = P[6], p3y = P[7], p3z = P[8];
-
-    // Exactly the reference's f32 operations (Ray.cxx:86-87, 102, 112, 122).
-    TriRec r;
-    r.e1x = p2x - p1x; r.e1y = p2y - p1y; r.e1z = p2z - p1z;
-    r.e2x = p3x - p1x; r.e2y = p3y - p1y; r.e2z = p3z - p1z;
-    r.tvx = p.ox - p1x; r.tvy = p.oy - p1y; r.tvz = p.oz - p1z;
-    r.qvx = r.tvy * r.e1z - r.tvz * r.e1y;
-    r.qvy = r.tvz * r.e1x - r.tvx * r.e1z;
-    r.qvz = r.tvx * r.e1y - r.tvy * r.e1x;
-    r.tnum = (r.e2x * r.qvx + r.e2y * r.qvy) + r.e2z * r.qvz;
-    r.pad0 = r.pad1 = r.pad2 = 0.0f;
-    recs[i] = r;
-    if (!culls) return;
-
-    // --- conservative footprint (DESIGN.md "Tile cull") ---------------------
-    const float kInf = __builtin_inff();
-    struct {
-        float4 bbox, e0, e1, e2;
-    } c;
-    c.bbox = make_float4(-kInf, kInf, -kInf, kInf);   // never cull
-    c.e0 = make_float4(0.0f, 0.0f, kInf, 0.0f);
-    c.e1 = c.e0;
-    c.e2 = c.e0;
-    auto store = [&]() {
-        culls[i] = c.bbox;
-        culls[(size_t)T + i] = c.e0;
-        culls[2 * (size_t)T + i] = c.e1;
-        culls[3 * (size_t)T + i] = c.e2;
-        if (bins.counts) bin_count(i, c.bbox, c.e0, c.e1, c.e2, p, bins, bs);
-    };
-
-    bool finite = isfinite(r.tnum) && isfinite(r.qvx) && isfinite(r.qvy) && isfinite(r.qvz);
-    if (finite && r.tnum == 0.0f) {
-        // t = 0 * inv_det is never > 1e-7: the triangle never contributes.
-        c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
-        c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
-        store();
-        return;
-    }
-    double E1[3] = {r.e1x, r.e1y, r.e1z};
-    double E2[3] = {r.e2x, r.e2y, r.e2z};
-    double TV[3] = {r.tvx, r.tvy, r.tvz};
-    double l1e1 = l1_d(E1), l1e2 = l1_d(E2), l1tv = l1_d(TV);
-    bool sane = finite && l1e1 > 0x1p-60 && l1e1 < 0x1p60 && l1e2 > 0x1p-60 && l1e2 < 0x1p60 &&
-                l1tv > 0x1p-60 && l1tv < 0x1p60;
-    if (!sane) {
-        store();
-        return;
-    }
-    double s = r.tnum > 0.0f ? 1.0 : -1.0;
-
-    double N[3][3];
-    cross_d(E2, TV, N[1]);     // a   = d . (edge2 x tvec)
-    cross_d(TV, E1, N[2]);     // b   = d . (tvec x edge1)
-    double Nd[3];
-    cross_d(E2, E1, Nd);       // det = d . (edge2 x edge1)
-    for (int k = 0; k < 3; ++k) N[0][k] = Nd[k] - N[1][k] - N[2][k];
-
-    double Ba = 32.0 * kEps * l1tv * l1e2;
-    double Bb = 32.0 * kEps * l1tv * l1e1;
-    double Bd = 32.0 * kEps * l1e1 * l1e2;
-    double Bx = 16.0 * kEps * l1e1 * l1e2;
-    double B[3] = {Bd + Ba + Bb + Bx, Ba + Bx, Bb + Bx};
-
-    double Cv[3] = {(double)p.cx - p.ox, (double)p.cy - p.oy, (double)p.cz - p.oz};
-    double Up[3] = {p.ux, p.uy, p.uz};
-    double Rt[3] = {p.rx, p.ry, p.rz};
-    double ps = p.spacing;
-    double cv = ps * (0.5 - cp.height / 2.0);
-    double cu = ps * (0.5 - cp.width / 2.0);
-
-    float ea[3], eb[3], ec[3];
-    bool constant_edge = false;
-    for (int k = 0; k < 3; ++k) {
-        double upn = dot_d(Up, N[k]);
-        double rtn = dot_d(Rt, N[k]);
-        double alpha = dot_d(Cv, N[k]) + cv * upn + cu * rtn;
-        double beta = ps * upn;    // per image row
-        double gamma = ps * rtn;   // per image column
-        double l1n = l1_d(N[k]);
-        double M = 4.0 * ((B[k] + 12.0 * kEps * l1n) * cp.dmax + 8.0 * kEps * cp.mag * l1n);
-        double nrm = sqrt(beta * beta + gamma * gamma);
-        if (!(nrm > 1e-30 * (fabs(alpha) + M + 1e-300))) {
-            // Edge function constant over the image plane.
-            if (s * alpha + M < 0.0) {
-                c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
-                c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
-                c.e1 = c.e2 = make_float4(0.0f, 0.0f, kInf, 0.0f);
-                store();
-                return;
-            }
-            ea[k] = 0.0f;
-            eb[k] = 0.0f;
-            ec[k] = kInf;
-            constant_edge = true;
-            continue;
-        }
-        double a = s * gamma / nrm;
-        double b = s * beta / nrm;
-        double cc = (s * alpha + M) / nrm;
-        cc += 0.05 + 64.0 * kEps * (cp.width + cp.height + fabs(cc));
-        ea[k] = (float)a;
-        eb[k] = (float)b;
-        ec[k] = (float)cc;
-    }
-    c.e0 = make_float4(ea[0], eb[0], ec[0], 0.0f);
-    c.e1 = make_float4(ea[1], eb[1], ec[1], 0.0f);
-    c.e2 = make_float4(ea[2], eb[2], ec[2], 0.0f);
-
-    if (!constant_edge) {
-        // Loosened triangle {a_k x + b_k y + c_k >= 0}: bounded iff the inward
-        // normals positively span the plane (cross products share a sign).
-        double A[3] = {ea[0], ea[1], ea[2]}, Bq[3] = {eb[0], eb[1], eb[2]}, Cq[3] = {ec[0], ec[1], ec[2]};
-        double x01 = A[0] * Bq[1] - A[1] * Bq[0];
-        double x12 = A[1] * Bq[2] - A[2] * Bq[1];
-        double x20 = A[2] * Bq[0] - A[0] * Bq[2];
-        const double tiny = 1e-9;
-        bool pos = x01 > tiny && x12 > tiny && x20 > tiny;
-        bool neg = x01 < -tiny && x12 < -tiny && x20 < -tiny;
-        if (pos || neg) {
-            double vx[3], vy[3];
-            const int pi[3] = {0, 1, 2}, pj[3] = {1, 2, 0};
-            const double cr[3] = {x01, x12, x20};
-            for (int q = 0; q < 3; ++q) {
-                int ii = pi[q], jj = pj[q];
-                vx[q] = (-Cq[ii] * Bq[jj] + Cq[jj] * Bq[ii]) / cr[q];
-                vy[q] = (-A[ii] * Cq[jj] + A[jj] * Cq[ii]) / cr[q];
-            }
-            double xmin = fmin(vx[0], fmin(vx[1], vx[2])), xmax = fmax(vx[0], fmax(vx[1], vx[2]));
-            double ymin = fmin(vy[0], fmin(vy[1], vy[2])), ymax = fmax(vy[0], fmax(vy[1], vy[2]));
-            double sx = 0.01 + 1e-4 * (fabs(xmin) + fabs(xmax));
-            double sy = 0.01 + 1e-4 * (fabs(ymin) + fabs(ymax));
-            if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax))
-                c.bbox = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy),
-                                     (float)(ymax + sy));
-        }
-    }
-    store();
-}
-
-// Single-workgroup exclusive scan of the region counts.
-__global__ __launch_bounds__(1024) void k_bin_scan(BinBuffers bins, BinState* __restrict__ bs)
-{
-    __shared__ uint32_t s_part[1024];
     const uint32_t n = bins.regions_x * bins.regions_y;
-    const uint32_t per = (n + 1023u) / 1024u;
+    const uint32_t nt = blockDim.x;
+    const uint32_t per = (n + nt - 1u) / nt;
     const uint32_t b = threadIdx.x * per, e = min(b + per, n);
     uint32_t sum = 0;
     for (uint32_t i = b; i < e; ++i) sum += bins.counts[i];
     s_part[threadIdx.x] = sum;
     __syncthreads();
-    for (uint32_t off = 1; off < 1024u; off <<= 1) {     // Hillis-Steele inclusive scan
-        uint32_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
+    for (uint32_t off = 1; off < nt; off <<= 1) {     // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
         __syncthreads();
         s_part[threadIdx.x] += v;
         __syncthreads();
@@ -690,27 +709,138 @@ __global__ __launch_bounds__(1024) void k_bin_scan(BinBuffers bins, BinState* __
         bins.cursor[i] = run;
         run += bins.counts[i];
     }
-    if (threadIdx.x == 1023u) {
-        bins.offsets[n] = s_part[1023];
-        bs->total = s_part[1023];
-        bs->overflow = s_part[1023] > bins.list_cap ? 1u : 0u;
+    if (threadIdx.x == nt - 1u) {
+        const uint32_t total = s_part[nt - 1u];
+        bins.offsets[n] = total;
+        bs->total = total;
+        bs->overflow = total > bins.list_cap ? 1u : 0u;
+        st->bin.total = total;
+        st->bin.overflow = bs->overflow;
+        st->bin.global_count = bs->global_count;
     }
 }
 
-// Fill pass: one thread per triangle appends it to its regions' lists.
+// ---------------------------------------------------------------------------
+// k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
+// terms), cull planes, and (binned) the region counts; the workgroup that
+// finishes last scans them.  Thread 0 also clears DevStats for the frame.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
+                                              RenderParams p, CullParams cp,
+                                              TriRec* __restrict__ recs,
+                                              float4* __restrict__ culls, BinBuffers bins,
+                                              BinState* __restrict__ bs, DevStats* __restrict__ st)
+{
+    __shared__ BinHash h;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < T;
+    if (i == 0 && st) {
+        DevStats z = {};
+        *st = z;
+    }
+    Footprint fp;
+    if (valid) {
+        const float* P = tris + 9ull * i;
+        float p1x = P[0], p1y = P[1], p1z = P[2];
+        float p2x = P[3], p2y = P[4], p2z = P[5];
+        float p3x = P[6], p3y = P[7], p3z = P[8];
+        // Exactly the reference's f32 operations (Ray.cxx:86-87, 102, 112, 122).
+        TriRec r;
+        r.e1x = p2x - p1x; r.e1y = p2y - p1y; r.e1z = p2z - p1z;
+        r.e2x = p3x - p1x; r.e2y = p3y - p1y; r.e2z = p3z - p1z;
+        r.tvx = p.ox - p1x; r.tvy = p.oy - p1y; r.tvz = p.oz - p1z;
+        r.qvx = r.tvy * r.e1z - r.tvz * r.e1y;
+        r.qvy = r.tvz * r.e1x - r.tvx * r.e1z;
+        r.qvz = r.tvx * r.e1y - r.tvy * r.e1x;
+        r.tnum = (r.e2x * r.qvx + r.e2y * r.qvy) + r.e2z * r.qvz;
+        r.pad0 = r.pad1 = r.pad2 = 0.0f;
+        recs[i] = r;
+        if (culls) {
+            fp = compute_footprint(r, p, cp);
+            culls[i] = fp.bbox;
+            culls[(size_t)T + i] = fp.e0;
+            culls[2 * (size_t)T + i] = fp.e1;
+            culls[3 * (size_t)T + i] = fp.e2;
+        }
+    }
+    if (!bins.counts) return;                      // kernel-uniform
+
+    // --- count (region, triangle) pairs --------------------------------------
+    hash_clear(h);
+    __syncthreads();
+    uint32_t x0, x1, y0, y1;
+    bool global = false;
+    if (valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global)) {
+        for_each_region(p, bins, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, [&](uint32_t r) {
+            const uint32_t slot = hash_insert(h, r);
+            if (slot != kEmpty) atomicAdd(&h.cnt[slot], 1u);
+            else atomicAdd(&bins.counts[r], 1u);
+        });
+    }
+    if (valid && global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x)
+        if (h.key[k] != kEmpty) atomicAdd(&bins.counts[h.key[k]], h.cnt[k]);
+
+    // --- last workgroup scans (release/acquire at agent scope, G16) ----------
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        h.last = atomicAdd(&bs->ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!h.last) return;                           // workgroup-uniform
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    scan_regions(bins, bs, st, h.cnt);
+}
+
+// Fill pass: one thread per triangle.  Pass A counts the workgroup's pairs per
+// region in the LDS table; one global atomic per distinct region reserves a
+// contiguous slot range; pass B writes the triangle ids into it.
 __global__ __launch_bounds__(256) void k_bin_fill(const float4* __restrict__ culls, RenderParams p,
                                                   BinBuffers bins, const BinState* __restrict__ bs)
 {
+    __shared__ BinHash h;
+    if (bs->overflow) return;                      // kernel-uniform
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t T = p.num_triangles;
-    if (j >= T || bs->overflow) return;
-    float4 bb = culls[j];
+    const bool valid = j < T;
+    hash_clear(h);
+    __syncthreads();
     uint32_t x0, x1, y0, y1;
-    if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return;
-    if ((uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1) > kGlobalRegions) return;   // in the global list
-    float4 e0 = culls[(size_t)T + j], e1 = culls[2 * (size_t)T + j], e2 = culls[3 * (size_t)T + j];
-    for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2,
-                    [&](uint32_t r) { bins.list[atomicAdd(&bins.cursor[r], 1u)] = j; });
+    bool global = false;
+    float4 bb = make_float4(1.0f, -1.0f, 1.0f, -1.0f), e0 = bb, e1 = bb, e2 = bb;
+    bool has = false;
+    if (valid) {
+        bb = culls[j];
+        has = bin_rect(bb, p, bins, x0, x1, y0, y1, global);
+        if (has) {
+            e0 = culls[(size_t)T + j];
+            e1 = culls[2 * (size_t)T + j];
+            e2 = culls[3 * (size_t)T + j];
+        }
+    }
+    if (has)
+        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) {
+            const uint32_t slot = hash_insert(h, r);
+            if (slot != kEmpty) atomicAdd(&h.cnt[slot], 1u);
+            else bins.list[atomicAdd(&bins.cursor[r], 1u)] = j;   // crowded table: direct
+        });
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) {
+        if (h.key[k] != kEmpty) h.base[k] = atomicAdd(&bins.cursor[h.key[k]], h.cnt[k]);
+        h.cnt[k] = 0u;
+    }
+    __syncthreads();
+    if (has)
+        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) {
+            const uint32_t slot = hash_find(h, r);
+            if (slot != kEmpty) bins.list[h.base[slot] + atomicAdd(&h.cnt[slot], 1u)] = j;
+        });
 }
 
 __global__ __launch_bounds__(256) void k_render_binned(const TriRec* __restrict__ recs,
@@ -904,4 +1034,4 @@ __global__ void k_probe_math(int op, const float* __restrict__ in, float* __rest
     outp[i] = y;
 }
 
-}  // namespace xrt
+}  // namespace XRT_KERNEL_NS

@@ -15,7 +15,7 @@
 #include "xrt.h"
 #include "kernels/xrt_kernels.h"
 
-using namespace xrt;
+using namespace XRT_KERNEL_NS;
 
 struct xrt_context {
     int device = 0;
@@ -35,7 +35,7 @@ struct xrt_context {
     size_t block_stats_cap = 0;
 
     // binning (XRT_KERNEL_BINNED)
-    uint32_t* d_bin_counts = nullptr;   // counts | offsets | cursor, 3 * (regions + 1)
+    uint32_t* d_bin_counts = nullptr;   // BinState | counts | offsets | cursor (regions + 1 each)
     size_t bin_counts_cap = 0;
     uint32_t* d_bin_list = nullptr;
     size_t bin_list_cap = 0;
@@ -219,39 +219,43 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.block_stats = ctx->d_block_stats;
 
     BinBuffers bins = {};
+    BinState* bin_ctl = nullptr;
     const uint32_t n_regions = rows ? grid.x * grid.y : 0u;
     if (binned && rows) {
         const size_t want = std::max<size_t>({ctx->bin_list_want, 4 * (size_t)T, (size_t)n_regions, 65536});
-        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, 3 * ((size_t)n_regions + 1)))) return rc;
+        const size_t ctl_words = sizeof(BinState) / sizeof(uint32_t);
+        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, ctl_words + 3 * ((size_t)n_regions + 1))))
+            return rc;
         if ((rc = ensure(ctx, ctx->d_bin_list, ctx->bin_list_cap, want))) return rc;
         if ((rc = ensure(ctx, ctx->d_global_list, ctx->global_list_cap, T))) return rc;
-        bins.counts = ctx->d_bin_counts;
-        bins.offsets = ctx->d_bin_counts + (n_regions + 1);
-        bins.cursor = ctx->d_bin_counts + 2 * (n_regions + 1);
+        bin_ctl = reinterpret_cast<BinState*>(ctx->d_bin_counts);
+        bins.counts = ctx->d_bin_counts + ctl_words;
+        bins.offsets = bins.counts + (n_regions + 1);
+        bins.cursor = bins.counts + 2 * (n_regions + 1);
         bins.list = ctx->d_bin_list;
         bins.global_list = ctx->d_global_list;
         bins.list_cap = (uint32_t)std::min<size_t>(ctx->bin_list_cap, 0xFFFFFFFFu);
         if (ctx->bin_force_cap) bins.list_cap = (uint32_t)std::min<size_t>(bins.list_cap, ctx->bin_force_cap);
         bins.regions_x = grid.x;
         bins.regions_y = grid.y;
-        XRT_HIP(ctx, hipMemsetAsync(bins.counts, 0, sizeof(uint32_t) * n_regions, stream));
+        // control block + counts in one clear
+        XRT_HIP(ctx, hipMemsetAsync(ctx->d_bin_counts, 0, sizeof(uint32_t) * (ctl_words + n_regions), stream));
     }
 
-    XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
-    if (T) {
+    if (T) {   // k_prep clears DevStats for the frame
         dim3 pg((unsigned)((T + 255) / 256));
         hipLaunchKernelGGL(k_prep, pg, dim3(256), 0, stream, ctx->d_tris, (uint32_t)T, p, cp,
-                           ctx->d_recs, culled ? ctx->d_cull : nullptr, bins, &ctx->d_stats->bin);
+                           ctx->d_recs, culled ? ctx->d_cull : nullptr, bins, bin_ctl, ctx->d_stats);
         XRT_HIP(ctx, hipGetLastError());
+    } else {
+        XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
+        if (binned && rows)   // no k_prep to scan: empty lists
+            XRT_HIP(ctx, hipMemsetAsync(bins.offsets, 0, sizeof(uint32_t) * (n_regions + 1), stream));
     }
-    if (binned && rows) {
-        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, stream, bins, &ctx->d_stats->bin);
+    if (binned && rows && T) {
+        hipLaunchKernelGGL(k_bin_fill, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream,
+                           ctx->d_cull, p, bins, bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
-        if (T) {
-            hipLaunchKernelGGL(k_bin_fill, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream,
-                               ctx->d_cull, p, bins, &ctx->d_stats->bin);
-            XRT_HIP(ctx, hipGetLastError());
-        }
     }
 
     hipEvent_t t0 = ctx->ev_begin, t1 = ctx->ev_end;
@@ -276,7 +280,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p, out);
         else
             hipLaunchKernelGGL(k_render_binned, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p,
-                               out, bins, &ctx->d_stats->bin);
+                               out, bins, bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
     }
     XRT_HIP(ctx, hipEventRecord(t1, stream));
@@ -609,7 +613,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull, nobins, &ctx->d_stats->bin);
+                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull, nobins, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, ctx->d_recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));

@@ -79,10 +79,14 @@ def main():
             if r > 0:   # round 0 is warm-up
                 times[name].append(ms.value / n.value)
             out = img.cpu().numpy().view(np.uint32)
-            if ref is None:
-                ref = out.copy()
-            elif not np.array_equal(out, ref):
-                print(f"WARNING: variant {name} output differs", file=sys.stderr)
+            csum = int(out.astype(np.uint64).sum())
+            if r == 0:
+                pass                       # warm-up round: not timed, not compared
+            elif ref is None:
+                ref = csum
+            elif csum != ref:
+                print(f"WARNING: round {r} variant {name} checksum {csum} != {ref}", file=sys.stderr)
+            img.fill_(-1.0)
     res = {name: {"median_ms": statistics.median(v), "min_ms": min(v)} for name, v in times.items()}
     print(json.dumps({"kernel": args.kernel, "size": [W, H], "results": res}))
 
