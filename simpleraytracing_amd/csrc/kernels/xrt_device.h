@@ -7,8 +7,9 @@
 //     pragma below); the only fused ops are the explicit fma() calls of
 //     glibc's expf, which are part of that function's definition;
 //   * f32 sqrt is correctly rounded (HIP's default
-//     -fhip-fp32-correctly-rounded-divide-sqrt); 1/det is computed as
-//     (float)(1.0/(double)det) exactly as src/Ray.cxx:99 writes it;
+//     -fhip-fp32-correctly-rounded-divide-sqrt); src/Ray.cxx:99's
+//     (float)(1.0/(double)det) is the correctly rounded f32 1.0f/det for
+//     every det (inv_det_of);
 //   * f32 denormals are preserved (no -fgpu-flush-denormals-to-zero).
 #pragma once
 
@@ -21,6 +22,26 @@
 // several can be loaded side by side without kernel-name collisions.
 #ifndef XRT_KERNEL_NS
 #define XRT_KERNEL_NS xrt
+#endif
+
+// Compile-time variants for A/B timing (tools/build_variants.sh, tools/ab.py);
+// the defaults are the measured-faster choices.
+#ifndef XRT_MED3
+#define XRT_MED3 1        // med3 insertion (else the compare-exchange chain)
+#endif
+#ifndef XRT_PAIR
+#define XRT_PAIR 1        // culled kernels test survivors two at a time
+#endif
+#ifndef XRT_WAVES_PER_EU
+#define XRT_WAVES_PER_EU 0   // >0: occupancy hint for the culled render kernels
+#endif
+#ifndef XRT_STAMPS
+#define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
+#endif
+#if XRT_WAVES_PER_EU > 0
+#define XRT_CULLED_ATTR __attribute__((amdgpu_waves_per_eu(XRT_WAVES_PER_EU, 8)))
+#else
+#define XRT_CULLED_ATTR
 #endif
 
 namespace XRT_KERNEL_NS {
@@ -66,6 +87,8 @@ constexpr uint32_t kAblateSweep = 2;        // tiled: no phase-1 footprint sweep
 constexpr uint32_t kAblateRayGen = 4;       // constant ray direction
 constexpr uint32_t kAblateStores = 8;       // no output stores
 constexpr uint32_t kAblateShade = 16;       // no expf / LUT
+constexpr uint32_t kAblateExact = 32;       // culled kernels: no Moller-Trumbore for survivors
+constexpr uint32_t kAblatePush = 64;        // culled kernels: exact test but no hit-list insert
 
 constexpr int kMaxHits = 16;
 
@@ -106,6 +129,22 @@ __device__ __forceinline__ void make_ray(const RenderParams& p, uint32_t row, ui
 // `u < 0 || u > 1` test (Ray.cxx:106) provably rejects, so the f64 division
 // runs only for candidates (DESIGN.md "Early reject").
 // ---------------------------------------------------------------------------
+// Ray.cxx:99 computes (float)(1.0 / (double)det).  For every f32 det that is
+// the correctly rounded f32 quotient 1.0f / det: 1/det is never within 2^-49
+// (relative) of an f32 rounding midpoint, so the f64 rounding cannot move it
+// across one.  Checked on all 2^32 inputs (tools/check_fp_identities.c,
+// tests/test_abi.py); the f32 division sequence is about half the f64 one.
+__device__ __forceinline__ float inv_det_of(float det) { return 1.0f / det; }
+
+// Branch-free Ray::intersect for the culled kernels, whose survivors almost
+// always have a hitting lane (so the early reject would not skip the wave's
+// division): the same comparisons as mt_intersect, combined with no control
+// flow so two tests can be interleaved.  `hit` includes accept_t.
+__device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1x, float e1y,
+                                         float e1z, float e2x, float e2y, float e2z, float tvx,
+                                         float tvy, float tvz, float qvx, float qvy, float qvz,
+                                         float tnum, bool& hit);
+
 __device__ __forceinline__ bool mt_intersect(float dx, float dy, float dz,
                                              float e1x, float e1y, float e1z,
                                              float e2x, float e2y, float e2z,
@@ -132,7 +171,7 @@ __device__ __forceinline__ bool mt_intersect(float dx, float dy, float dz,
     if (A < D * -0x1p-20f || A > D * 0x1.00001p0f) return false;
 
     if (det == 0.0f) return false;                        // Ray.cxx:94 (fpclassify FP_ZERO)
-    float inv_det = (float)(1.0 / (double)det);           // Ray.cxx:99
+    float inv_det = inv_det_of(det);                      // Ray.cxx:99
     float u = a * inv_det;                                // Ray.cxx:105
     if (u < 0.0f || u > 1.0f) return false;               // Ray.cxx:106
     float v = ((dx * qvx + dy * qvy) + dz * qvz) * inv_det;   // Ray.cxx:115
@@ -141,8 +180,26 @@ __device__ __forceinline__ bool mt_intersect(float dx, float dy, float dz,
     return true;
 }
 
-// t > 0.0000001 in double, main.cxx:687
-__device__ __forceinline__ bool accept_t(float t) { return (double)t > 0.0000001; }
+// main.cxx:687: (double)t > 0.0000001.  For f32 t that is t > 0x1.ad7f28p-24f,
+// the largest float not above 1e-7 (all 2^32 inputs: tools/check_fp_identities.c).
+__device__ __forceinline__ bool accept_t(float t) { return t > 0x1.ad7f28p-24f; }
+
+__device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1x, float e1y,
+                                         float e1z, float e2x, float e2y, float e2z, float tvx,
+                                         float tvy, float tvz, float qvx, float qvy, float qvz,
+                                         float tnum, bool& hit)
+{
+    const float px = dy * e2z - dz * e2y;                 // Ray.cxx:90
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    const float det = (e1x * px + e1y * py) + e1z * pz;   // Ray.cxx:93
+    const float inv_det = inv_det_of(det);                // Ray.cxx:99
+    const float u = ((tvx * px + tvy * py) + tvz * pz) * inv_det;    // Ray.cxx:105
+    const float v = ((dx * qvx + dy * qvy) + dz * qvz) * inv_det;    // Ray.cxx:115
+    const float t = tnum * inv_det;                       // Ray.cxx:122
+    hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
+    return t;
+}
 
 // ---------------------------------------------------------------------------
 // Per-ray sorted hit list in registers (static indices only).  Replaces the
@@ -159,41 +216,38 @@ struct HitList {
         n = 0;
     }
 
-    // Insertion keeps h[0..min(n,K)) ascending; +inf sentinels fill the rest.
-    // `bound` is a wave-uniform upper bound of n (the number of pushes the
-    // wave has issued): entries at or above it are still sentinels, so the
-    // compare-exchange chain stops there (the chains are unrolled statically).
-    __device__ __forceinline__ void insert_upto(float t, uint32_t bound)
+    // Keeps h ascending with +inf sentinels.  With h sorted, inserting x gives
+    // h'[k] = max(h[k-1], min(h[k], x)) = med3(h[k-1], h[k], x) (old values):
+    // one independent v_med3_f32 per slot instead of a compare-exchange chain.
+    // A miss inserts +inf, which leaves h unchanged.  hit == false or x > 0.
+    __device__ __forceinline__ void push_if(bool hit, float t)
     {
-        if (bound < 4u) {
-            insert_n<4>(t);
-        } else if (bound < 8u) {
-            insert_n<8>(t);
-        } else if (bound < 12u) {
-            insert_n<12>(t);
-        } else {
-            insert_n<kMaxHits>(t);
-        }
-        ++n;
-    }
-
-    template <int N>
-    __device__ __forceinline__ void insert_n(float t)
-    {
+#if !XRT_MED3
+        if (hit) {
 #pragma unroll
-        for (int k = 0; k < N; ++k) {
-            float cur = h[k];
-            bool lt = t < cur;
-            h[k] = lt ? t : cur;
-            t = lt ? cur : t;
+            for (int k = 0; k < kMaxHits; ++k) {
+                const float cur = h[k];
+                const bool lt = t < cur;
+                h[k] = lt ? t : cur;
+                t = lt ? cur : t;
+            }
+            ++n;
         }
+        return;
+#endif
+        const float x = hit ? t : __builtin_inff();
+        float prev = h[0];
+        h[0] = fminf(prev, x);
+#pragma unroll
+        for (int k = 1; k < kMaxHits; ++k) {
+            const float cur = h[k];
+            h[k] = __builtin_amdgcn_fmed3f(prev, cur, x);
+            prev = cur;
+        }
+        n += hit ? 1u : 0u;
     }
 
-    __device__ __forceinline__ void push(float t)
-    {
-        insert_n<kMaxHits>(t);
-        ++n;
-    }
+    __device__ __forceinline__ void push(float t) { push_if(true, t); }
 
     // main.cxx:703-708: pairwise sum of the sorted list, sequential f32.
     __device__ __forceinline__ float path_length() const
@@ -291,7 +345,11 @@ __host__ __device__ __forceinline__ uint8_t lut_u8(float v)
     if (v < vmin) return 0;
     if (v > vmax) return 255;
     if (v != v) return 0;
-    return (uint8_t)__builtin_round(255.0 * (double)(v - vmin) / (double)(vmax - vmin));
+    // 255.0 * v / 80.0 == v * 3.1875 exactly: 255*v is exact in f64 and the
+    // quotient 51*v/16 has at most 30 significant bits, so the correctly
+    // rounded division returns it unchanged (checked for every f32 in
+    // [0, 80]: tools/check_fp_identities.c).
+    return (uint8_t)__builtin_round((double)(v - vmin) * 3.1875);
 }
 
 }  // namespace XRT_KERNEL_NS

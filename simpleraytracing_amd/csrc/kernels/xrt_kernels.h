@@ -22,11 +22,6 @@
 
 #include "xrt_device.h"
 
-// Compile-time variants for A/B timing (tools/ab.py); the defaults are the
-// measured-faster choices.
-#ifndef XRT_BOUNDED_PUSH
-#define XRT_BOUNDED_PUSH 0   // wave-bounded insertion network: measured slower
-#endif
 
 namespace XRT_KERNEL_NS {
 
@@ -123,8 +118,19 @@ __device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t 
 
 // Combines the block's wave counters through LDS and stores one BlockStats.
 // Must be reached by every thread of the block.
+// XRT_STAMPS builds (diagnostics only) overwrite rays/hit_rays/max_hits/pad
+// with the workgroup's s_memrealtime start/end, XCC id and HW_ID register.
+__device__ __forceinline__ uint64_t block_start_stamp()
+{
+#if XRT_STAMPS
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
+
 __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
-                                                  BlockStats* out)
+                                                  BlockStats* out, uint64_t t_start = 0)
 {
     __shared__ WaveStats s_ws[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -153,6 +159,14 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
             b.max_hits = b.max_hits > s_ws[w].lane_max ? b.max_hits : s_ws[w].lane_max;
         }
         b.candidates = candidates;
+#if XRT_STAMPS
+        b.rays = t_start;
+        b.hit_rays = __builtin_amdgcn_s_memrealtime();
+        b.pad = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
+        b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+#else
+        (void)t_start;
+#endif
         out[blockIdx.y * gridDim.x + blockIdx.x] = b;
     }
 }
@@ -185,15 +199,22 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         }
         return;
     }
-    float photon = shade(distance);
+    // distance 0 (a miss or an odd count) shades to 80 * expf(-0) = 80 -> 255;
+    // the wave skips expf and the LUT when none of its rays needs them.
+    float photon = 80.0f;
+    uint8_t u8 = 255u;
+    if (__ballot(distance != 0.0f)) {
+        photon = shade(distance);
+        u8 = lut_u8(photon);
+    }
     if (out.image) out.image[o] = photon;
     if (out.lbuffer) out.lbuffer[o] = lval;
-    if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+    if (out.image_u8) out.image_u8[o] = u8;
 }
 
 // Loads one triangle record with a wave-uniform index (scalar loads).
 __device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
-                                            float dy, float dz, HitList& hl, uint32_t& pushes)
+                                            float dy, float dz, HitList& hl)
 {
     const float4* q = reinterpret_cast<const float4*>(recs + j);
     float4 a = q[0], b = q[1], c = q[2], d = q[3];
@@ -201,12 +222,7 @@ __device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uin
     const bool hit =
         mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
         accept_t(t);
-#if XRT_BOUNDED_PUSH
-    if (hit) hl.insert_upto(t, pushes);
-    pushes += __ballot(hit) != 0ull ? 1u : 0u;
-#else
-    if (hit) hl.push(t);
-#endif
+    hl.push_if(hit, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -226,8 +242,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     HitList hl;
     hl.init();
     const uint32_t T = p.num_triangles;
-    uint32_t pushes = 0;
-    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl, pushes);
+    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
     WaveStats ws = {};
     ws.tile_tests = T;
     finish_ray(p, out, active, row, col, hl, ws);
@@ -239,7 +254,9 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
 constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
-constexpr uint32_t kGlobalRegions = 64; // footprints over more regions go to the global list
+constexpr uint32_t kGlobalRegions = 1u << 20; // footprints over more regions go to the global list
+constexpr uint32_t kSerialRegions = 16;       // larger rectangles are enumerated by the whole workgroup
+constexpr uint32_t kBig = 64;                 // cooperative rectangles per workgroup
 
 // Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
 // function a*col + b*row + c.
@@ -298,9 +315,20 @@ __device__ __forceinline__ void stage_candidates(StageLDS& st, const TriRec* __r
     }
 }
 
+__device__ __forceinline__ float test_lds(const StageLDS& st, uint32_t k, float dx, float dy,
+                                          float dz, bool& hit)
+{
+    const float4 a = st.r0[k], b = st.r1[k], c = st.r2[k];
+    return mt_exact(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w,
+                    st.tnum[k], hit);
+}
+
+// Survivors are tested two at a time (independent dependency chains for the
+// scheduler to interleave), then pushed in ascending staged order.  The hit
+// set, and so the sorted list, does not depend on the pairing.
 __device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t count, float xc,
                                                 float yc, float dx, float dy, float dz, HitList& hl,
-                                                uint32_t& pushes)
+                                                uint32_t ablate)
 {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t tests = 0;
@@ -309,21 +337,24 @@ __device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t cou
         const bool pass = k < count && edges_pass(st.e0[k], st.e1[k], st.e2[k], xc, yc, 3.5f, 3.5f);
         unsigned long long m = __ballot(pass);
         tests += (uint32_t)__popcll(m);
+        if (ablate & kAblateExact) m = 0ull;
         while (m) {
-            const uint32_t kk = base + (uint32_t)__builtin_ctzll(m);
+            const uint32_t k0 = base + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            const float4 a = st.r0[kk], b = st.r1[kk], c = st.r2[kk];
-            const float tn = st.tnum[kk];
-            float t;
-            const bool hit = mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x,
-                                          c.y, c.z, c.w, tn, t) &&
-                             accept_t(t);
-#if XRT_BOUNDED_PUSH
-            if (hit) hl.insert_upto(t, pushes);
-            pushes += __ballot(hit) != 0ull ? 1u : 0u;
-#else
-            if (hit) hl.push(t);
-#endif
+            bool h0, h1 = false;
+            const float t0 = test_lds(st, k0, dx, dy, dz, h0);
+            float t1 = 0.0f;
+            if (XRT_PAIR && m) {                              // wave-uniform
+                const uint32_t k1 = base + (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                t1 = test_lds(st, k1, dx, dy, dz, h1);
+            }
+            if (ablate & kAblatePush) {
+                hl.n += (h0 ? 1u : 0u) + (h1 ? 1u : 0u);
+            } else {
+                hl.push_if(h0, t0);
+                hl.push_if(h1, t1);
+            }
         }
     }
     return tests;
@@ -359,16 +390,16 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         else dx = 1.0f;
         HitList hl;
         hl.init();
-        uint32_t tests = 0, pushes = 0;
+        uint32_t tests = 0;
         if (once) {
-            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, pushes);
+            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, p.ablate);
         } else {
             for (uint32_t first = 0; first < n_cand; first += kStage) {
                 const uint32_t count = min(kStage, n_cand - first);
                 __syncthreads();
                 stage_candidates(st, recs, culls, T, first, count, fetch);
                 __syncthreads();
-                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, pushes);
+                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, p.ablate);
             }
         }
         if (tile_live) {
@@ -381,13 +412,14 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
 // k_render_tiled: one 32x32 region per workgroup.  Phase 1: the 256 lanes
 // sweep the footprint boxes of the whole mesh (every region sees every
 // triangle) and compact the region's candidates into an LDS list.
-__global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__ recs,
+__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriRec* __restrict__ recs,
                                                       const float4* __restrict__ culls,
                                                       RenderParams p, Outputs out)
 {
     __shared__ uint32_t s_list[kListCap];
     __shared__ uint32_t s_count;
     __shared__ StageLDS st;
+    const uint64_t t_start = block_start_stamp();
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -440,7 +472,7 @@ __global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__
                             [&](uint32_t k) { return s_list[k]; }, ws, st);
     else   // list overflow: every triangle is a candidate (still exact)
         render_region_tiles(p, out, recs, culls, rx0, ry0, T, [](uint32_t k) { return k; }, ws, st);
-    store_block_stats(ws, n_cand, out.block_stats);
+    store_block_stats(ws, n_cand, out.block_stats, t_start);
 }
 
 // Conservative footprint of one triangle (DESIGN.md "Tile cull").
@@ -575,6 +607,7 @@ struct BinBuffers {
     uint32_t* cursor;        // [n_regions]            fill cursors
     uint32_t* list;          // [list_cap]             region candidate lists
     uint32_t* global_list;   // [T]
+    uint32_t* order;         // [n_regions] launch order: regions by descending log2(count); null = identity
     uint32_t list_cap;
     uint32_t regions_x, regions_y;
 };
@@ -685,6 +718,62 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
     return true;
 }
 
+// Rectangles of more than kSerialRegions regions are queued per workgroup (in
+// thread order, so both binning passes queue the same triangles) and their
+// regions are enumerated by all lanes together; past kBig queued rectangles a
+// triangle goes to the global list (decided identically in both passes).
+struct BigItem {
+    float4 e0, e1, e2;
+    uint32_t j, x0, x1, y0, y1, pad0, pad1, pad2;
+};
+
+struct BigList {
+    BigItem item[kBig];
+    uint32_t wave_count[4];
+    uint32_t n;
+};
+
+// Returns the queue slot of this thread's big rectangle (kEmpty if none or full).
+__device__ __forceinline__ uint32_t big_slot(BigList& big, bool is_big)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(is_big);
+    if (lane == 0) big.wave_count[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+        if (w < wave) before += big.wave_count[w];
+        total += big.wave_count[w];
+    }
+    if (threadIdx.x == 0) big.n = total < kBig ? total : kBig;
+    const uint32_t slot = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    return is_big && slot < kBig ? slot : kEmpty;
+}
+
+// Calls f(region, triangle) for every region pair of the workgroup's triangles:
+// small rectangles serially per lane, queued big ones cooperatively.
+template <typename F>
+__device__ __forceinline__ void for_each_pair(const RenderParams& p, const BinBuffers& bins,
+                                              BigList& big, bool has, uint32_t j, uint32_t x0,
+                                              uint32_t x1, uint32_t y0, uint32_t y1, float4 e0,
+                                              float4 e1, float4 e2, bool queued, F f)
+{
+    if (has && !queued)
+        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) { f(r, j); });
+    __syncthreads();
+    for (uint32_t b = 0; b < big.n; ++b) {
+        const BigItem it = big.item[b];
+        const uint32_t wr = it.x1 - it.x0 + 1u;
+        const uint32_t area = wr * (it.y1 - it.y0 + 1u);
+        for (uint32_t k = threadIdx.x; k < area; k += blockDim.x) {
+            const uint32_t rx = it.x0 + k % wr, ry = it.y0 + k / wr;
+            const float xc = (float)(rx * kRegion) + 15.5f;
+            const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
+            if (edges_pass(it.e0, it.e1, it.e2, xc, yc, 15.5f, 15.5f)) f(ry * bins.regions_x + rx, it.j);
+        }
+    }
+}
+
 // Exclusive scan of the region counts by one workgroup (the last k_prep one).
 __device__ void scan_regions(const BinBuffers& bins, BinState* __restrict__ bs, DevStats* __restrict__ st,
                              uint32_t* s_part)
@@ -708,6 +797,28 @@ __device__ void scan_regions(const BinBuffers& bins, BinState* __restrict__ bs, 
         bins.offsets[i] = run;
         bins.cursor[i] = run;
         run += bins.counts[i];
+    }
+    // Launch order, heaviest regions first (longest-job-first keeps the dense
+    // middle of the image from starting last and setting the kernel's tail):
+    // a counting sort on 32 - clz(count), descending.  Order within a bucket
+    // is unspecified; results do not depend on the order.
+    if (bins.order) {
+        uint32_t* s_bucket = s_part + nt;          // [33] counts, then cursors
+        if (threadIdx.x < 33u) s_bucket[threadIdx.x] = 0u;
+        __syncthreads();
+        for (uint32_t i = b; i < e; ++i) atomicAdd(&s_bucket[32 - __clz(bins.counts[i])], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int k = 32; k >= 0; --k) {
+                const uint32_t c = s_bucket[k];
+                s_bucket[k] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = b; i < e; ++i)
+            bins.order[atomicAdd(&s_bucket[32 - __clz(bins.counts[i])], 1u)] = i;
     }
     if (threadIdx.x == nt - 1u) {
         const uint32_t total = s_part[nt - 1u];
@@ -766,18 +877,27 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     if (!bins.counts) return;                      // kernel-uniform
 
     // --- count (region, triangle) pairs --------------------------------------
+    __shared__ BigList big;
     hash_clear(h);
-    __syncthreads();
-    uint32_t x0, x1, y0, y1;
+    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
-    if (valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global)) {
-        for_each_region(p, bins, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, [&](uint32_t r) {
-            const uint32_t slot = hash_insert(h, r);
-            if (slot != kEmpty) atomicAdd(&h.cnt[slot], 1u);
-            else atomicAdd(&bins.counts[r], 1u);
-        });
+    const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
+    const bool is_big = has && (x1 - x0 + 1u) * (y1 - y0 + 1u) > kSerialRegions;
+    const uint32_t slot = big_slot(big, is_big);          // contains a barrier
+    if (slot != kEmpty) {
+        BigItem it;
+        it.e0 = fp.e0; it.e1 = fp.e1; it.e2 = fp.e2;
+        it.j = i; it.x0 = x0; it.x1 = x1; it.y0 = y0; it.y1 = y1;
+        big.item[slot] = it;
     }
-    if (valid && global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
+    const bool to_global = global || (is_big && slot == kEmpty);
+    for_each_pair(p, bins, big, has && !to_global, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2,
+                  slot != kEmpty, [&](uint32_t r, uint32_t) {
+                      const uint32_t hs = hash_insert(h, r);
+                      if (hs != kEmpty) atomicAdd(&h.cnt[hs], 1u);
+                      else atomicAdd(&bins.counts[r], 1u);
+                  });
+    if (valid && to_global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x)
         if (h.key[k] != kEmpty) atomicAdd(&bins.counts[h.key[k]], h.cnt[k]);
@@ -805,53 +925,63 @@ __global__ __launch_bounds__(256) void k_bin_fill(const float4* __restrict__ cul
                                                   BinBuffers bins, const BinState* __restrict__ bs)
 {
     __shared__ BinHash h;
+    __shared__ BigList big;
     if (bs->overflow) return;                      // kernel-uniform
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t T = p.num_triangles;
     const bool valid = j < T;
     hash_clear(h);
-    __syncthreads();
-    uint32_t x0, x1, y0, y1;
-    bool global = false;
-    float4 bb = make_float4(1.0f, -1.0f, 1.0f, -1.0f), e0 = bb, e1 = bb, e2 = bb;
-    bool has = false;
+    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+    bool global = false, has = false;
+    float4 e0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), e1 = e0, e2 = e0;
     if (valid) {
-        bb = culls[j];
-        has = bin_rect(bb, p, bins, x0, x1, y0, y1, global);
+        has = bin_rect(culls[j], p, bins, x0, x1, y0, y1, global);
         if (has) {
             e0 = culls[(size_t)T + j];
             e1 = culls[2 * (size_t)T + j];
             e2 = culls[3 * (size_t)T + j];
         }
     }
-    if (has)
-        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) {
-            const uint32_t slot = hash_insert(h, r);
-            if (slot != kEmpty) atomicAdd(&h.cnt[slot], 1u);
-            else bins.list[atomicAdd(&bins.cursor[r], 1u)] = j;   // crowded table: direct
-        });
+    const bool is_big = has && (x1 - x0 + 1u) * (y1 - y0 + 1u) > kSerialRegions;
+    const uint32_t slot = big_slot(big, is_big);          // same queue as k_prep's
+    if (slot != kEmpty) {
+        BigItem it;
+        it.e0 = e0; it.e1 = e1; it.e2 = e2;
+        it.j = j; it.x0 = x0; it.x1 = x1; it.y0 = y0; it.y1 = y1;
+        big.item[slot] = it;
+    }
+    const bool live = has && !(is_big && slot == kEmpty);  // else it is in the global list
+    // pass A: count per region in LDS (crowded table: write directly)
+    for_each_pair(p, bins, big, live, j, x0, x1, y0, y1, e0, e1, e2, slot != kEmpty,
+                  [&](uint32_t r, uint32_t t) {
+                      const uint32_t hs = hash_insert(h, r);
+                      if (hs != kEmpty) atomicAdd(&h.cnt[hs], 1u);
+                      else bins.list[atomicAdd(&bins.cursor[r], 1u)] = t;
+                  });
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) {
         if (h.key[k] != kEmpty) h.base[k] = atomicAdd(&bins.cursor[h.key[k]], h.cnt[k]);
         h.cnt[k] = 0u;
     }
     __syncthreads();
-    if (has)
-        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) {
-            const uint32_t slot = hash_find(h, r);
-            if (slot != kEmpty) bins.list[h.base[slot] + atomicAdd(&h.cnt[slot], 1u)] = j;
-        });
+    // pass B: the slots
+    for_each_pair(p, bins, big, live, j, x0, x1, y0, y1, e0, e1, e2, slot != kEmpty,
+                  [&](uint32_t r, uint32_t t) {
+                      const uint32_t hs = hash_find(h, r);
+                      if (hs != kEmpty) bins.list[h.base[hs] + atomicAdd(&h.cnt[hs], 1u)] = t;
+                  });
 }
 
-__global__ __launch_bounds__(256) void k_render_binned(const TriRec* __restrict__ recs,
+__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_binned(const TriRec* __restrict__ recs,
                                                        const float4* __restrict__ culls,
                                                        RenderParams p, Outputs out, BinBuffers bins,
                                                        const BinState* __restrict__ bs)
 {
     __shared__ StageLDS st;
-    const uint32_t region = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t rx0 = blockIdx.x * kRegion;
-    const uint32_t ry0 = p.row_begin + blockIdx.y * kRegion;
+    const uint64_t t_start = block_start_stamp();
+    const uint32_t region = bins.order ? bins.order[blockIdx.x] : blockIdx.x;   // 1-D grid
+    const uint32_t rx0 = (region % bins.regions_x) * kRegion;
+    const uint32_t ry0 = p.row_begin + (region / bins.regions_x) * kRegion;
     WaveStats ws = {};
     uint32_t n_cand;
     if (bs->overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
@@ -866,7 +996,7 @@ __global__ __launch_bounds__(256) void k_render_binned(const TriRec* __restrict_
         render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand,
                             [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws, st);
     }
-    store_block_stats(ws, n_cand, out.block_stats);
+    store_block_stats(ws, n_cand, out.block_stats, t_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -1028,7 +1158,7 @@ __global__ void k_probe_math(int op, const float* __restrict__ in, float* __rest
     switch (op) {
     case 0: y = xrt_expf(x); break;
     case 1: y = sqrtf(x); break;
-    case 2: y = (float)(1.0 / (double)x); break;
+    case 2: y = inv_det_of(x); break;
     default: y = (float)lut_u8(x); break;
     }
     outp[i] = y;

@@ -33,6 +33,7 @@ struct xrt_context {
     DevStats* d_stats = nullptr;
     BlockStats* d_block_stats = nullptr;
     size_t block_stats_cap = 0;
+    uint32_t last_blocks = 0;          // workgroups of the last render (diagnostics)
 
     // binning (XRT_KERNEL_BINNED)
     uint32_t* d_bin_counts = nullptr;   // BinState | counts | offsets | cursor (regions + 1 each)
@@ -216,6 +217,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
                     : dim3((cam->width + kRegion - 1) / kRegion, (rows + kRegion - 1) / kRegion);
     const uint32_t n_blocks = rows ? grid.x * grid.y : 0u;
     if ((rc = ensure(ctx, ctx->d_block_stats, ctx->block_stats_cap, n_blocks))) return rc;
+    ctx->last_blocks = n_blocks;
     out.block_stats = ctx->d_block_stats;
 
     BinBuffers bins = {};
@@ -224,7 +226,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (binned && rows) {
         const size_t want = std::max<size_t>({ctx->bin_list_want, 4 * (size_t)T, (size_t)n_regions, 65536});
         const size_t ctl_words = sizeof(BinState) / sizeof(uint32_t);
-        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, ctl_words + 3 * ((size_t)n_regions + 1))))
+        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, ctl_words + 4 * ((size_t)n_regions + 1))))
             return rc;
         if ((rc = ensure(ctx, ctx->d_bin_list, ctx->bin_list_cap, want))) return rc;
         if ((rc = ensure(ctx, ctx->d_global_list, ctx->global_list_cap, T))) return rc;
@@ -232,6 +234,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         bins.counts = ctx->d_bin_counts + ctl_words;
         bins.offsets = bins.counts + (n_regions + 1);
         bins.cursor = bins.counts + 2 * (n_regions + 1);
+        bins.order = T ? bins.counts + 3 * (n_regions + 1) : nullptr;   // written by k_prep's scan
         bins.list = ctx->d_bin_list;
         bins.global_list = ctx->d_global_list;
         bins.list_cap = (uint32_t)std::min<size_t>(ctx->bin_list_cap, 0xFFFFFFFFu);
@@ -279,8 +282,8 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         else if (kernel == XRT_KERNEL_TILED)
             hipLaunchKernelGGL(k_render_tiled, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p, out);
         else
-            hipLaunchKernelGGL(k_render_binned, grid, dim3(256), 0, stream, ctx->d_recs, ctx->d_cull, p,
-                               out, bins, bin_ctl);
+            hipLaunchKernelGGL(k_render_binned, dim3(n_regions), dim3(256), 0, stream, ctx->d_recs,
+                               ctx->d_cull, p, out, bins, bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
     }
     XRT_HIP(ctx, hipEventRecord(t1, stream));
@@ -448,6 +451,20 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->bin_force_cap = (size_t)entries;
+    return XRT_OK;
+}
+
+int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint64_t* n_records)
+{
+    if (!ctx || !n_records) return XRT_ERR_ARGUMENT;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    if (ctx->pending) {
+        XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+        ctx->pending = false;
+    }
+    *n_records = ctx->last_blocks;
+    const size_t bytes = std::min<size_t>((size_t)capacity, (size_t)ctx->last_blocks * sizeof(BlockStats));
+    if (bytes && dst) XRT_HIP(ctx, hipMemcpy(dst, ctx->d_block_stats, bytes, hipMemcpyDeviceToHost));
     return XRT_OK;
 }
 

@@ -130,3 +130,13 @@ def test_cli_without_gpu_reports_error(tmp_path):
     r = subprocess.run([exe, "-s", "8", "8", "-i", DRAGON, "-f", "x.txt"], capture_output=True,
                        text=True, cwd=tmp_path)
     assert r.returncode == 1 and r.stderr.startswith("ERROR:")
+
+
+def test_fp_identities_exhaustive(tmp_path):
+    """The f32 identities the device code uses (inv_det_of, accept_t, lut_u8),
+    checked on every f32 input by tools/check_fp_identities.c."""
+    src = os.path.join(ROOT, "tools", "check_fp_identities.c")
+    exe = str(tmp_path / "cfi")
+    subprocess.run(["gcc", "-O2", "-o", exe, src, "-lm"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr

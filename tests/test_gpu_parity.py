@@ -78,12 +78,29 @@ def test_probe_sqrt_correctly_rounded(ctx):
 
 
 def test_probe_reciprocal_matches_double_division(ctx):
-    x = special_floats()
-    got = ctx.probe_math(_abi.XRT_PROBE_RCP, x)
-    with np.errstate(divide="ignore", over="ignore"):
-        want = (1.0 / x.astype(np.float64)).astype(np.float32)
-    same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
-    assert same.all(), x[~same][:8]
+    # the device's 1.0f / det against Ray.cxx:99's (float)(1.0 / (double)det)
+    # (identical for every f32: tools/check_fp_identities.c); specials plus a
+    # stride-61 sweep of all 2^32 bit patterns
+    sweep = np.arange(0, 1 << 32, 61, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    for x in (special_floats(), sweep):
+        for c in range(0, x.size, 1 << 25):
+            xc = x[c:c + (1 << 25)]
+            got = ctx.probe_math(_abi.XRT_PROBE_RCP, xc)
+            with np.errstate(divide="ignore", over="ignore"):
+                want = (1.0 / xc.astype(np.float64)).astype(np.float32)
+            same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+            assert same.all(), xc[~same][:8]
+
+
+def test_probe_lut_sweep(ctx):
+    # every 13th f32 in [0, 80] against Image.inl:195-211's formula in f64
+    # (round half away from zero == floor(x + 0.5) here, exactly)
+    v = np.arange(0, 0x42A00001, 13, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    for c in range(0, v.size, 1 << 24):
+        vc = v[c:c + (1 << 24)]
+        got = ctx.probe_math(_abi.XRT_PROBE_LUT_U8, vc)
+        want = np.floor(255.0 * vc.astype(np.float64) / 80.0 + 0.5).astype(np.float32)
+        assert np.array_equal(got, want), vc[got != want][:8]
 
 
 def test_probe_lut(ctx):
