@@ -57,7 +57,7 @@ typedef enum xrt_status {
 
 /* Kernel selection. */
 typedef enum xrt_kernel {
-    XRT_KERNEL_AUTO = 0,    /* TILED, or BINNED when T x regions > 2e8 */
+    XRT_KERNEL_AUTO = 0,    /* TILED, or BINNED when T x regions > 2e7 */
     XRT_KERNEL_BRUTE = 1,   /* every ray tests every triangle (renderLoop as written) */
     XRT_KERNEL_TILED = 2,   /* every 32x32 region sweeps every triangle's conservative
                                footprint; per 8x8 ray tile the survivors of a relaxed

@@ -25,13 +25,13 @@
 
 namespace XRT_KERNEL_NS {
 
-// Binning control block (zeroed per binned frame, in front of the counts) and
-// the copy reported in DevStats.
+// Binning control block.  Zero on entry to a binned frame: it is cleared when
+// allocated and by every binned frame's k_finish for the next one.
 struct BinState {
-    unsigned int ticket;        // k_prep workgroups done
+    unsigned int pair_count;    // (triangle, region) pairs emitted by k_prep
     unsigned int global_count;  // triangles in the global list
-    unsigned int total;         // sum of the region counts
-    unsigned int overflow;      // total > list_cap: regions fall back to the whole mesh
+    unsigned int total;         // sum of the region counts (k_bin_scan)
+    unsigned int overflow;      // pairs > capacity: regions fall back to the whole mesh
 };
 
 struct DevStats {
@@ -222,7 +222,7 @@ __device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uin
     const bool hit =
         mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
         accept_t(t);
-    hl.push_if(hit, t);
+    if (__ballot(hit)) hl.push_if(hit, t);   // wave-uniform: most tests miss on every lane
 }
 
 // ---------------------------------------------------------------------------
@@ -480,6 +480,48 @@ struct Footprint {
     float4 bbox, e0, e1, e2;
 };
 
+// Box of the loosened triangle when it is unbounded (its inward normals do not
+// positively span the plane, e.g. a sliver seen edge-on): the bounding box of
+// {A_k x + B_k y + C_k >= 0, k < 3} inside the image rectangle [-1, W] x
+// [-1, H] in pixel-centre coordinates.  That set is a convex polygon whose
+// vertices are intersections of two of its seven boundary lines; candidate
+// vertices are accepted with a generous tolerance (so the box can only grow).
+// Leaves `box` unchanged (unbounded: never culled by the box) if none is found.
+__device__ void clipped_box(const double A[3], const double B[3], const double C[3], double W,
+                            double H, float4& box)
+{
+    const double LA[7] = {A[0], A[1], A[2], 1.0, -1.0, 0.0, 0.0};
+    const double LB[7] = {B[0], B[1], B[2], 0.0, 0.0, 1.0, -1.0};
+    const double LC[7] = {C[0], C[1], C[2], 1.0, W, 1.0, H};
+    double xmin = __builtin_inf(), xmax = -__builtin_inf();
+    double ymin = __builtin_inf(), ymax = -__builtin_inf();
+    bool any = false;
+    for (int a = 0; a < 7; ++a) {
+        for (int b = a + 1; b < 7; ++b) {
+            const double det = LA[a] * LB[b] - LA[b] * LB[a];
+            const double scale = (fabs(LA[a]) + fabs(LB[a])) * (fabs(LA[b]) + fabs(LB[b]));
+            if (!(fabs(det) > 1e-9 * scale)) continue;           // parallel (or NaN)
+            const double x = (LB[a] * LC[b] - LB[b] * LC[a]) / det;
+            const double y = (LA[b] * LC[a] - LA[a] * LC[b]) / det;
+            bool ok = isfinite(x) && isfinite(y);
+            for (int k = 0; k < 7 && ok; ++k) {
+                const double v = LA[k] * x + LB[k] * y + LC[k];
+                const double tol = 1e-6 * (fabs(LA[k] * x) + fabs(LB[k] * y) + fabs(LC[k])) + 1e-6;
+                ok = v >= -tol;
+            }
+            if (ok) {
+                xmin = fmin(xmin, x); xmax = fmax(xmax, x);
+                ymin = fmin(ymin, y); ymax = fmax(ymax, y);
+                any = true;
+            }
+        }
+    }
+    if (!any) return;
+    const double sx = 0.01 + 1e-4 * (fabs(xmin) + fabs(xmax));
+    const double sy = 0.01 + 1e-4 * (fabs(ymin) + fabs(ymax));
+    box = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy), (float)(ymax + sy));
+}
+
 __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, const CullParams& cp)
 {
     const float kInf = __builtin_inff();
@@ -590,27 +632,38 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
             if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax))
                 c.bbox = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy),
                                      (float)(ymax + sy));
+        } else {
+            clipped_box(A, Bq, Cq, cp.width, cp.height, c.bbox);
         }
     }
     return c;
 }
 
 // ---------------------------------------------------------------------------
-// Binning (k_render_binned): footprints are assigned to 32x32 regions once per
-// frame -- count (in k_prep), scan, fill -- so each region's workgroup reads
-// only its own candidates.  Footprints covering more than kGlobalRegions
-// regions (or unbounded ones) go to a global list every region reads.
+// Binning (XRT_KERNEL_BINNED): the conservative footprints are assigned to
+// 32x32 regions once per frame, in three wide stages with no serial tail:
+//   k_prep      per triangle: footprint, then its (triangle, region) pairs
+//               are appended to a flat pair array (one atomic per workgroup
+//               reserves the range) and counted per region (no-return atomics);
+//   k_bin_scan  one workgroup: region list offsets and the launch order
+//               (regions by descending candidate count, in log2 buckets);
+//   k_bin_fill  one thread per pair: scatter into the region lists.
+// Footprints over more than kGlobalRegions regions go to a global list every
+// region reads.
 // ---------------------------------------------------------------------------
 struct BinBuffers {
-    uint32_t* counts;        // [n_regions]            zeroed before k_prep
-    uint32_t* offsets;       // [n_regions + 1]        exclusive scan of counts
-    uint32_t* cursor;        // [n_regions]            fill cursors
-    uint32_t* list;          // [list_cap]             region candidate lists
+    uint32_t* counts;        // [n_regions]   zero on entry to a binned frame
+    uint2* spans;            // [n_regions]   (list offset, count) per region
+    uint32_t* cursor;        // [n_regions]   fill cursors
+    uint4* slots;            // [n_regions]   launch order: (region, offset, count, global count)
+    uint2* pairs;            // [cap]         (triangle, region) in emission order
+    uint32_t* list;          // [cap]         region candidate lists
     uint32_t* global_list;   // [T]
-    uint32_t* order;         // [n_regions] launch order: regions by descending log2(count); null = identity
-    uint32_t list_cap;
+    uint32_t cap;            // capacity of pairs and list
     uint32_t regions_x, regions_y;
 };
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
 // footprint box may touch; false when it touches none.
@@ -649,57 +702,6 @@ __device__ __forceinline__ void for_each_region(const RenderParams& p, const Bin
             const float xc = (float)(rx * kRegion) + 15.5f;
             if (edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f)) f(ry * bins.regions_x + rx);
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Binning with workgroup-local aggregation.  A workgroup's 256 consecutive
-// triangles are spatially coherent, so their (region, triangle) pairs fall in
-// a few regions: they are counted (and later given list slots) in an LDS hash
-// table, and each distinct region costs one global atomic per workgroup
-// instead of one per pair -- same-address global atomics serialise in L2.
-// Keys that do not find a slot within kProbe probes take the direct global
-// path (consistently in both passes: slots are never freed).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kHash = 1024;
-constexpr uint32_t kProbe = 32;
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-
-struct BinHash {
-    uint32_t key[kHash];
-    uint32_t cnt[kHash];
-    uint32_t base[kHash];
-    uint32_t last;          // this workgroup took the last ticket
-};
-
-__device__ __forceinline__ uint32_t hash_insert(BinHash& h, uint32_t key)
-{
-    uint32_t s = (key * 2654435761u) >> 22;
-    for (uint32_t probe = 0; probe < kProbe; ++probe) {
-        const uint32_t old = atomicCAS(&h.key[s], kEmpty, key);
-        if (old == kEmpty || old == key) return s;
-        s = (s + 1u) & (kHash - 1u);
-    }
-    return kEmpty;
-}
-
-__device__ __forceinline__ uint32_t hash_find(const BinHash& h, uint32_t key)
-{
-    uint32_t s = (key * 2654435761u) >> 22;
-    for (uint32_t probe = 0; probe < kProbe; ++probe) {
-        const uint32_t k = h.key[s];
-        if (k == key) return s;
-        if (k == kEmpty) return kEmpty;
-        s = (s + 1u) & (kHash - 1u);
-    }
-    return kEmpty;
-}
-
-__device__ __forceinline__ void hash_clear(BinHash& h)
-{
-    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) {
-        h.key[k] = kEmpty;
-        h.cnt[k] = 0u;
     }
 }
 
@@ -774,67 +776,34 @@ __device__ __forceinline__ void for_each_pair(const RenderParams& p, const BinBu
     }
 }
 
-// Exclusive scan of the region counts by one workgroup (the last k_prep one).
-__device__ void scan_regions(const BinBuffers& bins, BinState* __restrict__ bs, DevStats* __restrict__ st,
-                             uint32_t* s_part)
+// Exclusive scan over the workgroup of one value per thread; `total` is the
+// workgroup sum.  `s_wave` holds one word per wave.  Contains barriers.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& total)
 {
-    const uint32_t n = bins.regions_x * bins.regions_y;
-    const uint32_t nt = blockDim.x;
-    const uint32_t per = (n + nt - 1u) / nt;
-    const uint32_t b = threadIdx.x * per, e = min(b + per, n);
-    uint32_t sum = 0;
-    for (uint32_t i = b; i < e; ++i) sum += bins.counts[i];
-    s_part[threadIdx.x] = sum;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off);
+        if (lane >= (uint32_t)off) inc += o;
+    }
+    if (lane == 63u) s_wave[wave] = inc;
     __syncthreads();
-    for (uint32_t off = 1; off < nt; off <<= 1) {     // Hillis-Steele inclusive scan
-        const uint32_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+        const uint32_t t = s_wave[w];
+        before += w < wave ? t : 0u;
+        total += t;
     }
-    uint32_t run = s_part[threadIdx.x] - sum;
-    for (uint32_t i = b; i < e; ++i) {
-        bins.offsets[i] = run;
-        bins.cursor[i] = run;
-        run += bins.counts[i];
-    }
-    // Launch order, heaviest regions first (longest-job-first keeps the dense
-    // middle of the image from starting last and setting the kernel's tail):
-    // a counting sort on 32 - clz(count), descending.  Order within a bucket
-    // is unspecified; results do not depend on the order.
-    if (bins.order) {
-        uint32_t* s_bucket = s_part + nt;          // [33] counts, then cursors
-        if (threadIdx.x < 33u) s_bucket[threadIdx.x] = 0u;
-        __syncthreads();
-        for (uint32_t i = b; i < e; ++i) atomicAdd(&s_bucket[32 - __clz(bins.counts[i])], 1u);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t run = 0;
-            for (int k = 32; k >= 0; --k) {
-                const uint32_t c = s_bucket[k];
-                s_bucket[k] = run;
-                run += c;
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = b; i < e; ++i)
-            bins.order[atomicAdd(&s_bucket[32 - __clz(bins.counts[i])], 1u)] = i;
-    }
-    if (threadIdx.x == nt - 1u) {
-        const uint32_t total = s_part[nt - 1u];
-        bins.offsets[n] = total;
-        bs->total = total;
-        bs->overflow = total > bins.list_cap ? 1u : 0u;
-        st->bin.total = total;
-        st->bin.overflow = bs->overflow;
-        st->bin.global_count = bs->global_count;
-    }
+    __syncthreads();
+    return before + inc - v;
 }
 
 // ---------------------------------------------------------------------------
 // k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
-// terms), cull planes, and (binned) the region counts; the workgroup that
-// finishes last scans them.  Thread 0 also clears DevStats for the frame.
+// terms), cull planes and (binned) the triangle's region pairs.  Thread 0
+// also clears DevStats for the frame.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
@@ -842,7 +811,6 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
                                               float4* __restrict__ culls, BinBuffers bins,
                                               BinState* __restrict__ bs, DevStats* __restrict__ st)
 {
-    __shared__ BinHash h;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
     if (i == 0 && st) {
@@ -876,9 +844,9 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     }
     if (!bins.counts) return;                      // kernel-uniform
 
-    // --- count (region, triangle) pairs --------------------------------------
     __shared__ BigList big;
-    hash_clear(h);
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_base;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
     const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
@@ -891,123 +859,262 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
         big.item[slot] = it;
     }
     const bool to_global = global || (is_big && slot == kEmpty);
-    for_each_pair(p, bins, big, has && !to_global, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2,
-                  slot != kEmpty, [&](uint32_t r, uint32_t) {
-                      const uint32_t hs = hash_insert(h, r);
-                      if (hs != kEmpty) atomicAdd(&h.cnt[hs], 1u);
-                      else atomicAdd(&bins.counts[r], 1u);
-                  });
+    const bool live = has && !to_global;
     if (valid && to_global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x)
-        if (h.key[k] != kEmpty) atomicAdd(&bins.counts[h.key[k]], h.cnt[k]);
 
-    // --- last workgroup scans (release/acquire at agent scope, G16) ----------
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // Pass 1 counts this thread's pairs (its small rectangle and its share of
+    // the queued big ones); pass 2 repeats the same enumeration and writes them.
+    uint32_t mine = 0;
+    for_each_pair(p, bins, big, live, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, slot != kEmpty,
+                  [&](uint32_t, uint32_t) { ++mine; });
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan(mine, s_wave, total);
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(&bs->pair_count, total) : 0u;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        h.last = atomicAdd(&bs->ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!h.last) return;                           // workgroup-uniform
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    scan_regions(bins, bs, st, h.cnt);
+    uint32_t pos = s_base + off;
+    for_each_pair(p, bins, big, live, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, slot != kEmpty,
+                  [&](uint32_t r, uint32_t t) {
+                      if (pos < bins.cap) bins.pairs[pos] = make_uint2(t, r);
+                      ++pos;
+                      atomicAdd(&bins.counts[r], 1u);
+                  });
 }
 
-// Fill pass: one thread per triangle.  Pass A counts the workgroup's pairs per
-// region in the LDS table; one global atomic per distinct region reserves a
-// contiguous slot range; pass B writes the triangle ids into it.
-__global__ __launch_bounds__(256) void k_bin_fill(const float4* __restrict__ culls, RenderParams p,
-                                                  BinBuffers bins, const BinState* __restrict__ bs)
+// ---------------------------------------------------------------------------
+// k_bin_scan: one workgroup of kScanThreads.  Region r belongs to thread
+// r % kScanThreads (coalesced loads).  Every thread histograms its regions by
+// launch bucket (heaviest first: log2 of the count) into its own LDS column;
+// one exclusive scan of the bucket-major table [bucket][thread] then gives
+// every (bucket, thread) its first launch slot, and one of the pair sums its
+// first list position.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kScanThreads = 1024;
+constexpr uint32_t kBuckets = 8;
+
+__device__ __forceinline__ uint32_t launch_bucket(uint32_t c)
 {
-    __shared__ BinHash h;
-    __shared__ BigList big;
-    if (bs->overflow) return;                      // kernel-uniform
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    // 0 = heaviest (>= 512 candidates), 1 = 256.., ..., 5 = 16..31,
+    // 6 = 1..15, 7 = empty region
+    if (c == 0u) return kBuckets - 1u;
+    const int b = 9 - (31 - __clz(c));             // 9 - floor(log2 c)
+    return b < 0 ? 0u : (b > 6 ? 6u : (uint32_t)b);
+}
+
+// In-place exclusive scan of tab[kBuckets * kScanThreads]; thread t scans the
+// kBuckets consecutive words from kBuckets * t.  Returns the table total.
+__device__ __forceinline__ uint32_t scan_table(uint32_t* tab, uint32_t* s_wave)
+{
+    uint32_t v[kBuckets];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kBuckets; ++q) {
+        v[q] = tab[kBuckets * threadIdx.x + q];
+        sum += v[q];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, s_wave, total);
+#pragma unroll
+    for (uint32_t q = 0; q < kBuckets; ++q) {
+        tab[kBuckets * threadIdx.x + q] = run;
+        run += v[q];
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_bin_scan(BinBuffers bins, const BinState* __restrict__ bs,
+                                                           DevStats* __restrict__ st)
+{
+    __shared__ uint32_t s_reg[kBuckets * kScanThreads];    // [bucket][thread]
+    __shared__ uint32_t s_pair[kBuckets * kScanThreads];
+    __shared__ uint32_t s_wave[kScanThreads / 64];
+    const uint32_t n = bins.regions_x * bins.regions_y;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t G = bs->global_count;
+    const uint32_t pairs_total = bs->pair_count;
+#pragma unroll
+    for (uint32_t q = 0; q < kBuckets; ++q) {
+        s_reg[q * kScanThreads + tid] = 0u;
+        s_pair[q * kScanThreads + tid] = 0u;
+    }
+    for (uint32_t r = tid; r < n; r += kScanThreads) {     // own column: no atomics
+        const uint32_t c = bins.counts[r];
+        const uint32_t b = launch_bucket(c);
+        s_reg[b * kScanThreads + tid] += 1u;
+        s_pair[b * kScanThreads + tid] += c;
+    }
+    __syncthreads();
+    scan_table(s_reg, s_wave);
+    const uint32_t total = scan_table(s_pair, s_wave);
+    for (uint32_t r = tid; r < n; r += kScanThreads) {
+        const uint32_t c = bins.counts[r];
+        const uint32_t b = launch_bucket(c);
+        const uint32_t slot = s_reg[b * kScanThreads + tid]++;
+        const uint32_t lo = s_pair[b * kScanThreads + tid];
+        s_pair[b * kScanThreads + tid] = lo + c;
+        bins.slots[slot] = make_uint4(r, lo, c, G);
+        bins.spans[r] = make_uint2(lo, c);
+        bins.cursor[r] = lo;
+    }
+    if (tid == 0) {
+        st->bin.pair_count = pairs_total;
+        st->bin.global_count = G;
+        st->bin.total = total;
+        st->bin.overflow = pairs_total > bins.cap ? 1u : 0u;
+    }
+}
+
+// k_bin_fill: one thread per pair, grid-stride.
+__global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const DevStats* __restrict__ st)
+{
+    if (st->bin.overflow) return;                  // kernel-uniform
+    const uint32_t n = st->bin.pair_count;
+    const uint32_t n_regions = bins.regions_x * bins.regions_y;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint2 pr = bins.pairs[k];
+        if (pr.y >= n_regions) continue;           // cannot happen; never write out of range
+        const uint32_t at = atomicAdd(&bins.cursor[pr.y], 1u);
+        if (at < bins.cap) bins.list[at] = pr.x;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_render_binned: wave-per-tile render over the binned region lists.
+// Each wavefront owns one 8x8 ray tile and walks its region's candidate list
+// straight from global memory (no LDS staging, no barrier until the block's
+// statistics): one lane per candidate evaluates the three relaxed edges at
+// the tile rectangle, a ballot keeps the survivors, and every survivor's
+// record is a wave-uniform scalar load tested exactly for all 64 rays.  The
+// ray directions are generated only when the first survivor appears: a tile
+// without survivors stores the miss constants (80, +inf, 255) directly.
+// The four waves of a workgroup take four tiles of one region, regions in
+// the launch order of the binning scan (heaviest first).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs, uint32_t j0,
+                                                 uint32_t j1, bool two, float dx, float dy,
+                                                 float dz, HitList& hl)
+{
+    const TriRec a = recs[j0];
+    bool h0, h1 = false;
+    const float t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
+                              a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
+    float t1 = 0.0f;
+    if (two) {
+        const TriRec b = recs[j1];
+        t1 = mt_exact(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
+                      b.qvx, b.qvy, b.qvz, b.tnum, h1);
+    }
+    hl.push_if(h0, t0);
+    hl.push_if(h1, t1);
+}
+
+template <typename Fetch>
+__device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Outputs& out,
+                                                 const TriRec* __restrict__ recs,
+                                                 const float4* __restrict__ culls, uint32_t tx0,
+                                                 uint32_t ty0, uint32_t n_cand, Fetch fetch,
+                                                 WaveStats& ws)
+{
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = p.num_triangles;
-    const bool valid = j < T;
-    hash_clear(h);
-    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
-    bool global = false, has = false;
-    float4 e0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), e1 = e0, e2 = e0;
-    if (valid) {
-        has = bin_rect(culls[j], p, bins, x0, x1, y0, y1, global);
-        if (has) {
-            e0 = culls[(size_t)T + j];
-            e1 = culls[2 * (size_t)T + j];
-            e2 = culls[3 * (size_t)T + j];
+    const uint32_t col = tx0 + (lane & 7u);
+    const uint32_t row = ty0 + (lane >> 3);
+    const bool active = col < p.width && row < p.row_end;
+    const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
+    if (p.ablate & kAblateCandidates) n_cand = 0;
+
+    float dx = 1.0f, dy = 0.0f, dz = 0.0f;
+    bool have_ray = false;                        // wave-uniform
+    HitList hl;
+    hl.init();
+    uint32_t tests = 0;
+    for (uint32_t base = 0; base < n_cand; base += 64u) {
+        const uint32_t k = base + lane;
+        uint32_t j = k < n_cand ? fetch(k) : 0u;
+        j = j < T ? j : 0u;                       // cannot happen; never read out of range
+        bool pass = false;
+        if (k < n_cand)
+            pass = edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
+                              xc, yc, 3.5f, 3.5f);
+        unsigned long long m = __ballot(pass);
+        if (!m) continue;
+        tests += (uint32_t)__popcll(m);
+        if (!have_ray) {
+            if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+            have_ray = true;
+        }
+        if (p.ablate & kAblateExact) continue;
+        while (m) {
+            const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)k0);
+            uint32_t j1 = j0;
+            const bool two = m != 0ull;
+            if (two) {
+                const uint32_t k1 = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                j1 = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)k1);
+            }
+            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl);
         }
     }
-    const bool is_big = has && (x1 - x0 + 1u) * (y1 - y0 + 1u) > kSerialRegions;
-    const uint32_t slot = big_slot(big, is_big);          // same queue as k_prep's
-    if (slot != kEmpty) {
-        BigItem it;
-        it.e0 = e0; it.e1 = e1; it.e2 = e2;
-        it.j = j; it.x0 = x0; it.x1 = x1; it.y0 = y0; it.y1 = y1;
-        big.item[slot] = it;
+    ws.tile_tests += tests;
+    if (have_ray) {
+        finish_ray(p, out, active, row, col, hl, ws);
+        return;
     }
-    const bool live = has && !(is_big && slot == kEmpty);  // else it is in the global list
-    // pass A: count per region in LDS (crowded table: write directly)
-    for_each_pair(p, bins, big, live, j, x0, x1, y0, y1, e0, e1, e2, slot != kEmpty,
-                  [&](uint32_t r, uint32_t t) {
-                      const uint32_t hs = hash_insert(h, r);
-                      if (hs != kEmpty) atomicAdd(&h.cnt[hs], 1u);
-                      else bins.list[atomicAdd(&bins.cursor[r], 1u)] = t;
-                  });
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) {
-        if (h.key[k] != kEmpty) h.base[k] = atomicAdd(&bins.cursor[h.key[k]], h.cnt[k]);
-        h.cnt[k] = 0u;
-    }
-    __syncthreads();
-    // pass B: the slots
-    for_each_pair(p, bins, big, live, j, x0, x1, y0, y1, e0, e1, e2, slot != kEmpty,
-                  [&](uint32_t r, uint32_t t) {
-                      const uint32_t hs = hash_find(h, r);
-                      if (hs != kEmpty) bins.list[h.base[hs] + atomicAdd(&h.cnt[hs], 1u)] = t;
-                  });
+    // No survivor: every ray of the tile misses (main.cxx:700-718 with no hit).
+    ws.rays += (uint32_t)__popcll(__ballot(active));
+    if (!active || (p.ablate & kAblateStores)) return;
+    const size_t o = (size_t)(row - p.row_begin) * p.width + col;
+    if (out.image) out.image[o] = 80.0f;
+    if (out.lbuffer) out.lbuffer[o] = __builtin_inff();
+    if (out.image_u8) out.image_u8[o] = 255u;
 }
 
-__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_binned(const TriRec* __restrict__ recs,
-                                                       const float4* __restrict__ culls,
-                                                       RenderParams p, Outputs out, BinBuffers bins,
-                                                       const BinState* __restrict__ bs)
+__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_binned(
+    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
+    BinBuffers bins)
 {
-    __shared__ StageLDS st;
     const uint64_t t_start = block_start_stamp();
-    const uint32_t region = bins.order ? bins.order[blockIdx.x] : blockIdx.x;   // 1-D grid
-    const uint32_t rx0 = (region % bins.regions_x) * kRegion;
-    const uint32_t ry0 = p.row_begin + (region / bins.regions_x) * kRegion;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint4 slot = bins.slots[blockIdx.x >> 2];              // 4 workgroups per region
+    const bool overflow = out.stats->bin.overflow != 0u;
+    const uint32_t region = slot.x;
+    const uint32_t tile = (blockIdx.x & 3u) * 4u + wave;         // 16 tiles per region
+    const uint32_t tx0 = (region % bins.regions_x) * kRegion + (tile & 3u) * 8u;
+    const uint32_t ty0 = p.row_begin + (region / bins.regions_x) * kRegion + (tile >> 2) * 8u;
     WaveStats ws = {};
-    uint32_t n_cand;
-    if (bs->overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
-        n_cand = p.num_triangles;
-        render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand, [](uint32_t k) { return k; }, ws, st);
-    } else {
-        const uint32_t lo = bins.offsets[region];
-        const uint32_t n_local = bins.offsets[region + 1] - lo;
-        const uint32_t* __restrict__ local = bins.list + lo;
-        const uint32_t* __restrict__ glob = bins.global_list;
-        n_cand = n_local + bs->global_count;
-        render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand,
-                            [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws, st);
+    uint32_t n_cand = 0;
+    if (tx0 < p.width && ty0 < p.row_end) {                     // wave-uniform
+        if (overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
+            n_cand = p.num_triangles;
+            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand, [](uint32_t k) { return k; }, ws);
+        } else {
+            const uint32_t n_local = slot.z;
+            const uint32_t* __restrict__ local = bins.list + slot.y;
+            const uint32_t* __restrict__ glob = bins.global_list;
+            n_cand = n_local + slot.w;
+            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand,
+                             [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
+        }
     }
-    store_block_stats(ws, n_cand, out.block_stats, t_start);
+    // candidates are counted once per region (by its first workgroup)
+    store_block_stats(ws, (blockIdx.x & 3u) == 0u ? n_cand : 0u, out.block_stats, t_start);
 }
 
 // ---------------------------------------------------------------------------
-// k_finish: (1) exact result for rays whose hit count exceeded the register
-// list -- the sorted hit sequence is streamed by repeated scans for the next
-// larger distance (with its multiplicity), so any hit count is handled with
-// O(1) state and main.cxx:703-708's sum runs in the same order; (2) workgroup
-// 0 sums the per-workgroup statistics.
+// k_finish: (1) every workgroup sums a slice of the per-workgroup statistics;
+// (2) exact result for rays whose hit count exceeded the register list, one
+// ray per workgroup at a time.  The workgroup tests the ray against the
+// candidates of its region (binned: region list + global list; otherwise the
+// whole mesh), collects the accepted distances in LDS, sorts them (bitonic)
+// and sums the pairs in ascending order as main.cxx:703-708 does.  A ray with
+// more than kOverflowLds hits streams its sorted sequence instead: repeated
+// workgroup-wide scans for the next larger distance and its multiplicity.
 // ---------------------------------------------------------------------------
-// Every k_finish workgroup sums a slice of the per-workgroup records and adds
-// it to DevStats (a handful of atomics per workgroup, spread over 8 words).
+constexpr uint32_t kOverflowLds = 2048;
+
 __device__ void stats_reduce_slice(const BlockStats* __restrict__ parts, uint32_t n_blocks,
                                    DevStats* __restrict__ st)
 {
@@ -1050,67 +1157,155 @@ __device__ void stats_reduce_slice(const BlockStats* __restrict__ parts, uint32_
     }
 }
 
-__global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs, RenderParams p,
-                                                Outputs out, uint32_t n_blocks)
-{
-    stats_reduce_slice(out.block_stats, n_blocks, out.stats);
-    const uint32_t count = out.stats->overflow_count;
-    const uint32_t T = p.num_triangles;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < count;
-         e += gridDim.x * blockDim.x) {
-        uint32_t o = out.overflow_list[e];
-        uint32_t row = p.row_begin + o / p.width;
-        uint32_t col = o % p.width;
-        float dx, dy, dz;
-        make_ray(p, row, col, dx, dy, dz);
+struct OverflowLDS {
+    float t[kOverflowLds];
+    uint32_t n;
+    float red_t[4];
+    uint32_t red_n[4];
+};
 
-        // Scan 1: total count.
-        uint64_t n = 0;
-        for (uint32_t j = 0; j < T; ++j) {
-            const TriRec& r = recs[j];
-            float t;
-            if (mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx, r.tvy,
-                             r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
-                accept_t(t))
-                ++n;
+// Workgroup min over lanes of `cur` and the number of lanes' `mult` whose cur
+// equals it (sum).  Every thread gets the result.
+__device__ __forceinline__ void block_min_mult(OverflowLDS& s, float& cur, uint32_t& mult)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float oc = __shfl_xor(cur, off);
+        const uint32_t om = __shfl_xor(mult, off);
+        if (oc < cur) { cur = oc; mult = om; }
+        else if (oc == cur) mult += om;
+    }
+    __syncthreads();
+    if (lane == 0) { s.red_t[wave] = cur; s.red_n[wave] = mult; }
+    __syncthreads();
+    cur = s.red_t[0];
+    mult = s.red_n[0];
+    for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) {
+        if (s.red_t[w] < cur) { cur = s.red_t[w]; mult = s.red_n[w]; }
+        else if (s.red_t[w] == cur) mult += s.red_n[w];
+    }
+}
+
+template <typename Fetch>
+__device__ float overflow_distance(OverflowLDS& s, const TriRec* __restrict__ recs, uint32_t n_cand,
+                                   Fetch fetch, float dx, float dy, float dz, uint32_t& n_hits)
+{
+    auto hit_of = [&](uint32_t k, float& t) {
+        const TriRec& r = recs[fetch(k)];
+        return mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx, r.tvy,
+                            r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
+               accept_t(t);
+    };
+    if (threadIdx.x == 0) s.n = 0;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n_cand; k += blockDim.x) {
+        float t;
+        if (hit_of(k, t)) {
+            const uint32_t idx = atomicAdd(&s.n, 1u);
+            if (idx < kOverflowLds) s.t[idx] = t;
         }
-        float distance = 0.0f;
-        if (n % 2 == 0) {
-            uint64_t pos = 0;
-            float prev = -__builtin_inff();
-            bool first = true;
-            float pending = 0.0f;
-            while (pos < n) {
-                // next distinct value > prev (any value on the first pass) and its multiplicity
-                float cur = __builtin_inff();
-                uint64_t mult = 0;
-                for (uint32_t j = 0; j < T; ++j) {
-                    const TriRec& r = recs[j];
-                    float t;
-                    if (mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx,
-                                     r.tvy, r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
-                        accept_t(t) && (first || t > prev)) {
-                        if (t < cur) {
-                            cur = t;
-                            mult = 1;
-                        } else if (t == cur) {
-                            ++mult;
-                        }
+    }
+    __syncthreads();
+    const uint32_t n = s.n;
+    n_hits = n;
+    if (n & 1u) return 0.0f;                 // odd count: main.cxx:709-713
+    float distance = 0.0f;
+    if (n <= kOverflowLds) {
+        uint32_t m = 1;
+        while (m < n) m <<= 1;
+        for (uint32_t k = n + threadIdx.x; k < m; k += blockDim.x) s.t[k] = __builtin_inff();
+        __syncthreads();
+        for (uint32_t size = 2; size <= m; size <<= 1) {          // bitonic sort, ascending
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+                    const uint32_t j = i ^ stride;
+                    if (j > i) {
+                        const float a = s.t[i], b = s.t[j];
+                        const bool up = (i & size) == 0;
+                        if (up ? (b < a) : (a < b)) { s.t[i] = b; s.t[j] = a; }
                     }
                 }
-                if (mult == 0) break;   // cannot happen; keeps the loop bounded
-                for (uint64_t q = 0; q < mult && pos < n; ++q, ++pos) {
-                    if ((pos & 1) == 0) pending = cur;
-                    else distance += cur - pending;
-                }
-                prev = cur;
-                first = false;
+                __syncthreads();
             }
         }
-        float photon = shade(distance);
-        if (out.image) out.image[o] = photon;
-        if (out.lbuffer) out.lbuffer[o] = distance;   // n > capacity >= 1, so the ray hit
-        if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+        if (threadIdx.x == 0)
+            for (uint32_t k = 0; k + 1 < n; k += 2) distance += s.t[k + 1] - s.t[k];
+        return distance;                     // valid in thread 0
+    }
+    // Streamed: the sorted sequence by repeated scans (value, multiplicity).
+    uint32_t pos = 0;
+    float prev = -__builtin_inff(), pending = 0.0f;
+    bool first = true;
+    while (pos < n) {
+        float cur = __builtin_inff();
+        uint32_t mult = 0;
+        for (uint32_t k = threadIdx.x; k < n_cand; k += blockDim.x) {
+            float t;
+            if (hit_of(k, t) && (first || t > prev)) {
+                if (t < cur) { cur = t; mult = 1; }
+                else if (t == cur) ++mult;
+            }
+        }
+        block_min_mult(s, cur, mult);
+        if (mult == 0) break;                // cannot happen; keeps the loop bounded
+        for (uint32_t q = 0; q < mult && pos < n; ++q, ++pos) {
+            if ((pos & 1u) == 0) pending = cur;
+            else distance += cur - pending;
+        }
+        prev = cur;
+        first = false;
+    }
+    return distance;
+}
+
+__global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs, RenderParams p,
+                                                Outputs out, uint32_t n_blocks, BinBuffers bins,
+                                                BinState* __restrict__ bs)
+{
+    __shared__ OverflowLDS s;
+    stats_reduce_slice(out.block_stats, n_blocks, out.stats);
+    const uint32_t count = out.stats->overflow_count;
+    const bool use_bins = bins.spans && !out.stats->bin.overflow;
+    for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+        const uint32_t o = out.overflow_list[e];
+        const uint32_t row = p.row_begin + o / p.width;
+        const uint32_t col = o % p.width;
+        float dx, dy, dz;
+        make_ray(p, row, col, dx, dy, dz);
+        uint32_t n_hits = 0;
+        float distance;
+        if (use_bins) {
+            const uint32_t region = (o / p.width / kRegion) * bins.regions_x + col / kRegion;
+            const uint2 span = bins.spans[region];
+            const uint32_t n_local = span.y;
+            const uint32_t* __restrict__ local = bins.list + span.x;
+            const uint32_t* __restrict__ glob = bins.global_list;
+            distance = overflow_distance(s, recs, n_local + out.stats->bin.global_count,
+                                         [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; },
+                                         dx, dy, dz, n_hits);
+        } else {
+            distance = overflow_distance(s, recs, p.num_triangles, [](uint32_t k) { return k; }, dx,
+                                         dy, dz, n_hits);
+        }
+        if (threadIdx.x == 0) {
+            const float photon = shade(distance);
+            if (out.image) out.image[o] = photon;
+            if (out.lbuffer) out.lbuffer[o] = distance;   // n > capacity >= 1, so the ray hit
+            if (out.image_u8) out.image_u8[o] = lut_u8(photon);
+        }
+        __syncthreads();                      // s is reused by the next ray
+    }
+    // Binned frames leave the counts and the control block zero for the next
+    // one (nothing after k_bin_scan reads them).
+    if (bins.counts) {
+        const uint32_t n = bins.regions_x * bins.regions_y;
+        for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
+            bins.counts[r] = 0u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            BinState z = {};
+            *bs = z;
+        }
     }
 }
 

@@ -194,6 +194,35 @@ def test_overflow_path_exact(ctx, dragon, kernel):
         assert_same(got, ref, f"{KNAME[kernel]} cap={cap}")
 
 
+def plane_stack(n, spacing=0.01):
+    """n parallel unit squares (2 triangles each) facing the detector: every ray
+    through the square hits each plane (twice on the shared diagonal)."""
+    x = (np.arange(n, dtype=np.float32) * np.float32(spacing)).astype(np.float32)
+    a = np.stack([x, np.zeros(n, np.float32), np.zeros(n, np.float32)], 1)
+    b = np.stack([x, np.ones(n, np.float32), np.zeros(n, np.float32)], 1)
+    c = np.stack([x, np.ones(n, np.float32), np.ones(n, np.float32)], 1)
+    d = np.stack([x, np.zeros(n, np.float32), np.ones(n, np.float32)], 1)
+    t1 = np.concatenate([a, b, c], 1)
+    t2 = np.concatenate([a, c, d], 1)
+    return np.ascontiguousarray(np.stack([t1, t2], 1).reshape(2 * n, 9), dtype=np.float32)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("planes,size", [(40, 48), (2100, 8)])
+def test_deep_stack_overflow(ctx, kernel, planes, size):
+    """Rays with 40..4200 hits: the cooperative overflow path (LDS sort up to
+    2048 hits, streamed beyond) must equal the oracle's std::sort + pair sum."""
+    if kernel == xrt.XRT_KERNEL_BRUTE and planes > 100:
+        pytest.skip("brute force is covered by the 40-plane case")
+    soup = plane_stack(planes)
+    cam = oracle.camera_for_mesh(soup, size, size)
+    ref = oracle.render_rows(soup, cam, size, size)
+    got = render(ctx, soup, size, size, kernel)
+    assert int(ref[3].max()) > 16
+    assert got[3].overflow_rays == int(np.count_nonzero(ref[3] > 16))
+    assert_same(got, ref, f"{KNAME[kernel]} {planes} planes")
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_empty_mesh(ctx, dragon, kernel):
     cam = xrt.camera_for_mesh(dragon, 40, 30)
