@@ -223,6 +223,13 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
  */
 int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint64_t* n_records);
 
+/*
+ * Diagnostics: copies up to `n` u64 phase timestamps (s_memrealtime, 100 MHz)
+ * of the last frame's binning kernels into `dst` (layout in xrt_kernels.h,
+ * XRT_STAMP_*).  Builds without XRT_STAMPS return zeros.
+ */
+int xrt_debug_stamps(xrt_context* ctx, uint64_t* dst, uint64_t n);
+
 #ifdef __cplusplus
 }
 #endif

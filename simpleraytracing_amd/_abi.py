@@ -100,6 +100,7 @@ XRT_SYMBOLS = {
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
+    "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
 }
 
 # every C symbol declared in include/xrt_host.h

@@ -31,7 +31,7 @@ struct BinState {
     unsigned int pair_count;    // (triangle, region) pairs emitted by k_prep
     unsigned int global_count;  // triangles in the global list
     unsigned int total;         // sum of the region counts (k_bin_scan)
-    unsigned int overflow;      // pairs > capacity: regions fall back to the whole mesh
+    unsigned int overflow;      // pairs over capacity: regions fall back to the whole mesh
 };
 
 struct DevStats {
@@ -128,6 +128,24 @@ __device__ __forceinline__ uint64_t block_start_stamp()
     return 0;
 #endif
 }
+
+// Phase timestamps of the binning kernels (XRT_STAMPS builds): one u64 per
+// (workgroup, phase) in g_stamps; the workgroup's threads are synchronised
+// first so a stamp marks the end of the phase for the whole workgroup.
+constexpr uint32_t kStampsN = 1u << 16;
+constexpr uint32_t kStampPrep = 0;          // k_prep: 8 per workgroup
+constexpr uint32_t kStampScan = 60000;      // k_bin_scan: 8
+constexpr uint32_t kStampFill = 32768;      // k_bin_fill: 2 per workgroup
+#if XRT_STAMPS
+__device__ uint64_t g_stamps[kStampsN];
+#define XRT_STAMP(idx)                                                               \
+    do {                                                                             \
+        __syncthreads();                                                             \
+        if (threadIdx.x == 0 && (idx) < kStampsN) g_stamps[(idx)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define XRT_STAMP(idx) do {} while (0)
+#endif
 
 __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
                                                   BlockStats* out, uint64_t t_start = 0)
@@ -254,9 +272,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
 constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
-constexpr uint32_t kGlobalRegions = 1u << 20; // footprints over more regions go to the global list
-constexpr uint32_t kSerialRegions = 16;       // larger rectangles are enumerated by the whole workgroup
-constexpr uint32_t kBig = 64;                 // cooperative rectangles per workgroup
+constexpr uint32_t kGlobalRegions = 4096;     // footprints over more regions go to the global list
 
 // Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
 // function a*col + b*row + c.
@@ -642,21 +658,32 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // ---------------------------------------------------------------------------
 // Binning (XRT_KERNEL_BINNED): the conservative footprints are assigned to
 // 32x32 regions once per frame, in three wide stages with no serial tail:
-//   k_prep      per triangle: footprint, then its (triangle, region) pairs
-//               are appended to a flat pair array (one atomic per workgroup
-//               reserves the range) and counted per region (no-return atomics);
+//   k_prep      per triangle: footprint and its rectangle of regions; then the
+//               workgroup expands the rectangles of its 256 triangles into
+//               cells, one thread per cell (load-balanced by a search over the
+//               rectangles' prefix sum), tests each cell's 32x32 square against
+//               the relaxed edges, stages the passing (triangle, region) pairs
+//               in LDS, reserves their range with one atomic and copies them
+//               out; regions are counted with fire-and-forget atomics on
+//               line-padded counters;
 //   k_bin_scan  one workgroup: region list offsets and the launch order
 //               (regions by descending candidate count, in log2 buckets);
 //   k_bin_fill  one thread per pair: scatter into the region lists.
 // Footprints over more than kGlobalRegions regions go to a global list every
 // region reads.
 // ---------------------------------------------------------------------------
+// Region counters touched by atomics are padded to one 128-B L2 line each:
+// atomics on one line serialise, and neighbouring regions are hot together.
+constexpr uint32_t kCounterStride = 32;
+constexpr uint32_t kWaveStage = 1024;        // pairs staged in LDS per k_prep wave
+constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
+
 struct BinBuffers {
-    uint32_t* counts;        // [n_regions]   zero on entry to a binned frame
+    uint32_t* counts;        // [n_regions * kCounterStride] zero on entry to a binned frame
     uint2* spans;            // [n_regions]   (list offset, count) per region
-    uint32_t* cursor;        // [n_regions]   fill cursors
+    uint32_t* cursor;        // [n_regions * kCounterStride] fill cursors
     uint4* slots;            // [n_regions]   launch order: (region, offset, count, global count)
-    uint2* pairs;            // [cap]         (triangle, region) in emission order
+    uint2* pairs;            // [cap]         (triangle, region)
     uint32_t* list;          // [cap]         region candidate lists
     uint32_t* global_list;   // [T]
     uint32_t cap;            // capacity of pairs and list
@@ -664,6 +691,27 @@ struct BinBuffers {
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+// Runs of consecutive active lanes holding the same key (a wave-uniform call
+// with every lane present).  `head` is the lane that starts this lane's run,
+// `len` (valid in the head) the run length: one atomic per run replaces up to
+// 64 same-address atomics, which serialise in L2.
+__device__ __forceinline__ void lane_runs(bool active, uint32_t key, uint32_t& head, uint32_t& len)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t prev = __shfl_up(key, 1);
+    const uint32_t next = __shfl_down(key, 1);
+    const unsigned long long act = __ballot(active);
+    const bool same_prev = lane > 0u && ((act >> (lane - 1u)) & 1ull) && prev == key;
+    const bool same_next = lane < 63u && ((act >> (lane + 1u)) & 1ull) && next == key;
+    const unsigned long long heads = __ballot(active && !same_prev);
+    const unsigned long long tails = __ballot(active && !same_next);
+    const unsigned long long upto = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+    const unsigned long long h = heads & upto;
+    head = h ? 63u - (uint32_t)__clzll(h) : 0u;
+    const unsigned long long t = tails >> lane;
+    len = t ? (uint32_t)__builtin_ctzll(t) + 1u : 1u;
+}
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
 // footprint box may touch; false when it touches none.
@@ -689,22 +737,6 @@ __device__ __forceinline__ bool footprint_regions(float4 bb, const RenderParams&
     return true;
 }
 
-// Calls f(region) for every region of the rectangle whose 32x32 pixel-centre
-// square passes the relaxed edge functions.
-template <typename F>
-__device__ __forceinline__ void for_each_region(const RenderParams& p, const BinBuffers& bins,
-                                                uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1,
-                                                float4 e0, float4 e1, float4 e2, F f)
-{
-    for (uint32_t ry = y0; ry <= y1; ++ry) {
-        const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
-        for (uint32_t rx = x0; rx <= x1; ++rx) {
-            const float xc = (float)(rx * kRegion) + 15.5f;
-            if (edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f)) f(ry * bins.regions_x + rx);
-        }
-    }
-}
-
 // Region rectangle of a footprint; false when the triangle is in no region
 // list (no region, or in the global list -- `global` tells which).
 __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const BinBuffers& bins,
@@ -718,62 +750,6 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
         return false;
     }
     return true;
-}
-
-// Rectangles of more than kSerialRegions regions are queued per workgroup (in
-// thread order, so both binning passes queue the same triangles) and their
-// regions are enumerated by all lanes together; past kBig queued rectangles a
-// triangle goes to the global list (decided identically in both passes).
-struct BigItem {
-    float4 e0, e1, e2;
-    uint32_t j, x0, x1, y0, y1, pad0, pad1, pad2;
-};
-
-struct BigList {
-    BigItem item[kBig];
-    uint32_t wave_count[4];
-    uint32_t n;
-};
-
-// Returns the queue slot of this thread's big rectangle (kEmpty if none or full).
-__device__ __forceinline__ uint32_t big_slot(BigList& big, bool is_big)
-{
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(is_big);
-    if (lane == 0) big.wave_count[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
-        if (w < wave) before += big.wave_count[w];
-        total += big.wave_count[w];
-    }
-    if (threadIdx.x == 0) big.n = total < kBig ? total : kBig;
-    const uint32_t slot = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    return is_big && slot < kBig ? slot : kEmpty;
-}
-
-// Calls f(region, triangle) for every region pair of the workgroup's triangles:
-// small rectangles serially per lane, queued big ones cooperatively.
-template <typename F>
-__device__ __forceinline__ void for_each_pair(const RenderParams& p, const BinBuffers& bins,
-                                              BigList& big, bool has, uint32_t j, uint32_t x0,
-                                              uint32_t x1, uint32_t y0, uint32_t y1, float4 e0,
-                                              float4 e1, float4 e2, bool queued, F f)
-{
-    if (has && !queued)
-        for_each_region(p, bins, x0, x1, y0, y1, e0, e1, e2, [&](uint32_t r) { f(r, j); });
-    __syncthreads();
-    for (uint32_t b = 0; b < big.n; ++b) {
-        const BigItem it = big.item[b];
-        const uint32_t wr = it.x1 - it.x0 + 1u;
-        const uint32_t area = wr * (it.y1 - it.y0 + 1u);
-        for (uint32_t k = threadIdx.x; k < area; k += blockDim.x) {
-            const uint32_t rx = it.x0 + k % wr, ry = it.y0 + k / wr;
-            const float xc = (float)(rx * kRegion) + 15.5f;
-            const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
-            if (edges_pass(it.e0, it.e1, it.e2, xc, yc, 15.5f, 15.5f)) f(ry * bins.regions_x + rx, it.j);
-        }
-    }
 }
 
 // Exclusive scan over the workgroup of one value per thread; `total` is the
@@ -813,6 +789,7 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
     if (i == 0 && st) {
         DevStats z = {};
         *st = z;
@@ -842,42 +819,180 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
             culls[3 * (size_t)T + i] = fp.e2;
         }
     }
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
     if (!bins.counts) return;                      // kernel-uniform
 
-    __shared__ BigList big;
+    // Each wave stages its passing (triangle, region) pairs in its own LDS
+    // segment with a wave-uniform running count (no LDS atomics); the
+    // workgroup then reserves one range and copies the segments out.
+    __shared__ uint32_t s_pairs[4][kWaveStage];    // local triangle << 24 | region
+    __shared__ float4 s_e[3][256];                 // relaxed edges (big triangles)
+    __shared__ uint2 s_rect[256];                  // (x0 | x1 << 16, y0 | y1 << 16)
+    __shared__ uint32_t s_big[256];                // big triangles (local index)
+    __shared__ uint32_t s_cum[256];                // inclusive prefix of their cell counts
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_base[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
     const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
-    const bool is_big = has && (x1 - x0 + 1u) * (y1 - y0 + 1u) > kSerialRegions;
-    const uint32_t slot = big_slot(big, is_big);          // contains a barrier
-    if (slot != kEmpty) {
-        BigItem it;
-        it.e0 = fp.e0; it.e1 = fp.e1; it.e2 = fp.e2;
-        it.j = i; it.x0 = x0; it.x1 = x1; it.y0 = y0; it.y1 = y1;
-        big.item[slot] = it;
-    }
-    const bool to_global = global || (is_big && slot == kEmpty);
-    const bool live = has && !to_global;
-    if (valid && to_global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
+    if (valid && global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
+    const uint32_t wr = x1 - x0 + 1u;
+    const uint32_t cells = has ? wr * (y1 - y0 + 1u) : 0u;
+    const bool big = cells > kSerialRegions;
 
-    // Pass 1 counts this thread's pairs (its small rectangle and its share of
-    // the queued big ones); pass 2 repeats the same enumeration and writes them.
-    uint32_t mine = 0;
-    for_each_pair(p, bins, big, live, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, slot != kEmpty,
-                  [&](uint32_t, uint32_t) { ++mine; });
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan(mine, s_wave, total);
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(&bs->pair_count, total) : 0u;
+    uint32_t wn = 0;                               // wave-uniform: pairs staged by this wave
+    bool lost = false;                             // staging segment overflowed
+    auto emit = [&](bool pass, uint32_t pr) {
+        const unsigned long long m = __ballot(pass);
+        if (pass) {
+            const uint32_t idx = wn + (uint32_t)__popcll(m & lt);
+            if (idx < kWaveStage) s_pairs[wave][idx] = pr;
+            atomicAdd(&bins.counts[(size_t)(pr & 0xFFFFFFu) * kCounterStride], 1u);
+        }
+        wn += (uint32_t)__popcll(m);
+    };
+    auto region_of = [&](uint32_t rx, uint32_t ry) { return ry * bins.regions_x + rx; };
+    auto cell_pass = [&](float4 e0, float4 e1, float4 e2, uint32_t rx, uint32_t ry) {
+        const float xc = (float)(rx * kRegion) + 15.5f;
+        const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
+        return edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f);
+    };
+
+    // Small rectangles: lane-serial, cell k of every lane in step k.
+    const uint32_t my_small = (has && !big) ? cells : 0u;
+    for (uint32_t k = 0; k < kSerialRegions; ++k) {
+        if (!__ballot(k < my_small)) break;         // wave-uniform
+        bool pass = false;
+        uint32_t pr = 0;
+        if (k < my_small) {
+            const uint32_t rx = x0 + k % wr, ry = y0 + k / wr;
+            pass = cell_pass(fp.e0, fp.e1, fp.e2, rx, ry);
+            pr = (tid << 24) | region_of(rx, ry);
+        }
+        emit(pass, pr);
+    }
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
+
+    // Big rectangles: their cells flattened over the whole workgroup.
+    const unsigned long long mb = __ballot(big);
+    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(mb);
     __syncthreads();
-    uint32_t pos = s_base + off;
-    for_each_pair(p, bins, big, live, i, x0, x1, y0, y1, fp.e0, fp.e1, fp.e2, slot != kEmpty,
-                  [&](uint32_t r, uint32_t t) {
-                      if (pos < bins.cap) bins.pairs[pos] = make_uint2(t, r);
-                      ++pos;
-                      atomicAdd(&bins.counts[r], 1u);
-                  });
+    uint32_t nbig = 0, bslot = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+        bslot += w < wave ? s_wave[w] : 0u;
+        nbig += s_wave[w];
+    }
+    bslot += (uint32_t)__popcll(mb & lt);
+    if (big) {
+        s_big[bslot] = tid;
+        s_e[0][bslot] = fp.e0;
+        s_e[1][bslot] = fp.e1;
+        s_e[2][bslot] = fp.e2;
+        s_rect[bslot] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
+    }
+    __syncthreads();
+    if (nbig) {                                    // workgroup-uniform
+        if (tid == 0) {
+            uint32_t run = 0;
+            for (uint32_t b = 0; b < nbig; ++b) {
+                const uint2 rc = s_rect[b];
+                run += ((rc.x >> 16) - (rc.x & 0xFFFFu) + 1u) * ((rc.y >> 16) - (rc.y & 0xFFFFu) + 1u);
+                s_cum[b] = run;
+            }
+        }
+        __syncthreads();
+        const uint32_t total_cells = s_cum[nbig - 1u];
+        for (uint32_t c0 = 0; c0 < total_cells; c0 += blockDim.x) {     // block-uniform
+            const uint32_t c = c0 + tid;
+            bool pass = false;
+            uint32_t pr = 0;
+            if (c < total_cells) {
+                uint32_t lo = 0, hi = nbig - 1u;    // first b with s_cum[b] > c
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
+                }
+                const uint2 rc = s_rect[lo];
+                const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+                const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
+                const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
+                pass = cell_pass(s_e[0][lo], s_e[1][lo], s_e[2][lo], rx, ry);
+                pr = (s_big[lo] << 24) | region_of(rx, ry);
+            }
+            emit(pass, pr);
+        }
+    }
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
+
+    // Reserve the workgroup's range and copy the wave segments out.
+    lost = wn > kWaveStage;
+    if (lane == 0) s_wave[wave] = wn;
+    __syncthreads();
+    uint32_t before = 0, npairs = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+        before += w < wave ? s_wave[w] : 0u;
+        npairs += s_wave[w];
+    }
+    if (tid == 0) s_base[0] = npairs ? atomicAdd(&bs->pair_count, npairs) : 0u;
+    __syncthreads();
+    const uint32_t base = s_base[0] + before;
+    const uint32_t i0 = blockIdx.x * blockDim.x;
+    const uint32_t keep = wn < kWaveStage ? wn : kWaveStage;
+    for (uint32_t k = lane; k < keep; k += 64u) {
+        const uint32_t v = s_pairs[wave][k];
+        if (base + k < bins.cap) bins.pairs[base + k] = make_uint2(i0 + (v >> 24), v & 0xFFFFFFu);
+    }
+    if (__syncthreads_or(lost)) {
+        // A wave staged more pairs than its segment holds: it repeats its
+        // enumeration and writes the pairs past the segment straight out
+        // (same order, so the same indices).
+        uint32_t wn2 = 0;
+        auto emit2 = [&](bool pass, uint32_t pr) {
+            const unsigned long long m = __ballot(pass);
+            const uint32_t idx = wn2 + (uint32_t)__popcll(m & lt);
+            if (pass && idx >= kWaveStage && base + idx < bins.cap)
+                bins.pairs[base + idx] = make_uint2(i0 + (pr >> 24), pr & 0xFFFFFFu);
+            wn2 += (uint32_t)__popcll(m);
+        };
+        if (lost) {                                // wave-uniform
+            for (uint32_t k = 0; k < kSerialRegions; ++k) {
+                if (!__ballot(k < my_small)) break;
+                bool pass = false;
+                uint32_t pr = 0;
+                if (k < my_small) {
+                    const uint32_t rx = x0 + k % wr, ry = y0 + k / wr;
+                    pass = cell_pass(fp.e0, fp.e1, fp.e2, rx, ry);
+                    pr = (tid << 24) | region_of(rx, ry);
+                }
+                emit2(pass, pr);
+            }
+        }
+        if (nbig) {
+            const uint32_t total_cells = s_cum[nbig - 1u];
+            for (uint32_t c0 = 0; c0 < total_cells; c0 += blockDim.x) {
+                const uint32_t c = c0 + tid;
+                bool pass = false;
+                uint32_t pr = 0;
+                if (c < total_cells) {
+                    uint32_t lo = 0, hi = nbig - 1u;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
+                    }
+                    const uint2 rc = s_rect[lo];
+                    const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+                    const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
+                    const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
+                    pass = cell_pass(s_e[0][lo], s_e[1][lo], s_e[2][lo], rx, ry);
+                    pr = (s_big[lo] << 24) | region_of(rx, ry);
+                }
+                if (lost) emit2(pass, pr);
+            }
+        }
+    }
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -890,6 +1005,7 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
 // ---------------------------------------------------------------------------
 constexpr uint32_t kScanThreads = 1024;
 constexpr uint32_t kBuckets = 8;
+constexpr uint32_t kScanCache = 16;          // regions per thread held in registers
 
 __device__ __forceinline__ uint32_t launch_bucket(uint32_t c)
 {
@@ -928,54 +1044,106 @@ __global__ __launch_bounds__(kScanThreads) void k_bin_scan(BinBuffers bins, cons
     __shared__ uint32_t s_reg[kBuckets * kScanThreads];    // [bucket][thread]
     __shared__ uint32_t s_pair[kBuckets * kScanThreads];
     __shared__ uint32_t s_wave[kScanThreads / 64];
+    XRT_STAMP(kStampScan + 0);
     const uint32_t n = bins.regions_x * bins.regions_y;
     const uint32_t tid = threadIdx.x;
     const uint32_t G = bs->global_count;
-    const uint32_t pairs_total = bs->pair_count;
+    const uint32_t pair_total = bs->pair_count;
+    // The first kScanCache regions of this thread stay in registers (all
+    // loads in flight together); images past kScanCache x kScanThreads
+    // regions reload the rest.
+    uint32_t cc[kScanCache];
 #pragma unroll
-    for (uint32_t q = 0; q < kBuckets; ++q) {
-        s_reg[q * kScanThreads + tid] = 0u;
-        s_pair[q * kScanThreads + tid] = 0u;
+    for (uint32_t q = 0; q < kScanCache; ++q) {
+        const uint32_t r = tid + q * kScanThreads;
+        cc[q] = r < n ? bins.counts[(size_t)r * kCounterStride] : 0u;
     }
-    for (uint32_t r = tid; r < n; r += kScanThreads) {     // own column: no atomics
-        const uint32_t c = bins.counts[r];
-        const uint32_t b = launch_bucket(c);
-        s_reg[b * kScanThreads + tid] += 1u;
-        s_pair[b * kScanThreads + tid] += c;
+    uint32_t nreg[kBuckets], npair[kBuckets];
+#pragma unroll
+    for (uint32_t b = 0; b < kBuckets; ++b) { nreg[b] = 0u; npair[b] = 0u; }
+    auto tally = [&](uint32_t c) {
+        const uint32_t bk = launch_bucket(c);
+#pragma unroll
+        for (uint32_t b = 0; b < kBuckets; ++b) {
+            nreg[b] += b == bk ? 1u : 0u;
+            npair[b] += b == bk ? c : 0u;
+        }
+    };
+#pragma unroll
+    for (uint32_t q = 0; q < kScanCache; ++q)
+        if (tid + q * kScanThreads < n) tally(cc[q]);
+    for (uint32_t r = tid + kScanCache * kScanThreads; r < n; r += kScanThreads)
+        tally(bins.counts[(size_t)r * kCounterStride]);
+#pragma unroll
+    for (uint32_t b = 0; b < kBuckets; ++b) {
+        s_reg[b * kScanThreads + tid] = nreg[b];
+        s_pair[b * kScanThreads + tid] = npair[b];
     }
     __syncthreads();
+    XRT_STAMP(kStampScan + 1);
     scan_table(s_reg, s_wave);
     const uint32_t total = scan_table(s_pair, s_wave);
-    for (uint32_t r = tid; r < n; r += kScanThreads) {
-        const uint32_t c = bins.counts[r];
-        const uint32_t b = launch_bucket(c);
-        const uint32_t slot = s_reg[b * kScanThreads + tid]++;
-        const uint32_t lo = s_pair[b * kScanThreads + tid];
-        s_pair[b * kScanThreads + tid] = lo + c;
+    XRT_STAMP(kStampScan + 2);
+    // this thread's first slot and list position per bucket
+#pragma unroll
+    for (uint32_t b = 0; b < kBuckets; ++b) {
+        nreg[b] = s_reg[b * kScanThreads + tid];
+        npair[b] = s_pair[b * kScanThreads + tid];
+    }
+    auto place = [&](uint32_t r, uint32_t c) {
+        const uint32_t bk = launch_bucket(c);
+        uint32_t slot = 0, lo = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < kBuckets; ++b) {
+            if (b == bk) {
+                slot = nreg[b];
+                lo = npair[b];
+                nreg[b] += 1u;
+                npair[b] += c;
+            }
+        }
         bins.slots[slot] = make_uint4(r, lo, c, G);
         bins.spans[r] = make_uint2(lo, c);
-        bins.cursor[r] = lo;
+        bins.cursor[(size_t)r * kCounterStride] = lo;
+    };
+#pragma unroll
+    for (uint32_t q = 0; q < kScanCache; ++q) {
+        const uint32_t r = tid + q * kScanThreads;
+        if (r < n) place(r, cc[q]);
     }
+    for (uint32_t r = tid + kScanCache * kScanThreads; r < n; r += kScanThreads)
+        place(r, bins.counts[(size_t)r * kCounterStride]);
     if (tid == 0) {
-        st->bin.pair_count = pairs_total;
+        st->bin.pair_count = pair_total;
         st->bin.global_count = G;
         st->bin.total = total;
-        st->bin.overflow = pairs_total > bins.cap ? 1u : 0u;
+        st->bin.overflow = (total > bins.cap || pair_total > bins.cap) ? 1u : 0u;
     }
+    XRT_STAMP(kStampScan + 3);
 }
 
-// k_bin_fill: one thread per pair, grid-stride.
+// k_bin_fill: one thread per pair, grid-stride with block-uniform trip counts;
+// one cursor atomic per run of equal regions across a wave.
 __global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const DevStats* __restrict__ st)
 {
+    XRT_STAMP(kStampFill + 2 * blockIdx.x);
     if (st->bin.overflow) return;                  // kernel-uniform
     const uint32_t n = st->bin.pair_count;
     const uint32_t n_regions = bins.regions_x * bins.regions_y;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint2 pr = bins.pairs[k];
-        if (pr.y >= n_regions) continue;           // cannot happen; never write out of range
-        const uint32_t at = atomicAdd(&bins.cursor[pr.y], 1u);
-        if (at < bins.cap) bins.list[at] = pr.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t k = base + threadIdx.x;
+        uint2 pr = make_uint2(0u, kEmpty);
+        if (k < n) pr = bins.pairs[k];
+        const bool active = pr.y < n_regions;      // (always, for k < n) never write out of range
+        uint32_t head, len;
+        lane_runs(active, pr.y, head, len);
+        uint32_t at = 0;
+        if (active && head == lane) at = atomicAdd(&bins.cursor[(size_t)pr.y * kCounterStride], len);
+        at = __shfl(at, (int)head) + (lane - head);
+        if (active && at < bins.cap) bins.list[at] = pr.x;
     }
+    XRT_STAMP(kStampFill + 2 * blockIdx.x + 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1301,7 +1469,7 @@ __global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs,
     if (bins.counts) {
         const uint32_t n = bins.regions_x * bins.regions_y;
         for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
-            bins.counts[r] = 0u;
+            bins.counts[(size_t)r * kCounterStride] = 0u;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             BinState z = {};
             *bs = z;

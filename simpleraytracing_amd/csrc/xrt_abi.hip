@@ -42,13 +42,13 @@ struct xrt_context {
     uint32_t* d_bin_aux = nullptr;      // cursor | spans | slots
     size_t bin_aux_cap = 0;
     bool bins_clean = false;           // counts + control block are zero
-    uint2* d_bin_pairs = nullptr;
+    uint2* d_bin_pairs = nullptr;       // (triangle, region) pairs
     size_t bin_pairs_cap = 0;
+    size_t bin_list_want = 0;           // pair/list capacity wanted (grown by sizing)
     uint32_t* d_bin_list = nullptr;
     size_t bin_list_cap = 0;
     uint32_t* d_global_list = nullptr;
     size_t global_list_cap = 0;
-    size_t bin_list_want = 0;          // grown after a frame overflowed its lists
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     uint32_t* d_overflow = nullptr;
     size_t overflow_cap = 0;
@@ -220,16 +220,19 @@ int bin_buffers(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, BinState
                 hipStream_t stream)
 {
     const uint64_t T = ctx->num_tris;
-    const size_t ctl_words = 4;   // BinState
-    static_assert(sizeof(BinState) == 16, "BinState is 4 words");
+    static_assert(sizeof(BinState) <= kCounterStride * sizeof(uint32_t), "BinState fits its line");
     int rc;
-    if (ctl_words + n_regions > ctx->bin_counts_cap || !ctx->d_bin_counts) {
-        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, ctl_words + (size_t)n_regions))) return rc;
+    // control block padded to a line, then one line-padded counter per region
+    const size_t counter_words = kCounterStride + (size_t)kCounterStride * n_regions;
+    if (counter_words > ctx->bin_counts_cap || !ctx->d_bin_counts) {
+        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, counter_words))) return rc;
         ctx->bins_clean = false;
     }
-    // aux words: cursor (1/region) | spans (2/region) | slots (4/region), 16-B aligned parts
+    // aux words: cursor (kCounterStride/region) | spans (2/region) | slots (4/region)
     const size_t nr = ((size_t)n_regions + 3) & ~(size_t)3;
-    if ((rc = ensure(ctx, ctx->d_bin_aux, ctx->bin_aux_cap, 7 * nr))) return rc;
+    if ((rc = ensure(ctx, ctx->d_bin_aux, ctx->bin_aux_cap, (kCounterStride + 6) * nr))) return rc;
+    // pair and list capacity: sized by the last frame of this geometry
+    // (xrt_context::BinKey), at least 4 pairs per triangle
     const size_t want = std::max<size_t>({ctx->bin_list_want, 4 * (size_t)T, (size_t)n_regions, 65536});
     if ((rc = ensure(ctx, ctx->d_bin_list, ctx->bin_list_cap, want))) return rc;
     if ((rc = ensure(ctx, ctx->d_bin_pairs, ctx->bin_pairs_cap, ctx->bin_list_cap))) return rc;
@@ -239,10 +242,10 @@ int bin_buffers(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, BinState
         ctx->bins_clean = true;
     }
     ctl = reinterpret_cast<BinState*>(ctx->d_bin_counts);
-    bins.counts = ctx->d_bin_counts + ctl_words;
+    bins.counts = ctx->d_bin_counts + kCounterStride;
     bins.cursor = ctx->d_bin_aux;
-    bins.spans = reinterpret_cast<uint2*>(ctx->d_bin_aux + nr);
-    bins.slots = reinterpret_cast<uint4*>(ctx->d_bin_aux + 3 * nr);
+    bins.spans = reinterpret_cast<uint2*>(ctx->d_bin_aux + kCounterStride * nr);
+    bins.slots = reinterpret_cast<uint4*>(ctx->d_bin_aux + (kCounterStride + 2) * nr);
     bins.pairs = ctx->d_bin_pairs;
     bins.list = ctx->d_bin_list;
     bins.global_list = ctx->d_global_list;
@@ -554,6 +557,20 @@ int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint
     *n_records = ctx->last_blocks;
     const size_t bytes = std::min<size_t>((size_t)capacity, (size_t)ctx->last_blocks * sizeof(BlockStats));
     if (bytes && dst) XRT_HIP(ctx, hipMemcpy(dst, ctx->d_block_stats, bytes, hipMemcpyDeviceToHost));
+    return XRT_OK;
+}
+
+int xrt_debug_stamps(xrt_context* ctx, uint64_t* dst, uint64_t n)
+{
+    if (!ctx || (n && !dst)) return XRT_ERR_ARGUMENT;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    XRT_HIP(ctx, hipDeviceSynchronize());
+    n = std::min<uint64_t>(n, kStampsN);
+#if XRT_STAMPS
+    if (n) XRT_HIP(ctx, hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), n * sizeof(uint64_t)));
+#else
+    std::memset(dst, 0, n * sizeof(uint64_t));
+#endif
     return XRT_OK;
 }
 
