@@ -189,6 +189,41 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
     }
 }
 
+// One wave's statistics as one BlockStats record (no LDS, no barrier): the
+// lane sums are reduced across the wave and lane 0 stores the record.
+__device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t candidates,
+                                                 BlockStats* out, uint32_t index, uint64_t t_start = 0)
+{
+    uint32_t hits = ws.lane_hits, mx = ws.lane_max;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        hits += __shfl_xor(hits, off);
+        const uint32_t o = __shfl_xor(mx, off);
+        mx = mx > o ? mx : o;
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        BlockStats b;
+        b.rays = ws.rays;
+        b.hit_rays = ws.hit_rays;
+        b.odd_rays = ws.odd_rays;
+        b.overflow_rays = ws.overflow_rays;
+        b.hits = hits;
+        b.tile_tests = ws.tile_tests;
+        b.candidates = candidates;
+        b.max_hits = mx;
+        b.pad = 0;
+#if XRT_STAMPS
+        b.rays = t_start;
+        b.hit_rays = __builtin_amdgcn_s_memrealtime();
+        b.pad = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
+        b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+#else
+        (void)t_start;
+#endif
+        out[index] = b;
+    }
+}
+
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
                                            uint32_t row, uint32_t col, const HitList& hl,
                                            WaveStats& ws)
@@ -684,7 +719,7 @@ struct BinBuffers {
     uint32_t* cursor;        // [n_regions * kCounterStride] fill cursors
     uint4* slots;            // [n_regions]   launch order: (region, offset, count, global count)
     uint2* pairs;            // [cap]         (triangle, region)
-    uint32_t* list;          // [cap]         region candidate lists
+    uint2* list;             // [cap]         region candidate lists: (triangle, 16-bit tile mask)
     uint32_t* global_list;   // [T]
     uint32_t cap;            // capacity of pairs and list
     uint32_t regions_x, regions_y;
@@ -1124,7 +1159,8 @@ __global__ __launch_bounds__(kScanThreads) void k_bin_scan(BinBuffers bins, cons
 
 // k_bin_fill: one thread per pair, grid-stride with block-uniform trip counts;
 // one cursor atomic per run of equal regions across a wave.
-__global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const DevStats* __restrict__ st)
+__global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const float4* __restrict__ culls,
+                                                  RenderParams p, const DevStats* __restrict__ st)
 {
     XRT_STAMP(kStampFill + 2 * blockIdx.x);
     if (st->bin.overflow) return;                  // kernel-uniform
@@ -1141,7 +1177,23 @@ __global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const DevStat
         uint32_t at = 0;
         if (active && head == lane) at = atomicAdd(&bins.cursor[(size_t)pr.y * kCounterStride], len);
         at = __shfl(at, (int)head) + (lane - head);
-        if (active && at < bins.cap) bins.list[at] = pr.x;
+        if (active && at < bins.cap) {
+            // which of the region's 16 tiles (8x8) the relaxed edges pass:
+            // the render's tile test, evaluated once per (region, triangle)
+            const uint32_t T = p.num_triangles;
+            const float4 e0 = culls[(size_t)T + pr.x], e1 = culls[2 * (size_t)T + pr.x],
+                         e2 = culls[3 * (size_t)T + pr.x];
+            const uint32_t rx0 = (pr.y % bins.regions_x) * kRegion;
+            const uint32_t ry0 = p.row_begin + (pr.y / bins.regions_x) * kRegion;
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 16u; ++t) {
+                const float xc = (float)(rx0 + (t & 3u) * 8u) + 3.5f;
+                const float yc = (float)(ry0 + (t >> 2) * 8u) + 3.5f;
+                mask |= edges_pass(e0, e1, e2, xc, yc, 3.5f, 3.5f) ? (1u << t) : 0u;
+            }
+            bins.list[at] = make_uint2(pr.x, mask);
+        }
     }
     XRT_STAMP(kStampFill + 2 * blockIdx.x + 1);
 }
@@ -1160,28 +1212,65 @@ __global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const DevStat
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs, uint32_t j0,
                                                  uint32_t j1, bool two, float dx, float dy,
-                                                 float dz, HitList& hl)
+                                                 float dz, HitList& hl, uint32_t& tier)
 {
     const TriRec a = recs[j0];
     bool h0, h1 = false;
-    const float t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
-                              a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
-    float t1 = 0.0f;
+    float t0, t1 = 0.0f;
+#if XRT_PACKED
+    if (two) {
+        const TriRec b = recs[j1];
+        mt_exact2(dx, dy, dz, xrt_f2{a.e1x, b.e1x}, xrt_f2{a.e1y, b.e1y}, xrt_f2{a.e1z, b.e1z},
+                  xrt_f2{a.e2x, b.e2x}, xrt_f2{a.e2y, b.e2y}, xrt_f2{a.e2z, b.e2z},
+                  xrt_f2{a.tvx, b.tvx}, xrt_f2{a.tvy, b.tvy}, xrt_f2{a.tvz, b.tvz},
+                  xrt_f2{a.qvx, b.qvx}, xrt_f2{a.qvy, b.qvy}, xrt_f2{a.qvz, b.qvz},
+                  xrt_f2{a.tnum, b.tnum}, t0, h0, t1, h1);
+    } else {
+        t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz,
+                      a.qvx, a.qvy, a.qvz, a.tnum, h0);
+    }
+#else
+    t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
+                  a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
     if (two) {
         const TriRec b = recs[j1];
         t1 = mt_exact(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
                       b.qvx, b.qvy, b.qvz, b.tnum, h1);
     }
+#endif
+#if XRT_TIERED
+    // Tiered insertion: the network spans only the slots a lane of this wave
+    // can reach (every lane holds <= tier - 2 hits before the pair).
+    while (tier < (uint32_t)kMaxHits && __ballot(hl.n + 2u > tier)) tier *= 2u;   // wave-uniform
+    if (tier == 4u) {
+        hl.push_if_first<4>(h0, t0);
+        hl.push_if_first<4>(h1, t1);
+    } else if (tier == 8u) {
+        hl.push_if_first<8>(h0, t0);
+        hl.push_if_first<8>(h1, t1);
+    } else {
+        hl.push_if(h0, t0);
+        hl.push_if(h1, t1);
+    }
+#else
+    (void)tier;
     hl.push_if(h0, t0);
     hl.push_if(h1, t1);
+#endif
 }
+
+// fetch(k) returns (triangle, tile mask) of the k-th candidate: bit t of the
+// mask is set when the triangle's relaxed edges pass tile t of the region
+// (evaluated by k_bin_fill); kTestEdges asks the wave to evaluate them itself
+// (global-list and whole-mesh candidates).
+constexpr uint32_t kTestEdges = 0x10000u;
 
 template <typename Fetch>
 __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Outputs& out,
                                                  const TriRec* __restrict__ recs,
                                                  const float4* __restrict__ culls, uint32_t tx0,
-                                                 uint32_t ty0, uint32_t n_cand, Fetch fetch,
-                                                 WaveStats& ws)
+                                                 uint32_t ty0, uint32_t tile, uint32_t n_cand,
+                                                 Fetch fetch, WaveStats& ws)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = p.num_triangles;
@@ -1193,25 +1282,64 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     bool have_ray = false;                        // wave-uniform
+#if XRT_EAGER_RAY
+    // The directions are computed while the candidate loads are in flight.
+    if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+#endif
     HitList hl;
     hl.init();
     uint32_t tests = 0;
+    uint32_t tier = 4;                            // wave-uniform insertion tier (XRT_TIERED)
     for (uint32_t base = 0; base < n_cand; base += 64u) {
         const uint32_t k = base + lane;
-        uint32_t j = k < n_cand ? fetch(k) : 0u;
-        j = j < T ? j : 0u;                       // cannot happen; never read out of range
-        bool pass = false;
-        if (k < n_cand)
+        const uint2 cand = k < n_cand ? fetch(k) : make_uint2(0u, 0u);
+        const uint32_t j = cand.x < T ? cand.x : 0u;   // (always) never read out of range
+        bool pass = (cand.y >> tile) & 1u;
+        if (cand.y & kTestEdges)
             pass = edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
                               xc, yc, 3.5f, 3.5f);
         unsigned long long m = __ballot(pass);
         if (!m) continue;
         tests += (uint32_t)__popcll(m);
         if (!have_ray) {
+#if !XRT_EAGER_RAY
             if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+#endif
             have_ray = true;
         }
         if (p.ablate & kAblateExact) continue;
+#if XRT_VREC
+        // Every survivor lane loads its own record (all in flight together);
+        // the tests broadcast them with v_readlane.
+        TriRec mine = {};
+        if (pass) mine = recs[j];
+        while (m) {
+            const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            const bool two = m != 0ull;
+            const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m) : k0;
+            if (two) m &= m - 1ull;
+            auto bc = [&](float v, uint32_t l) {
+                return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+            };
+            bool h0, h1 = false;
+            const float t0 = mt_exact(dx, dy, dz, bc(mine.e1x, k0), bc(mine.e1y, k0), bc(mine.e1z, k0),
+                                      bc(mine.e2x, k0), bc(mine.e2y, k0), bc(mine.e2z, k0),
+                                      bc(mine.tvx, k0), bc(mine.tvy, k0), bc(mine.tvz, k0),
+                                      bc(mine.qvx, k0), bc(mine.qvy, k0), bc(mine.qvz, k0),
+                                      bc(mine.tnum, k0), h0);
+            float t1 = 0.0f;
+            if (two)
+                t1 = mt_exact(dx, dy, dz, bc(mine.e1x, k1), bc(mine.e1y, k1), bc(mine.e1z, k1),
+                              bc(mine.e2x, k1), bc(mine.e2y, k1), bc(mine.e2z, k1),
+                              bc(mine.tvx, k1), bc(mine.tvy, k1), bc(mine.tvz, k1),
+                              bc(mine.qvx, k1), bc(mine.qvy, k1), bc(mine.qvz, k1),
+                              bc(mine.tnum, k1), h1);
+            hl.push_if(h0, t0);
+            hl.push_if(h1, t1);
+        }
+        continue;
+#endif
         while (m) {
             const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
@@ -1223,7 +1351,7 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
                 m &= m - 1ull;
                 j1 = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)k1);
             }
-            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl);
+            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl, tier);
         }
     }
     ws.tile_tests += tests;
@@ -1240,16 +1368,22 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
     if (out.image_u8) out.image_u8[o] = 255u;
 }
 
-__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_binned(
+constexpr uint32_t kTileWaves = XRT_TILE_WAVES;   // tile waves per workgroup (divides 16)
+
+// One 8x8 tile per wave, kTileWaves waves per workgroup (regions in
+// the binning scan's launch order); each wave stores its own statistics
+// record, so no wave waits for another.  8 waves per SIMD: the tile waves
+// are latency-bound, and occupancy is what hides it.
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins)
 {
     const uint64_t t_start = block_start_stamp();
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint4 slot = bins.slots[blockIdx.x >> 2];              // 4 workgroups per region
+    const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // tile wave of the grid
+    const uint4 slot = bins.slots[g >> 4];
     const bool overflow = out.stats->bin.overflow != 0u;
     const uint32_t region = slot.x;
-    const uint32_t tile = (blockIdx.x & 3u) * 4u + wave;         // 16 tiles per region
+    const uint32_t tile = g & 15u;
     const uint32_t tx0 = (region % bins.regions_x) * kRegion + (tile & 3u) * 8u;
     const uint32_t ty0 = p.row_begin + (region / bins.regions_x) * kRegion + (tile >> 2) * 8u;
     WaveStats ws = {};
@@ -1257,18 +1391,21 @@ __global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_binned(
     if (tx0 < p.width && ty0 < p.row_end) {                     // wave-uniform
         if (overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
             n_cand = p.num_triangles;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand, [](uint32_t k) { return k; }, ws);
+            render_tile_wave(p, out, recs, culls, tx0, ty0, tile, n_cand,
+                             [](uint32_t k) { return make_uint2(k, kTestEdges); }, ws);
         } else {
             const uint32_t n_local = slot.z;
-            const uint32_t* __restrict__ local = bins.list + slot.y;
+            const uint2* __restrict__ local = bins.list + slot.y;
             const uint32_t* __restrict__ glob = bins.global_list;
             n_cand = n_local + slot.w;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand,
-                             [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
+            render_tile_wave(p, out, recs, culls, tx0, ty0, tile, n_cand,
+                             [&](uint32_t k) {
+                                 return k < n_local ? local[k] : make_uint2(glob[k - n_local], kTestEdges);
+                             }, ws);
         }
     }
-    // candidates are counted once per region (by its first workgroup)
-    store_block_stats(ws, (blockIdx.x & 3u) == 0u ? n_cand : 0u, out.block_stats, t_start);
+    // candidates are counted once per region (by its tile 0)
+    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -1447,10 +1584,10 @@ __global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs,
             const uint32_t region = (o / p.width / kRegion) * bins.regions_x + col / kRegion;
             const uint2 span = bins.spans[region];
             const uint32_t n_local = span.y;
-            const uint32_t* __restrict__ local = bins.list + span.x;
+            const uint2* __restrict__ local = bins.list + span.x;
             const uint32_t* __restrict__ glob = bins.global_list;
             distance = overflow_distance(s, recs, n_local + out.stats->bin.global_count,
-                                         [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; },
+                                         [&](uint32_t k) { return k < n_local ? local[k].x : glob[k - n_local]; },
                                          dx, dy, dz, n_hits);
         } else {
             distance = overflow_distance(s, recs, p.num_triangles, [](uint32_t k) { return k; }, dx,

@@ -45,7 +45,7 @@ struct xrt_context {
     uint2* d_bin_pairs = nullptr;       // (triangle, region) pairs
     size_t bin_pairs_cap = 0;
     size_t bin_list_want = 0;           // pair/list capacity wanted (grown by sizing)
-    uint32_t* d_bin_list = nullptr;
+    uint2* d_bin_list = nullptr;        // (triangle, tile mask) region lists
     size_t bin_list_cap = 0;
     uint32_t* d_global_list = nullptr;
     size_t global_list_cap = 0;
@@ -290,9 +290,10 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.stats = ctx->d_stats;
     const uint32_t n_regions = rows ? rx * ry : 0u;
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
-              : binned                     ? dim3(4 * n_regions)   // 4 workgroups (16 tile waves) per region
+              : binned                     ? dim3(16 / kTileWaves * n_regions)   // 16 tile waves per region
                                            : dim3(rx, ry);
-    const uint32_t n_blocks = rows ? grid.x * grid.y : 0u;
+    // stats records: one per workgroup, one per tile wave for BINNED
+    const uint32_t n_blocks = rows ? grid.x * grid.y * (binned ? kTileWaves : 1u) : 0u;
     if ((rc = ensure(ctx, ctx->d_block_stats, ctx->block_stats_cap, n_blocks))) return rc;
     ctx->last_blocks = n_blocks;
     out.block_stats = ctx->d_block_stats;
@@ -340,7 +341,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         XRT_HIP(ctx, hipGetLastError());
         const unsigned fill_blocks = (unsigned)std::min<uint64_t>(2048, ((uint64_t)bins.cap + 255) / 256);
         hipLaunchKernelGGL(k_bin_fill, dim3(std::max(1u, fill_blocks)), dim3(256), 0, stream, bins,
-                           (const DevStats*)ctx->d_stats);
+                           (const float4*)ctx->d_cull, p, (const DevStats*)ctx->d_stats);
         XRT_HIP(ctx, hipGetLastError());
     }
 
@@ -367,7 +368,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
                                   ctx->d_recs, ctx->d_cull, p, out);
         else
-            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(256), 0, stream, t0, t1, 0, ctx->d_recs,
+            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, ctx->d_recs,
                                   ctx->d_cull, p, out, bins);
         XRT_HIP(ctx, hipGetLastError());
         ctx->last_t0 = t0;
