@@ -215,11 +215,12 @@ int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
 int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
 
 /*
- * Diagnostics: copies the last render's per-workgroup records (64 bytes each:
- * six u64 counters -- rays, hit rays, odd rays, overflow rays, hits, wave-level
- * triangle tests -- then u64 candidates, u32 max hits, u32 pad; builds with
- * XRT_STAMPS put timestamps and hardware ids there instead) into `dst`, at most
- * `capacity` bytes; `*n_records` receives the number of workgroups.
+ * Diagnostics: copies the last render's statistics records (32 bytes each, one
+ * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
+ * overflow rays, hits, wave-level triangle tests, candidates, max hits; builds
+ * with XRT_STAMPS put u64 start/end timestamps and hardware ids there instead)
+ * into `dst`, at most `capacity` bytes; `*n_records` receives the number of
+ * records.
  */
 int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint64_t* n_records);
 

@@ -129,7 +129,8 @@ def load():
     """Returns the bound libxrt.so; raises if it has not been built."""
     global _lib
     if _lib is None:
-        path = lib_path("libxrt.so")
+        # XRT_LIB: a variant build (tools/build_variants.sh) for A/B timing only
+        path = os.environ.get("XRT_LIB") or lib_path("libxrt.so")
         if not os.path.exists(path):
             raise RuntimeError(
                 f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -50,6 +50,12 @@
 #ifndef XRT_TIERED
 #define XRT_TIERED 0      // binned tiles: hit insertion over 4 / 8 / 16 slots by wave occupancy (A/B: no gain)
 #endif
+#ifndef XRT_PREP_SETPRIO
+#define XRT_PREP_SETPRIO 1   // preparation kernels raise their wave priority (s_setprio 3)
+#endif
+#ifndef XRT_FINISH_BLOCKS
+#define XRT_FINISH_BLOCKS 64   // k_finish workgroups (statistics slices, overflow rays)
+#endif
 #ifndef XRT_STAMPS
 #define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
 #endif

@@ -27,11 +27,12 @@ namespace XRT_KERNEL_NS {
 
 // Binning control block.  Zero on entry to a binned frame: it is cleared when
 // allocated and by every binned frame's k_finish for the next one.
+// Cleared with the region counters before every binned frame's k_prep.
 struct BinState {
-    unsigned int pair_count;    // (triangle, region) pairs emitted by k_prep
+    unsigned int max_count;     // largest region count of the frame (list sizing)
     unsigned int global_count;  // triangles in the global list
-    unsigned int total;         // sum of the region counts (k_bin_scan)
-    unsigned int overflow;      // pairs over capacity: regions fall back to the whole mesh
+    unsigned int overflow;      // some region count exceeded the list capacity
+    unsigned int pad;
 };
 
 struct DevStats {
@@ -57,11 +58,12 @@ struct CullParams {
 // Per-workgroup statistics, written with plain stores (one record per block)
 // and summed by k_stats_reduce: same-address global atomics from every wave
 // serialise in L2 and dominated short renders.
+// 32 bytes; XRT_STAMPS builds store the start/end s_memrealtime in the first
+// four words (two u64), the HW_ID in `candidates` and the XCC id in `max_hits`.
 struct BlockStats {
-    unsigned long long rays, hit_rays, odd_rays, overflow_rays, hits, tile_tests, candidates;
-    unsigned int max_hits, pad;
+    unsigned int rays, hit_rays, odd_rays, overflow_rays, hits, tile_tests, candidates, max_hits;
 };
-static_assert(sizeof(BlockStats) == 64, "BlockStats must be 64 bytes");
+static_assert(sizeof(BlockStats) == 32, "BlockStats must be 32 bytes");
 
 struct Outputs {
     float* image;
@@ -129,13 +131,17 @@ __device__ __forceinline__ uint64_t block_start_stamp()
 #endif
 }
 
+#if XRT_PREP_SETPRIO
+#define XRT_PREP_PRIO() __builtin_amdgcn_s_setprio(3)
+#else
+#define XRT_PREP_PRIO() do {} while (0)
+#endif
+
 // Phase timestamps of the binning kernels (XRT_STAMPS builds): one u64 per
 // (workgroup, phase) in g_stamps; the workgroup's threads are synchronised
 // first so a stamp marks the end of the phase for the whole workgroup.
 constexpr uint32_t kStampsN = 1u << 16;
 constexpr uint32_t kStampPrep = 0;          // k_prep: 8 per workgroup
-constexpr uint32_t kStampScan = 60000;      // k_bin_scan: 8
-constexpr uint32_t kStampFill = 32768;      // k_bin_fill: 2 per workgroup
 #if XRT_STAMPS
 __device__ uint64_t g_stamps[kStampsN];
 #define XRT_STAMP(idx)                                                               \
@@ -146,6 +152,24 @@ __device__ uint64_t g_stamps[kStampsN];
 #else
 #define XRT_STAMP(idx) do {} while (0)
 #endif
+
+// XRT_STAMPS builds: workgroup/wave start and end time and hardware ids in
+// place of the counters (diagnostics only; the totals are then wrong).
+__device__ __forceinline__ void stamp_record(BlockStats& b, uint64_t t_start)
+{
+#if XRT_STAMPS
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    b.rays = (unsigned int)t_start;
+    b.hit_rays = (unsigned int)(t_start >> 32);
+    b.odd_rays = (unsigned int)t_end;
+    b.overflow_rays = (unsigned int)(t_end >> 32);
+    b.candidates = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);    // HW_REG_XCC_ID
+#else
+    (void)b;
+    (void)t_start;
+#endif
+}
 
 __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
                                                   BlockStats* out, uint64_t t_start = 0)
@@ -177,14 +201,7 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
             b.max_hits = b.max_hits > s_ws[w].lane_max ? b.max_hits : s_ws[w].lane_max;
         }
         b.candidates = candidates;
-#if XRT_STAMPS
-        b.rays = t_start;
-        b.hit_rays = __builtin_amdgcn_s_memrealtime();
-        b.pad = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
-        b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
-#else
-        (void)t_start;
-#endif
+        stamp_record(b, t_start);
         out[blockIdx.y * gridDim.x + blockIdx.x] = b;
     }
 }
@@ -211,15 +228,7 @@ __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t c
         b.tile_tests = ws.tile_tests;
         b.candidates = candidates;
         b.max_hits = mx;
-        b.pad = 0;
-#if XRT_STAMPS
-        b.rays = t_start;
-        b.hit_rays = __builtin_amdgcn_s_memrealtime();
-        b.pad = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
-        b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
-#else
-        (void)t_start;
-#endif
+        stamp_record(b, t_start);
         out[index] = b;
     }
 }
@@ -691,62 +700,31 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 }
 
 // ---------------------------------------------------------------------------
-// Binning (XRT_KERNEL_BINNED): the conservative footprints are assigned to
-// 32x32 regions once per frame, in three wide stages with no serial tail:
-//   k_prep      per triangle: footprint and its rectangle of regions; then the
-//               workgroup expands the rectangles of its 256 triangles into
-//               cells, one thread per cell (load-balanced by a search over the
-//               rectangles' prefix sum), tests each cell's 32x32 square against
-//               the relaxed edges, stages the passing (triangle, region) pairs
-//               in LDS, reserves their range with one atomic and copies them
-//               out; regions are counted with fire-and-forget atomics on
-//               line-padded counters;
-//   k_bin_scan  one workgroup: region list offsets and the launch order
-//               (regions by descending candidate count, in log2 buckets);
-//   k_bin_fill  one thread per pair: scatter into the region lists.
-// Footprints over more than kGlobalRegions regions go to a global list every
-// region reads.
+// Binning (XRT_KERNEL_BINNED), inside k_prep: each triangle's conservative
+// footprint is assigned to the 32x32 regions it may touch, straight into
+// fixed-capacity region lists -- slot = atomic increment of the region's
+// count (line-padded counters, all of a lane's atomics in flight together),
+// entry = (triangle, 16-bit mask of the region's 8x8 tiles its relaxed edges
+// pass).  No scan and no second pass, so the whole preparation is one kernel.
+// The capacity per region is sized from the largest count of the last frame
+// of the same geometry (xrt_context::BinKey); a region past it renders from
+// the whole mesh (exact, slower).  Footprints over more than kGlobalRegions
+// regions go to a global list every region reads.
 // ---------------------------------------------------------------------------
 // Region counters touched by atomics are padded to one 128-B L2 line each:
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
-constexpr uint32_t kWaveStage = 1024;        // pairs staged in LDS per k_prep wave
 constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
 
 struct BinBuffers {
-    uint32_t* counts;        // [n_regions * kCounterStride] zero on entry to a binned frame
-    uint2* spans;            // [n_regions]   (list offset, count) per region
-    uint32_t* cursor;        // [n_regions * kCounterStride] fill cursors
-    uint4* slots;            // [n_regions]   launch order: (region, offset, count, global count)
-    uint2* pairs;            // [cap]         (triangle, region)
-    uint2* list;             // [cap]         region candidate lists: (triangle, 16-bit tile mask)
+    uint32_t* counts;        // [n_regions * kCounterStride] cleared before every binned frame
+    uint32_t* list;          // [n_regions * cap] triangle ids per region
     uint32_t* global_list;   // [T]
-    uint32_t cap;            // capacity of pairs and list
+    uint32_t cap;            // list capacity per region
     uint32_t regions_x, regions_y;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-
-// Runs of consecutive active lanes holding the same key (a wave-uniform call
-// with every lane present).  `head` is the lane that starts this lane's run,
-// `len` (valid in the head) the run length: one atomic per run replaces up to
-// 64 same-address atomics, which serialise in L2.
-__device__ __forceinline__ void lane_runs(bool active, uint32_t key, uint32_t& head, uint32_t& len)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t prev = __shfl_up(key, 1);
-    const uint32_t next = __shfl_down(key, 1);
-    const unsigned long long act = __ballot(active);
-    const bool same_prev = lane > 0u && ((act >> (lane - 1u)) & 1ull) && prev == key;
-    const bool same_next = lane < 63u && ((act >> (lane + 1u)) & 1ull) && next == key;
-    const unsigned long long heads = __ballot(active && !same_prev);
-    const unsigned long long tails = __ballot(active && !same_next);
-    const unsigned long long upto = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
-    const unsigned long long h = heads & upto;
-    head = h ? 63u - (uint32_t)__clzll(h) : 0u;
-    const unsigned long long t = tails >> lane;
-    len = t ? (uint32_t)__builtin_ctzll(t) + 1u : 1u;
-}
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
 // footprint box may touch; false when it touches none.
@@ -787,34 +765,11 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
     return true;
 }
 
-// Exclusive scan over the workgroup of one value per thread; `total` is the
-// workgroup sum.  `s_wave` holds one word per wave.  Contains barriers.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& total)
-{
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(inc, off);
-        if (lane >= (uint32_t)off) inc += o;
-    }
-    if (lane == 63u) s_wave[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-    total = 0;
-    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
-        const uint32_t t = s_wave[w];
-        before += w < wave ? t : 0u;
-        total += t;
-    }
-    __syncthreads();
-    return before + inc - v;
-}
 
 // ---------------------------------------------------------------------------
 // k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
-// terms), cull planes and (binned) the triangle's region pairs.  Thread 0
-// also clears DevStats for the frame.
+// terms), cull planes and (binned) the triangle's region list entries.
+// Thread 0 also clears DevStats for the frame.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
@@ -822,6 +777,9 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
                                               float4* __restrict__ culls, BinBuffers bins,
                                               BinState* __restrict__ bs, DevStats* __restrict__ st)
 {
+    // The preparation of frame N+1 shares the CUs with frame N's render (prep
+    // stream): top wave priority keeps this latency-bound chain short.
+    XRT_PREP_PRIO();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
@@ -857,16 +815,12 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
     if (!bins.counts) return;                      // kernel-uniform
 
-    // Each wave stages its passing (triangle, region) pairs in its own LDS
-    // segment with a wave-uniform running count (no LDS atomics); the
-    // workgroup then reserves one range and copies the segments out.
-    __shared__ uint32_t s_pairs[4][kWaveStage];    // local triangle << 24 | region
     __shared__ float4 s_e[3][256];                 // relaxed edges (big triangles)
     __shared__ uint2 s_rect[256];                  // (x0 | x1 << 16, y0 | y1 << 16)
     __shared__ uint32_t s_big[256];                // big triangles (local index)
     __shared__ uint32_t s_cum[256];                // inclusive prefix of their cell counts
     __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_base[4];
+    __shared__ uint32_t s_max;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
@@ -876,37 +830,38 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     const uint32_t wr = x1 - x0 + 1u;
     const uint32_t cells = has ? wr * (y1 - y0 + 1u) : 0u;
     const bool big = cells > kSerialRegions;
+    if (tid == 0) s_max = 0u;
 
-    uint32_t wn = 0;                               // wave-uniform: pairs staged by this wave
-    bool lost = false;                             // staging segment overflowed
-    auto emit = [&](bool pass, uint32_t pr) {
-        const unsigned long long m = __ballot(pass);
-        if (pass) {
-            const uint32_t idx = wn + (uint32_t)__popcll(m & lt);
-            if (idx < kWaveStage) s_pairs[wave][idx] = pr;
-            atomicAdd(&bins.counts[(size_t)(pr & 0xFFFFFFu) * kCounterStride], 1u);
-        }
-        wn += (uint32_t)__popcll(m);
+    uint32_t my_max = 0;                           // 1 + the largest slot this thread took
+    auto place = [&](uint32_t r, uint32_t slot, uint32_t tri) {
+        my_max = max(my_max, slot + 1u);
+        if (slot < bins.cap) bins.list[(size_t)r * bins.cap + slot] = tri;
     };
-    auto region_of = [&](uint32_t rx, uint32_t ry) { return ry * bins.regions_x + rx; };
     auto cell_pass = [&](float4 e0, float4 e1, float4 e2, uint32_t rx, uint32_t ry) {
         const float xc = (float)(rx * kRegion) + 15.5f;
         const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
         return edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f);
     };
 
-    // Small rectangles: lane-serial, cell k of every lane in step k.
-    const uint32_t my_small = (has && !big) ? cells : 0u;
-    for (uint32_t k = 0; k < kSerialRegions; ++k) {
-        if (!__ballot(k < my_small)) break;         // wave-uniform
-        bool pass = false;
-        uint32_t pr = 0;
-        if (k < my_small) {
-            const uint32_t rx = x0 + k % wr, ry = y0 + k / wr;
-            pass = cell_pass(fp.e0, fp.e1, fp.e2, rx, ry);
-            pr = (tid << 24) | region_of(rx, ry);
+    // Small rectangles, lane-serial: the passing regions first, then all of
+    // their count atomics back to back, then the entries.
+    if (has && !big) {
+        uint32_t reg[kSerialRegions], slot[kSerialRegions];
+        uint32_t cx = x0, cy = y0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSerialRegions; ++k) {
+            reg[k] = kEmpty;
+            if (k < cells) {
+                if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = cy * bins.regions_x + cx;
+                if (++cx > x1) { cx = x0; ++cy; }
+            }
         }
-        emit(pass, pr);
+#pragma unroll
+        for (uint32_t k = 0; k < kSerialRegions; ++k)
+            slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kSerialRegions; ++k)
+            if (reg[k] != kEmpty) place(reg[k], slot[k], i);
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
@@ -939,263 +894,33 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
         }
         __syncthreads();
         const uint32_t total_cells = s_cum[nbig - 1u];
-        for (uint32_t c0 = 0; c0 < total_cells; c0 += blockDim.x) {     // block-uniform
-            const uint32_t c = c0 + tid;
-            bool pass = false;
-            uint32_t pr = 0;
-            if (c < total_cells) {
-                uint32_t lo = 0, hi = nbig - 1u;    // first b with s_cum[b] > c
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
-                }
-                const uint2 rc = s_rect[lo];
-                const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
-                const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
-                const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
-                pass = cell_pass(s_e[0][lo], s_e[1][lo], s_e[2][lo], rx, ry);
-                pr = (s_big[lo] << 24) | region_of(rx, ry);
+        const uint32_t i0 = blockIdx.x * blockDim.x;
+        for (uint32_t c = tid; c < total_cells; c += blockDim.x) {
+            uint32_t lo = 0, hi = nbig - 1u;        // first b with s_cum[b] > c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
             }
-            emit(pass, pr);
+            const uint2 rc = s_rect[lo];
+            const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+            const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
+            const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
+            const float4 e0 = s_e[0][lo], e1 = s_e[1][lo], e2 = s_e[2][lo];
+            if (cell_pass(e0, e1, e2, rx, ry)) {
+                const uint32_t r = ry * bins.regions_x + rx;
+                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u), i0 + s_big[lo]);
+            }
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
-
-    // Reserve the workgroup's range and copy the wave segments out.
-    lost = wn > kWaveStage;
-    if (lane == 0) s_wave[wave] = wn;
+    // the frame's largest region count (list sizing; > cap flags the overflow)
+    if (my_max) atomicMax(&s_max, my_max);
     __syncthreads();
-    uint32_t before = 0, npairs = 0;
-    for (uint32_t w = 0; w < 4; ++w) {
-        before += w < wave ? s_wave[w] : 0u;
-        npairs += s_wave[w];
-    }
-    if (tid == 0) s_base[0] = npairs ? atomicAdd(&bs->pair_count, npairs) : 0u;
-    __syncthreads();
-    const uint32_t base = s_base[0] + before;
-    const uint32_t i0 = blockIdx.x * blockDim.x;
-    const uint32_t keep = wn < kWaveStage ? wn : kWaveStage;
-    for (uint32_t k = lane; k < keep; k += 64u) {
-        const uint32_t v = s_pairs[wave][k];
-        if (base + k < bins.cap) bins.pairs[base + k] = make_uint2(i0 + (v >> 24), v & 0xFFFFFFu);
-    }
-    if (__syncthreads_or(lost)) {
-        // A wave staged more pairs than its segment holds: it repeats its
-        // enumeration and writes the pairs past the segment straight out
-        // (same order, so the same indices).
-        uint32_t wn2 = 0;
-        auto emit2 = [&](bool pass, uint32_t pr) {
-            const unsigned long long m = __ballot(pass);
-            const uint32_t idx = wn2 + (uint32_t)__popcll(m & lt);
-            if (pass && idx >= kWaveStage && base + idx < bins.cap)
-                bins.pairs[base + idx] = make_uint2(i0 + (pr >> 24), pr & 0xFFFFFFu);
-            wn2 += (uint32_t)__popcll(m);
-        };
-        if (lost) {                                // wave-uniform
-            for (uint32_t k = 0; k < kSerialRegions; ++k) {
-                if (!__ballot(k < my_small)) break;
-                bool pass = false;
-                uint32_t pr = 0;
-                if (k < my_small) {
-                    const uint32_t rx = x0 + k % wr, ry = y0 + k / wr;
-                    pass = cell_pass(fp.e0, fp.e1, fp.e2, rx, ry);
-                    pr = (tid << 24) | region_of(rx, ry);
-                }
-                emit2(pass, pr);
-            }
-        }
-        if (nbig) {
-            const uint32_t total_cells = s_cum[nbig - 1u];
-            for (uint32_t c0 = 0; c0 < total_cells; c0 += blockDim.x) {
-                const uint32_t c = c0 + tid;
-                bool pass = false;
-                uint32_t pr = 0;
-                if (c < total_cells) {
-                    uint32_t lo = 0, hi = nbig - 1u;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
-                    }
-                    const uint2 rc = s_rect[lo];
-                    const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
-                    const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
-                    const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
-                    pass = cell_pass(s_e[0][lo], s_e[1][lo], s_e[2][lo], rx, ry);
-                    pr = (s_big[lo] << 24) | region_of(rx, ry);
-                }
-                if (lost) emit2(pass, pr);
-            }
-        }
+    if (tid == 0 && s_max) {
+        atomicMax(&bs->max_count, s_max);
+        if (s_max > bins.cap) atomicOr(&bs->overflow, 1u);
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 4);
-}
-
-// ---------------------------------------------------------------------------
-// k_bin_scan: one workgroup of kScanThreads.  Region r belongs to thread
-// r % kScanThreads (coalesced loads).  Every thread histograms its regions by
-// launch bucket (heaviest first: log2 of the count) into its own LDS column;
-// one exclusive scan of the bucket-major table [bucket][thread] then gives
-// every (bucket, thread) its first launch slot, and one of the pair sums its
-// first list position.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kScanThreads = 1024;
-constexpr uint32_t kBuckets = 8;
-constexpr uint32_t kScanCache = 16;          // regions per thread held in registers
-
-__device__ __forceinline__ uint32_t launch_bucket(uint32_t c)
-{
-    // 0 = heaviest (>= 512 candidates), 1 = 256.., ..., 5 = 16..31,
-    // 6 = 1..15, 7 = empty region
-    if (c == 0u) return kBuckets - 1u;
-    const int b = 9 - (31 - __clz(c));             // 9 - floor(log2 c)
-    return b < 0 ? 0u : (b > 6 ? 6u : (uint32_t)b);
-}
-
-// In-place exclusive scan of tab[kBuckets * kScanThreads]; thread t scans the
-// kBuckets consecutive words from kBuckets * t.  Returns the table total.
-__device__ __forceinline__ uint32_t scan_table(uint32_t* tab, uint32_t* s_wave)
-{
-    uint32_t v[kBuckets];
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kBuckets; ++q) {
-        v[q] = tab[kBuckets * threadIdx.x + q];
-        sum += v[q];
-    }
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(sum, s_wave, total);
-#pragma unroll
-    for (uint32_t q = 0; q < kBuckets; ++q) {
-        tab[kBuckets * threadIdx.x + q] = run;
-        run += v[q];
-    }
-    __syncthreads();
-    return total;
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_bin_scan(BinBuffers bins, const BinState* __restrict__ bs,
-                                                           DevStats* __restrict__ st)
-{
-    __shared__ uint32_t s_reg[kBuckets * kScanThreads];    // [bucket][thread]
-    __shared__ uint32_t s_pair[kBuckets * kScanThreads];
-    __shared__ uint32_t s_wave[kScanThreads / 64];
-    XRT_STAMP(kStampScan + 0);
-    const uint32_t n = bins.regions_x * bins.regions_y;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t G = bs->global_count;
-    const uint32_t pair_total = bs->pair_count;
-    // The first kScanCache regions of this thread stay in registers (all
-    // loads in flight together); images past kScanCache x kScanThreads
-    // regions reload the rest.
-    uint32_t cc[kScanCache];
-#pragma unroll
-    for (uint32_t q = 0; q < kScanCache; ++q) {
-        const uint32_t r = tid + q * kScanThreads;
-        cc[q] = r < n ? bins.counts[(size_t)r * kCounterStride] : 0u;
-    }
-    uint32_t nreg[kBuckets], npair[kBuckets];
-#pragma unroll
-    for (uint32_t b = 0; b < kBuckets; ++b) { nreg[b] = 0u; npair[b] = 0u; }
-    auto tally = [&](uint32_t c) {
-        const uint32_t bk = launch_bucket(c);
-#pragma unroll
-        for (uint32_t b = 0; b < kBuckets; ++b) {
-            nreg[b] += b == bk ? 1u : 0u;
-            npair[b] += b == bk ? c : 0u;
-        }
-    };
-#pragma unroll
-    for (uint32_t q = 0; q < kScanCache; ++q)
-        if (tid + q * kScanThreads < n) tally(cc[q]);
-    for (uint32_t r = tid + kScanCache * kScanThreads; r < n; r += kScanThreads)
-        tally(bins.counts[(size_t)r * kCounterStride]);
-#pragma unroll
-    for (uint32_t b = 0; b < kBuckets; ++b) {
-        s_reg[b * kScanThreads + tid] = nreg[b];
-        s_pair[b * kScanThreads + tid] = npair[b];
-    }
-    __syncthreads();
-    XRT_STAMP(kStampScan + 1);
-    scan_table(s_reg, s_wave);
-    const uint32_t total = scan_table(s_pair, s_wave);
-    XRT_STAMP(kStampScan + 2);
-    // this thread's first slot and list position per bucket
-#pragma unroll
-    for (uint32_t b = 0; b < kBuckets; ++b) {
-        nreg[b] = s_reg[b * kScanThreads + tid];
-        npair[b] = s_pair[b * kScanThreads + tid];
-    }
-    auto place = [&](uint32_t r, uint32_t c) {
-        const uint32_t bk = launch_bucket(c);
-        uint32_t slot = 0, lo = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < kBuckets; ++b) {
-            if (b == bk) {
-                slot = nreg[b];
-                lo = npair[b];
-                nreg[b] += 1u;
-                npair[b] += c;
-            }
-        }
-        bins.slots[slot] = make_uint4(r, lo, c, G);
-        bins.spans[r] = make_uint2(lo, c);
-        bins.cursor[(size_t)r * kCounterStride] = lo;
-    };
-#pragma unroll
-    for (uint32_t q = 0; q < kScanCache; ++q) {
-        const uint32_t r = tid + q * kScanThreads;
-        if (r < n) place(r, cc[q]);
-    }
-    for (uint32_t r = tid + kScanCache * kScanThreads; r < n; r += kScanThreads)
-        place(r, bins.counts[(size_t)r * kCounterStride]);
-    if (tid == 0) {
-        st->bin.pair_count = pair_total;
-        st->bin.global_count = G;
-        st->bin.total = total;
-        st->bin.overflow = (total > bins.cap || pair_total > bins.cap) ? 1u : 0u;
-    }
-    XRT_STAMP(kStampScan + 3);
-}
-
-// k_bin_fill: one thread per pair, grid-stride with block-uniform trip counts;
-// one cursor atomic per run of equal regions across a wave.
-__global__ __launch_bounds__(256) void k_bin_fill(BinBuffers bins, const float4* __restrict__ culls,
-                                                  RenderParams p, const DevStats* __restrict__ st)
-{
-    XRT_STAMP(kStampFill + 2 * blockIdx.x);
-    if (st->bin.overflow) return;                  // kernel-uniform
-    const uint32_t n = st->bin.pair_count;
-    const uint32_t n_regions = bins.regions_x * bins.regions_y;
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        const uint32_t k = base + threadIdx.x;
-        uint2 pr = make_uint2(0u, kEmpty);
-        if (k < n) pr = bins.pairs[k];
-        const bool active = pr.y < n_regions;      // (always, for k < n) never write out of range
-        uint32_t head, len;
-        lane_runs(active, pr.y, head, len);
-        uint32_t at = 0;
-        if (active && head == lane) at = atomicAdd(&bins.cursor[(size_t)pr.y * kCounterStride], len);
-        at = __shfl(at, (int)head) + (lane - head);
-        if (active && at < bins.cap) {
-            // which of the region's 16 tiles (8x8) the relaxed edges pass:
-            // the render's tile test, evaluated once per (region, triangle)
-            const uint32_t T = p.num_triangles;
-            const float4 e0 = culls[(size_t)T + pr.x], e1 = culls[2 * (size_t)T + pr.x],
-                         e2 = culls[3 * (size_t)T + pr.x];
-            const uint32_t rx0 = (pr.y % bins.regions_x) * kRegion;
-            const uint32_t ry0 = p.row_begin + (pr.y / bins.regions_x) * kRegion;
-            uint32_t mask = 0;
-#pragma unroll
-            for (uint32_t t = 0; t < 16u; ++t) {
-                const float xc = (float)(rx0 + (t & 3u) * 8u) + 3.5f;
-                const float yc = (float)(ry0 + (t >> 2) * 8u) + 3.5f;
-                mask |= edges_pass(e0, e1, e2, xc, yc, 3.5f, 3.5f) ? (1u << t) : 0u;
-            }
-            bins.list[at] = make_uint2(pr.x, mask);
-        }
-    }
-    XRT_STAMP(kStampFill + 2 * blockIdx.x + 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1259,18 +984,14 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
 #endif
 }
 
-// fetch(k) returns (triangle, tile mask) of the k-th candidate: bit t of the
-// mask is set when the triangle's relaxed edges pass tile t of the region
-// (evaluated by k_bin_fill); kTestEdges asks the wave to evaluate them itself
-// (global-list and whole-mesh candidates).
-constexpr uint32_t kTestEdges = 0x10000u;
-
+// fetch(k) returns the triangle of the k-th candidate; the wave evaluates its
+// relaxed edges at the tile rectangle, one lane per candidate.
 template <typename Fetch>
 __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Outputs& out,
                                                  const TriRec* __restrict__ recs,
                                                  const float4* __restrict__ culls, uint32_t tx0,
-                                                 uint32_t ty0, uint32_t tile, uint32_t n_cand,
-                                                 Fetch fetch, WaveStats& ws)
+                                                 uint32_t ty0, uint32_t n_cand, Fetch fetch,
+                                                 WaveStats& ws)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = p.num_triangles;
@@ -1292,12 +1013,11 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
     uint32_t tier = 4;                            // wave-uniform insertion tier (XRT_TIERED)
     for (uint32_t base = 0; base < n_cand; base += 64u) {
         const uint32_t k = base + lane;
-        const uint2 cand = k < n_cand ? fetch(k) : make_uint2(0u, 0u);
-        const uint32_t j = cand.x < T ? cand.x : 0u;   // (always) never read out of range
-        bool pass = (cand.y >> tile) & 1u;
-        if (cand.y & kTestEdges)
-            pass = edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
-                              xc, yc, 3.5f, 3.5f);
+        uint32_t j = k < n_cand ? fetch(k) : 0u;
+        j = j < T ? j : 0u;                       // (always) never read out of range
+        const bool pass = k < n_cand &&
+                          edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
+                                     xc, yc, 3.5f, 3.5f);
         unsigned long long m = __ballot(pass);
         if (!m) continue;
         tests += (uint32_t)__popcll(m);
@@ -1376,32 +1096,27 @@ constexpr uint32_t kTileWaves = XRT_TILE_WAVES;   // tile waves per workgroup (d
 // are latency-bound, and occupancy is what hides it.
 __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
-    BinBuffers bins)
+    BinBuffers bins, const BinState* __restrict__ bs)
 {
     const uint64_t t_start = block_start_stamp();
     const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // tile wave of the grid
-    const uint4 slot = bins.slots[g >> 4];
-    const bool overflow = out.stats->bin.overflow != 0u;
-    const uint32_t region = slot.x;
+    const uint32_t region = g >> 4;
     const uint32_t tile = g & 15u;
     const uint32_t tx0 = (region % bins.regions_x) * kRegion + (tile & 3u) * 8u;
     const uint32_t ty0 = p.row_begin + (region / bins.regions_x) * kRegion + (tile >> 2) * 8u;
     WaveStats ws = {};
     uint32_t n_cand = 0;
     if (tx0 < p.width && ty0 < p.row_end) {                     // wave-uniform
-        if (overflow) {   // list capacity exceeded this frame: whole mesh (exact, slower)
+        const uint32_t n_local = bins.counts[(size_t)region * kCounterStride];
+        if (n_local > bins.cap) {   // the region's list overflowed: whole mesh (exact, slower)
             n_cand = p.num_triangles;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, tile, n_cand,
-                             [](uint32_t k) { return make_uint2(k, kTestEdges); }, ws);
+            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand, [](uint32_t k) { return k; }, ws);
         } else {
-            const uint32_t n_local = slot.z;
-            const uint2* __restrict__ local = bins.list + slot.y;
+            const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
             const uint32_t* __restrict__ glob = bins.global_list;
-            n_cand = n_local + slot.w;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, tile, n_cand,
-                             [&](uint32_t k) {
-                                 return k < n_local ? local[k] : make_uint2(glob[k - n_local], kTestEdges);
-                             }, ws);
+            n_cand = n_local + bs->global_count;
+            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand,
+                             [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
         }
     }
     // candidates are counted once per region (by its tile 0)
@@ -1571,7 +1286,7 @@ __global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs,
     __shared__ OverflowLDS s;
     stats_reduce_slice(out.block_stats, n_blocks, out.stats);
     const uint32_t count = out.stats->overflow_count;
-    const bool use_bins = bins.spans && !out.stats->bin.overflow;
+    const uint32_t G = bins.counts ? bs->global_count : 0u;
     for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
         const uint32_t o = out.overflow_list[e];
         const uint32_t row = p.row_begin + o / p.width;
@@ -1580,14 +1295,13 @@ __global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs,
         make_ray(p, row, col, dx, dy, dz);
         uint32_t n_hits = 0;
         float distance;
-        if (use_bins) {
-            const uint32_t region = (o / p.width / kRegion) * bins.regions_x + col / kRegion;
-            const uint2 span = bins.spans[region];
-            const uint32_t n_local = span.y;
-            const uint2* __restrict__ local = bins.list + span.x;
+        const uint32_t region = (o / p.width / kRegion) * bins.regions_x + col / kRegion;
+        const uint32_t n_local = bins.counts ? bins.counts[(size_t)region * kCounterStride] : 0u;
+        if (bins.counts && n_local <= bins.cap) {
+            const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
             const uint32_t* __restrict__ glob = bins.global_list;
-            distance = overflow_distance(s, recs, n_local + out.stats->bin.global_count,
-                                         [&](uint32_t k) { return k < n_local ? local[k].x : glob[k - n_local]; },
+            distance = overflow_distance(s, recs, n_local + G,
+                                         [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; },
                                          dx, dy, dz, n_hits);
         } else {
             distance = overflow_distance(s, recs, p.num_triangles, [](uint32_t k) { return k; }, dx,
@@ -1601,16 +1315,11 @@ __global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs,
         }
         __syncthreads();                      // s is reused by the next ray
     }
-    // Binned frames leave the counts and the control block zero for the next
-    // one (nothing after k_bin_scan reads them).
-    if (bins.counts) {
-        const uint32_t n = bins.regions_x * bins.regions_y;
-        for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
-            bins.counts[(size_t)r * kCounterStride] = 0u;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            BinState z = {};
-            *bs = z;
-        }
+    // Binned frames: the frame's binning state for xrt_read_stats.
+    if (bins.counts && blockIdx.x == 0 && threadIdx.x == 0) {
+        out.stats->bin.max_count = bs->max_count;
+        out.stats->bin.global_count = bs->global_count;
+        out.stats->bin.overflow = bs->overflow;
     }
 }
 

@@ -18,6 +18,49 @@
 
 using namespace XRT_KERNEL_NS;
 
+// Region list capacity: the first frame of a geometry starts here; the sizing
+// read (xrt_context::BinKey) raises it to a power of two above 1.25x the
+// largest region count, up to kMaxRegionCap (past it a region renders from
+// the whole mesh).
+constexpr uint32_t kInitialRegionCap = 256;
+constexpr uint32_t kMaxRegionCap = 1u << 16;
+// Timed regions put render timing events on every kTimingStride-th frame.
+constexpr uint64_t kTimingStride = 4;
+constexpr unsigned kFinishBlocks = XRT_FINISH_BLOCKS;   // k_finish workgroups
+
+inline uint32_t region_cap_for(uint32_t max_count)
+{
+    uint64_t want = (uint64_t)max_count + max_count / 4u + 1u;
+    uint32_t cap = 64;
+    while (cap < want && cap < kMaxRegionCap) cap <<= 1;
+    return cap;
+}
+
+// Everything one frame's preparation writes and its render reads.  Two sets
+// alternate, so frame N+1's preparation (k_prep, binning) runs on the
+// context's prep stream while frame N renders on the caller's stream.
+struct FrameSet {
+    TriRec* recs = nullptr;        // per-render records
+    size_t recs_cap = 0;
+    float4* cull = nullptr;        // per-render cull planes (4 x T float4)
+    size_t cull_cap = 0;
+    DevStats* stats = nullptr;
+
+    // binning (XRT_KERNEL_BINNED)
+    uint32_t* bin_counts = nullptr;    // BinState line | line-padded region counts
+    size_t bin_counts_cap = 0;
+    uint32_t* bin_list = nullptr;      // regions x capacity triangle ids
+    size_t bin_list_cap = 0;
+    uint32_t* global_list = nullptr;
+    size_t global_list_cap = 0;
+    uint32_t* overflow = nullptr;      // rays past the register hit list
+    size_t overflow_cap = 0;
+
+    hipEvent_t ready = nullptr;        // preparation done (prep stream)
+    hipEvent_t done = nullptr;         // render + k_finish done (caller's stream)
+    bool done_valid = false;
+};
+
 struct xrt_context {
     int device = 0;
     std::string error;
@@ -26,32 +69,16 @@ struct xrt_context {
     uint64_t num_tris = 0;
     size_t tris_cap = 0;
 
-    TriRec* d_recs = nullptr;      // per-render records
-    size_t recs_cap = 0;
-    float4* d_cull = nullptr;      // per-render cull planes (4 x T float4)
-    size_t cull_cap = 0;
+    FrameSet sets[2];
+    int next_set = 0;
+    FrameSet* last_set = nullptr;      // set of the last enqueued frame
+    hipStream_t prep_stream = nullptr;
 
-    DevStats* d_stats = nullptr;
-    BlockStats* d_block_stats = nullptr;
+    BlockStats* d_block_stats = nullptr;   // written by the render, read by k_finish (caller's stream)
     size_t block_stats_cap = 0;
     uint32_t last_blocks = 0;          // workgroups of the last render (diagnostics)
-
-    // binning (XRT_KERNEL_BINNED)
-    uint32_t* d_bin_counts = nullptr;   // BinState | counts   (zero between frames)
-    size_t bin_counts_cap = 0;
-    uint32_t* d_bin_aux = nullptr;      // cursor | spans | slots
-    size_t bin_aux_cap = 0;
-    bool bins_clean = false;           // counts + control block are zero
-    uint2* d_bin_pairs = nullptr;       // (triangle, region) pairs
-    size_t bin_pairs_cap = 0;
-    size_t bin_list_want = 0;           // pair/list capacity wanted (grown by sizing)
-    uint2* d_bin_list = nullptr;        // (triangle, tile mask) region lists
-    size_t bin_list_cap = 0;
-    uint32_t* d_global_list = nullptr;
-    size_t global_list_cap = 0;
+    uint32_t bin_region_cap = kInitialRegionCap;   // list capacity per region (grown by sizing)
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
-    uint32_t* d_overflow = nullptr;
-    size_t overflow_cap = 0;
 
     // staging for the host-pointer entry point
     float* d_image = nullptr;
@@ -65,6 +92,7 @@ struct xrt_context {
     bool timing = false;
     std::vector<hipEvent_t> tev;      // pairs: [2i] before, [2i+1] after the main kernel
     size_t tev_used = 0;
+    uint64_t timed_frames = 0;        // frames enqueued since xrt_timing_begin
     hipStream_t last_stream = nullptr;
     bool pending = false;
     int kernel = XRT_KERNEL_AUTO;
@@ -200,23 +228,20 @@ int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, ui
     return XRT_OK;
 }
 
-int launch_prep(xrt_context* ctx, const RenderParams& p, const CullParams& cp, bool culled,
+int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const CullParams& cp, bool culled,
                 const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream)
 {
     const uint64_t T = ctx->num_tris;
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, ctx->d_tris,
-                       (uint32_t)T, p, cp, ctx->d_recs, culled ? ctx->d_cull : nullptr, bins, bin_ctl,
-                       ctx->d_stats);
+                       (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl, fs.stats);
     XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
 
-// Region buffers of a binned frame.  The control block and the counts live in
-// their own allocation and are zero between frames (cleared on allocation and
-// by k_finish; `bins_clean` is false after an enqueue that did not reach
-// k_finish, and the next binned frame clears them first).  Cursors, spans and
-// launch slots are rewritten every frame by k_bin_scan.
-int bin_buffers(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, BinState*& ctl,
+// Region buffers of a binned frame.  The control block and the line-padded
+// counters are cleared on the prep stream in front of every binned k_prep
+// (off the critical path when frames are pipelined).
+int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& bins, BinState*& ctl,
                 hipStream_t stream)
 {
     const uint64_t T = ctx->num_tris;
@@ -224,32 +249,16 @@ int bin_buffers(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, BinState
     int rc;
     // control block padded to a line, then one line-padded counter per region
     const size_t counter_words = kCounterStride + (size_t)kCounterStride * n_regions;
-    if (counter_words > ctx->bin_counts_cap || !ctx->d_bin_counts) {
-        if ((rc = ensure(ctx, ctx->d_bin_counts, ctx->bin_counts_cap, counter_words))) return rc;
-        ctx->bins_clean = false;
-    }
-    // aux words: cursor (kCounterStride/region) | spans (2/region) | slots (4/region)
-    const size_t nr = ((size_t)n_regions + 3) & ~(size_t)3;
-    if ((rc = ensure(ctx, ctx->d_bin_aux, ctx->bin_aux_cap, (kCounterStride + 6) * nr))) return rc;
-    // pair and list capacity: sized by the last frame of this geometry
-    // (xrt_context::BinKey), at least 4 pairs per triangle
-    const size_t want = std::max<size_t>({ctx->bin_list_want, 4 * (size_t)T, (size_t)n_regions, 65536});
-    if ((rc = ensure(ctx, ctx->d_bin_list, ctx->bin_list_cap, want))) return rc;
-    if ((rc = ensure(ctx, ctx->d_bin_pairs, ctx->bin_pairs_cap, ctx->bin_list_cap))) return rc;
-    if ((rc = ensure(ctx, ctx->d_global_list, ctx->global_list_cap, T))) return rc;
-    if (!ctx->bins_clean) {
-        XRT_HIP(ctx, hipMemsetAsync(ctx->d_bin_counts, 0, ctx->bin_counts_cap * sizeof(uint32_t), stream));
-        ctx->bins_clean = true;
-    }
-    ctl = reinterpret_cast<BinState*>(ctx->d_bin_counts);
-    bins.counts = ctx->d_bin_counts + kCounterStride;
-    bins.cursor = ctx->d_bin_aux;
-    bins.spans = reinterpret_cast<uint2*>(ctx->d_bin_aux + kCounterStride * nr);
-    bins.slots = reinterpret_cast<uint4*>(ctx->d_bin_aux + (kCounterStride + 2) * nr);
-    bins.pairs = ctx->d_bin_pairs;
-    bins.list = ctx->d_bin_list;
-    bins.global_list = ctx->d_global_list;
-    bins.cap = (uint32_t)std::min<size_t>(std::min(ctx->bin_list_cap, ctx->bin_pairs_cap), 0xFFFFFFFFu);
+    if ((rc = ensure(ctx, fs.bin_counts, fs.bin_counts_cap, counter_words))) return rc;
+    const uint32_t cap = ctx->bin_region_cap;
+    if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, (size_t)n_regions * cap))) return rc;
+    if ((rc = ensure(ctx, fs.global_list, fs.global_list_cap, T))) return rc;
+    XRT_HIP(ctx, hipMemsetAsync(fs.bin_counts, 0, counter_words * sizeof(uint32_t), stream));
+    ctl = reinterpret_cast<BinState*>(fs.bin_counts);
+    bins.counts = fs.bin_counts + kCounterStride;
+    bins.list = fs.bin_list;
+    bins.global_list = fs.global_list;
+    bins.cap = cap;
     if (ctx->bin_force_cap) bins.cap = (uint32_t)std::min<size_t>(bins.cap, ctx->bin_force_cap);
     return XRT_OK;
 }
@@ -276,9 +285,18 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     const bool culled = kernel != XRT_KERNEL_BRUTE;
     const bool binned = kernel == XRT_KERNEL_BINNED && rows > 0 && T > 0;
 
-    if ((rc = ensure(ctx, ctx->d_recs, ctx->recs_cap, T))) return rc;
-    if (culled && (rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes))) return rc;
-    if ((rc = ensure(ctx, ctx->d_overflow, ctx->overflow_cap, rays))) return rc;
+    // This frame's buffer set; its preparation waits (on the prep stream) for
+    // the render that last used the set, the render waits for the preparation.
+    FrameSet& fs = ctx->sets[ctx->next_set];
+    static const bool serial = [] {          // A/B only: XRT_PIPELINE=0 prepares on the caller's stream
+        const char* e = std::getenv("XRT_PIPELINE");
+        return e && std::atoi(e) == 0;
+    }();
+    hipStream_t ps = serial ? stream : ctx->prep_stream;
+    if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
+    if (culled && (rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
+    if ((rc = ensure(ctx, fs.overflow, fs.overflow_cap, rays))) return rc;
+    if (fs.done_valid && ps != stream) XRT_HIP(ctx, hipStreamWaitEvent(ps, fs.done, 0));
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
     CullParams cp = make_cull_params(*cam);
@@ -286,8 +304,8 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.image = d_image;
     out.lbuffer = d_lbuffer;
     out.image_u8 = d_u8;
-    out.overflow_list = ctx->d_overflow;
-    out.stats = ctx->d_stats;
+    out.overflow_list = fs.overflow;
+    out.stats = fs.stats;
     const uint32_t n_regions = rows ? rx * ry : 0u;
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
               : binned                     ? dim3(16 / kTileWaves * n_regions)   // 16 tile waves per region
@@ -303,19 +321,18 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
-        if ((rc = bin_buffers(ctx, n_regions, bins, bin_ctl, stream))) return rc;
-        ctx->bins_clean = false;             // until this frame's k_finish is enqueued
+        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;
     }
 
     if (T) {   // k_prep clears DevStats for the frame
-        if ((rc = launch_prep(ctx, p, cp, culled, bins, bin_ctl, stream))) return rc;
+        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps))) return rc;
     } else {
-        XRT_HIP(ctx, hipMemsetAsync(ctx->d_stats, 0, sizeof(DevStats), stream));
+        XRT_HIP(ctx, hipMemsetAsync(fs.stats, 0, sizeof(DevStats), ps));
     }
     if (binned && !ctx->bin_force_cap) {
-        // Size the pair/list buffers once per frame geometry (mesh, camera,
-        // strip): a synchronous read of the pair count, and a re-run of
-        // k_prep with larger buffers if this frame's pairs did not fit.
+        // Size the region lists once per frame geometry (mesh, camera,
+        // strip): a synchronous read of the largest region count, and a
+        // re-run of k_prep with larger lists if this frame's did not fit.
         xrt_context::BinKey key = {};
         key.cam = *cam;
         key.row_begin = row_begin;
@@ -324,31 +341,32 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         key.gen = ctx->mesh_gen;
         if (!ctx->bin_key_valid || std::memcmp(&key, &ctx->bin_key, sizeof key) != 0) {
             BinState h = {};
-            XRT_HIP(ctx, hipMemcpyAsync(&h, bin_ctl, sizeof h, hipMemcpyDeviceToHost, stream));
-            XRT_HIP(ctx, hipStreamSynchronize(stream));
+            XRT_HIP(ctx, hipMemcpyAsync(&h, bin_ctl, sizeof h, hipMemcpyDeviceToHost, ps));
+            XRT_HIP(ctx, hipStreamSynchronize(ps));
             ctx->bin_key = key;
             ctx->bin_key_valid = true;
-            if (h.pair_count > bins.cap) {
-                ctx->bin_list_want = (size_t)h.pair_count + h.pair_count / 4 + 1024;
-                if ((rc = bin_buffers(ctx, n_regions, bins, bin_ctl, stream))) return rc;   // clears
-                ctx->bins_clean = false;
-                if ((rc = launch_prep(ctx, p, cp, culled, bins, bin_ctl, stream))) return rc;
+            if (h.max_count > bins.cap && ctx->bin_region_cap < kMaxRegionCap) {
+                ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(h.max_count));
+                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;   // clears
+                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps))) return rc;
             }
         }
     }
-    if (binned) {
-        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(kScanThreads), 0, stream, bins, bin_ctl, ctx->d_stats);
-        XRT_HIP(ctx, hipGetLastError());
-        const unsigned fill_blocks = (unsigned)std::min<uint64_t>(2048, ((uint64_t)bins.cap + 255) / 256);
-        hipLaunchKernelGGL(k_bin_fill, dim3(std::max(1u, fill_blocks)), dim3(256), 0, stream, bins,
-                           (const float4*)ctx->d_cull, p, (const DevStats*)ctx->d_stats);
-        XRT_HIP(ctx, hipGetLastError());
+    if (ps != stream) {
+        XRT_HIP(ctx, hipEventRecord(fs.ready, ps));
+        XRT_HIP(ctx, hipStreamWaitEvent(stream, fs.ready, 0));
     }
 
     // The render kernel's own dispatch carries the timing events
     // (hipExtLaunchKernel): no separate event packets between the kernels.
+    // Inside a timed region (xrt_timing_begin/end) every kTimingStride-th
+    // frame carries them -- each pair costs the frame a few microseconds --
+    // and the mean render duration is taken over those frames.
     hipEvent_t t0 = ctx->ev_begin, t1 = ctx->ev_end;
-    if (ctx->timing) {
+    const bool sampled = ctx->timing && (ctx->timed_frames++ % kTimingStride) == 0;
+    if (ctx->timing && !sampled) {
+        t0 = t1 = nullptr;
+    } else if (ctx->timing) {
         if (ctx->tev_used + 2 > ctx->tev.size()) {
             for (int k = 0; k < 256; ++k) {
                 hipEvent_t e;
@@ -361,27 +379,41 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         ctx->tev_used += 2;
     }
     ctx->last_t0 = ctx->last_t1 = nullptr;
+    static const bool no_events = [] {      // A/B of the event cost only
+        const char* e = std::getenv("XRT_NO_EVENTS");
+        return e && std::atoi(e) != 0;
+    }();
+    if (no_events) t0 = t1 = nullptr;
     if (rows > 0) {
         if (kernel == XRT_KERNEL_BRUTE)
-            hipExtLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, t0, t1, 0, ctx->d_recs, p, out);
+            hipExtLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, t0, t1, 0, fs.recs, p, out);
         else if (kernel == XRT_KERNEL_TILED || !binned)
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
-                                  ctx->d_recs, ctx->d_cull, p, out);
+                                  fs.recs, fs.cull, p, out);
         else
-            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, ctx->d_recs,
-                                  ctx->d_cull, p, out, bins);
+            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
+                                  fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
-        ctx->last_t0 = t0;
-        ctx->last_t1 = t1;
-    } else if (ctx->timing) {
-        ctx->tev_used -= 2;     // nothing launched, nothing to time
+        if (t0) {
+            ctx->last_t0 = t0;
+            ctx->last_t1 = t1;
+        } else if (sampled) {
+            ctx->tev_used -= 2;     // XRT_NO_EVENTS
+        }
+    } else if (sampled) {
+        ctx->tev_used -= 2;         // nothing launched, nothing to time
     }
     if (rows > 0) {
-        hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, stream, ctx->d_recs, p, out, n_blocks,
+        hipLaunchKernelGGL(k_finish, dim3(kFinishBlocks), dim3(256), 0, stream, fs.recs, p, out, n_blocks,
                            bins, bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
     }
-    if (binned) ctx->bins_clean = true;
+    if (ps != stream) {
+        XRT_HIP(ctx, hipEventRecord(fs.done, stream));
+        fs.done_valid = true;
+    }
+    ctx->last_set = &fs;
+    ctx->next_set ^= 1;
     ctx->last_stream = stream;
     ctx->pending = true;
     ctx->last_kernel = kernel;
@@ -416,8 +448,20 @@ int xrt_create(int device, xrt_context** out)
         return fail(nullptr, XRT_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
     xrt_context* ctx = new xrt_context();
     ctx->device = device;
-    if (hipMalloc(&ctx->d_stats, sizeof(DevStats)) != hipSuccess ||
-        hipEventCreate(&ctx->ev_begin) != hipSuccess || hipEventCreate(&ctx->ev_end) != hipSuccess) {
+    // The prep stream gets the highest queue priority: its small workgroups
+    // must find CU slots while the previous frame's render fills the chip.
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+    const char* pp = std::getenv("XRT_PREP_PRIORITY");   // A/B only: "0" = default priority
+    if (pp && std::atoi(pp) == 0) prio_greatest = prio_least;
+    bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess &&
+              hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+    for (FrameSet& fs : ctx->sets)
+        ok = ok && hipMalloc(&fs.stats, sizeof(DevStats)) == hipSuccess &&
+             hipMemset(fs.stats, 0, sizeof(DevStats)) == hipSuccess &&
+             hipEventCreateWithFlags(&fs.ready, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&fs.done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         xrt_destroy(ctx);
         return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
     }
@@ -432,16 +476,19 @@ void xrt_destroy(xrt_context* ctx)
     if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
     (void)hipDeviceSynchronize();
     (void)hipFree(ctx->d_tris);
-    (void)hipFree(ctx->d_recs);
-    (void)hipFree(ctx->d_cull);
-    (void)hipFree(ctx->d_stats);
+    for (FrameSet& fs : ctx->sets) {
+        (void)hipFree(fs.recs);
+        (void)hipFree(fs.cull);
+        (void)hipFree(fs.stats);
+        (void)hipFree(fs.bin_counts);
+        (void)hipFree(fs.bin_list);
+        (void)hipFree(fs.global_list);
+        (void)hipFree(fs.overflow);
+        if (fs.ready) (void)hipEventDestroy(fs.ready);
+        if (fs.done) (void)hipEventDestroy(fs.done);
+    }
+    if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
     (void)hipFree(ctx->d_block_stats);
-    (void)hipFree(ctx->d_bin_counts);
-    (void)hipFree(ctx->d_bin_list);
-    (void)hipFree(ctx->d_bin_pairs);
-    (void)hipFree(ctx->d_bin_aux);
-    (void)hipFree(ctx->d_global_list);
-    (void)hipFree(ctx->d_overflow);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
@@ -462,6 +509,7 @@ int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_trian
     if (num_triangles && !triangles) return fail(ctx, XRT_ERR_ARGUMENT, "triangles is NULL");
     if (num_triangles > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many triangles");
     XRT_HIP(ctx, hipSetDevice(ctx->device));
+    XRT_HIP(ctx, hipDeviceSynchronize());        // frames in flight read the mesh (prep stream)
     int rc = ensure(ctx, ctx->d_tris, ctx->tris_cap, 9 * num_triangles);
     if (rc) return rc;
     if (num_triangles)
@@ -593,7 +641,8 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
         ctx->pending = false;
     }
     DevStats s;
-    XRT_HIP(ctx, hipMemcpy(&s, ctx->d_stats, sizeof s, hipMemcpyDeviceToHost));
+    if (ctx->last_set) XRT_HIP(ctx, hipMemcpy(&s, ctx->last_set->stats, sizeof s, hipMemcpyDeviceToHost));
+    else std::memset(&s, 0, sizeof s);
     float ms = 0.0f;
     if (!ctx->last_t0 || hipEventElapsedTime(&ms, ctx->last_t0, ctx->last_t1) != hipSuccess) ms = 0.0f;
     stats->rays = s.rays;
@@ -607,7 +656,7 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     stats->candidates = s.candidates;
     stats->tile_tests = s.tile_tests;
     if (s.bin.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
-        ctx->bin_list_want = std::max(ctx->bin_list_want, (size_t)s.bin.pair_count + s.bin.pair_count / 4 + 1024);
+        ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(s.bin.max_count));
     return XRT_OK;
 }
 
@@ -616,6 +665,7 @@ int xrt_timing_begin(xrt_context* ctx)
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->timing = true;
     ctx->tev_used = 0;
+    ctx->timed_frames = 0;
     return XRT_OK;
 }
 
@@ -731,20 +781,22 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     XRT_HIP(ctx, hipSetDevice(ctx->device));
     const uint64_t T = ctx->num_tris;
     if (!T) return XRT_OK;
-    if ((rc = ensure(ctx, ctx->d_recs, ctx->recs_cap, T))) return rc;
-    if ((rc = ensure(ctx, ctx->d_cull, ctx->cull_cap, (size_t)T * kCullPlanes))) return rc;
+    XRT_HIP(ctx, hipDeviceSynchronize());        // no frame in flight uses the set
+    FrameSet& fs = ctx->sets[ctx->next_set];
+    if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
+    if ((rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
     RenderParams p = make_params(*camera, 0, camera->height, T, ctx->hit_capacity);
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, ctx->d_recs, ctx->d_cull, nobins, nullptr, nullptr);
+                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
-        XRT_HIP(ctx, hipMemcpy(records, ctx->d_recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));
+        XRT_HIP(ctx, hipMemcpy(records, fs.recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));
     if (footprint) {
         // planes [bbox | e0 | e1 | e2] of T float4 -> per triangle 16 floats
         std::vector<float4> planes((size_t)T * kCullPlanes);
-        XRT_HIP(ctx, hipMemcpy(planes.data(), ctx->d_cull, planes.size() * sizeof(float4),
+        XRT_HIP(ctx, hipMemcpy(planes.data(), fs.cull, planes.size() * sizeof(float4),
                                hipMemcpyDeviceToHost));
         for (uint64_t i = 0; i < T; ++i)
             for (int k = 0; k < kCullPlanes; ++k)

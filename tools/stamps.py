@@ -20,8 +20,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-REC = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("odd", "<u8"), ("ovf", "<u8"), ("hits", "<u8"),
-                ("tile_tests", "<u8"), ("candidates", "<u8"), ("xcc", "<u4"), ("hwid", "<u4")])
+REC = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("hits", "<u4"), ("tile_tests", "<u4"),
+                ("hwid", "<u4"), ("xcc", "<u4")])
 TICK_US = 0.01   # s_memrealtime runs at 100 MHz
 
 
