@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BYTES_PER_TEST = 36            # 9 f32 vertex operands per ray-triangle test
 BYTES_OUT_PER_RAY = 9          # L f32 + image f32 + u8
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2   # CUs x SIMDs x clock / 2 cycles per wave64 VALU op
 
 
 def parse():
@@ -225,13 +226,24 @@ def main():
         workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
                                                          if args.tile_mesh > 1 else "") + f" {W}x{H}"
         traffic = None
+        valu_instr = None
         try:
             with open(args.traffic_json) as f:
                 tr = json.load(f).get(f"{result_kernel}:{workload}")
             if tr:
                 traffic = tr.get("hbm_bytes_per_launch")
+                valu_instr = tr.get("valu_wave_instr_per_launch")
         except (OSError, ValueError):
             pass
+        # The culled render is instruction-bound, not HBM-bound: its VALU issue
+        # rate (PMC instruction count per launch / live mean duration) against
+        # the chip's issue peak (a wave64 VALU op every 2 cycles per SIMD).
+        compute = None
+        if valu_instr and avg_kernel_s > 0:
+            rate = valu_instr / avg_kernel_s
+            compute = {"bound": "valu", "achieved": rate, "peak": VALU_PEAK_WAVE_INSTR_S,
+                       "unit": "wave-instr/s", "frac": rate / VALU_PEAK_WAVE_INSTR_S,
+                       "valu_wave_instr_per_launch": valu_instr}
         result = {
             "metric": "Mrays/s (dragon.ply render, whole job)",
             "value": value,
@@ -267,6 +279,7 @@ def main():
                 "kernel": "k_render_" + {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel],
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "launches": launches,
+                "compute": compute,
             },
             "render_stats": {
                 "hit_rays": stats.hit_rays, "odd_rays": stats.odd_rays, "max_hits": stats.max_hits,

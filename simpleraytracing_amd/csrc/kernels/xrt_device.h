@@ -56,6 +56,9 @@
 #ifndef XRT_FINISH_BLOCKS
 #define XRT_FINISH_BLOCKS 64   // k_finish workgroups (statistics slices, overflow rays)
 #endif
+#ifndef XRT_DEFAULT_ORDER
+#define XRT_DEFAULT_ORDER 1    // binned render launch order: 0 raster, 1 centre first
+#endif
 #ifndef XRT_STAMPS
 #define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
 #endif

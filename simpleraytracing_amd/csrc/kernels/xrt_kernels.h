@@ -720,6 +720,7 @@ struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] cleared before every binned frame
     uint32_t* list;          // [n_regions * cap] triangle ids per region
     uint32_t* global_list;   // [T]
+    const uint32_t* order;   // [n_regions] render launch order (null: raster order)
     uint32_t cap;            // list capacity per region
     uint32_t regions_x, regions_y;
 };
@@ -1100,7 +1101,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 {
     const uint64_t t_start = block_start_stamp();
     const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // tile wave of the grid
-    const uint32_t region = g >> 4;
+    const uint32_t region = bins.order ? bins.order[g >> 4] : g >> 4;
     const uint32_t tile = g & 15u;
     const uint32_t tx0 = (region % bins.regions_x) * kRegion + (tile & 3u) * 8u;
     const uint32_t ty0 = p.row_begin + (region / bins.regions_x) * kRegion + (tile >> 2) * 8u;

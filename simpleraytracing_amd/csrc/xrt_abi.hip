@@ -79,6 +79,9 @@ struct xrt_context {
     uint32_t last_blocks = 0;          // workgroups of the last render (diagnostics)
     uint32_t bin_region_cap = kInitialRegionCap;   // list capacity per region (grown by sizing)
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
+    uint32_t* d_order = nullptr;       // render launch order of the regions (launch_order)
+    size_t order_cap = 0;
+    uint32_t order_rx = 0, order_ry = 0;
 
     // staging for the host-pointer entry point
     float* d_image = nullptr;
@@ -263,6 +266,38 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
     return XRT_OK;
 }
 
+// Render launch order of the regions (XRT_ORDER): 0 raster; 1 centre
+// first (regions by distance of their centre from the image centre), so the
+// dense middle of a centred object does not start last and set the tail.
+// A function of the region grid only, uploaded when the grid changes.
+int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
+{
+    static const int mode = [] {
+        const char* e = std::getenv("XRT_ORDER");
+        return e ? std::atoi(e) : XRT_DEFAULT_ORDER;
+    }();
+    bins.order = nullptr;
+    if (mode == 0) return XRT_OK;
+    if (ctx->order_rx != rx || ctx->order_ry != ry || !ctx->d_order) {
+        const size_t n = (size_t)rx * ry;
+        std::vector<uint32_t> order(n);
+        for (size_t r = 0; r < n; ++r) order[r] = (uint32_t)r;
+        const double cx = 0.5 * (rx - 1), cy = 0.5 * (ry - 1);
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
+            return ax * ax + ay * ay < bx * bx + by * by;
+        });
+        XRT_HIP(ctx, hipDeviceSynchronize());   // the previous order may be in use
+        int rc = ensure(ctx, ctx->d_order, ctx->order_cap, n);
+        if (rc) return rc;
+        XRT_HIP(ctx, hipMemcpy(ctx->d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ctx->order_rx = rx;
+        ctx->order_ry = ry;
+    }
+    bins.order = ctx->d_order;
+    return XRT_OK;
+}
+
 int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
                    float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream)
 {
@@ -322,6 +357,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         bins.regions_x = rx;
         bins.regions_y = ry;
         if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;
+        if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
     }
 
     if (T) {   // k_prep clears DevStats for the frame
@@ -489,6 +525,7 @@ void xrt_destroy(xrt_context* ctx)
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
     (void)hipFree(ctx->d_block_stats);
+    (void)hipFree(ctx->d_order);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
