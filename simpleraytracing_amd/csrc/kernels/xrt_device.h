@@ -35,20 +35,8 @@
 #ifndef XRT_WAVES_PER_EU
 #define XRT_WAVES_PER_EU 0   // >0: occupancy hint for the culled render kernels
 #endif
-#ifndef XRT_EAGER_RAY
-#define XRT_EAGER_RAY 0   // binned tiles: ray directions before the candidate loads return
-#endif
-#ifndef XRT_VREC
-#define XRT_VREC 0        // binned tiles: survivor records by vector loads + v_readlane
-#endif
 #ifndef XRT_TILE_WAVES
 #define XRT_TILE_WAVES 4  // binned render: tile waves per workgroup
-#endif
-#ifndef XRT_PACKED
-#define XRT_PACKED 0      // paired exact tests on v_pk_mul_f32 / v_pk_add_f32 (A/B: slower, spills at 8 waves)
-#endif
-#ifndef XRT_TIERED
-#define XRT_TIERED 0      // binned tiles: hit insertion over 4 / 8 / 16 slots by wave occupancy (A/B: no gain)
 #endif
 #ifndef XRT_PREP_SETPRIO
 #define XRT_PREP_SETPRIO 1   // preparation kernels raise their wave priority (s_setprio 3)
@@ -225,34 +213,6 @@ __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1
     return t;
 }
 
-// Two Ray::intersect tests at once (triangles a and b, same ray): every f32
-// multiply and add of mt_exact on a two-lane vector, which gfx950 issues as
-// one v_pk_mul_f32 / v_pk_add_f32 per pair.  Each lane of a packed op rounds
-// exactly like the scalar op, so t0/h0 and t1/h1 equal two mt_exact calls.
-typedef float xrt_f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void mt_exact2(float dx, float dy, float dz, xrt_f2 e1x, xrt_f2 e1y,
-                                          xrt_f2 e1z, xrt_f2 e2x, xrt_f2 e2y, xrt_f2 e2z,
-                                          xrt_f2 tvx, xrt_f2 tvy, xrt_f2 tvz, xrt_f2 qvx,
-                                          xrt_f2 qvy, xrt_f2 qvz, xrt_f2 tnum, float& t0, bool& h0,
-                                          float& t1, bool& h1)
-{
-    const xrt_f2 DX = {dx, dx}, DY = {dy, dy}, DZ = {dz, dz};
-    const xrt_f2 px = DY * e2z - DZ * e2y;                // Ray.cxx:90
-    const xrt_f2 py = DZ * e2x - DX * e2z;
-    const xrt_f2 pz = DX * e2y - DY * e2x;
-    const xrt_f2 det = (e1x * px + e1y * py) + e1z * pz;  // Ray.cxx:93
-    const xrt_f2 inv = {inv_det_of(det.x), inv_det_of(det.y)};   // Ray.cxx:99
-    const xrt_f2 u = ((tvx * px + tvy * py) + tvz * pz) * inv;   // Ray.cxx:105
-    const xrt_f2 v = ((DX * qvx + DY * qvy) + DZ * qvz) * inv;   // Ray.cxx:115
-    const xrt_f2 t = tnum * inv;                          // Ray.cxx:122
-    const xrt_f2 uv = u + v;
-    t0 = t.x;
-    t1 = t.y;
-    h0 = det.x != 0.0f && !(u.x < 0.0f || u.x > 1.0f) && !(v.x < 0.0f || uv.x > 1.0f) && accept_t(t.x);
-    h1 = det.y != 0.0f && !(u.y < 0.0f || u.y > 1.0f) && !(v.y < 0.0f || uv.y > 1.0f) && accept_t(t.y);
-}
-
 // ---------------------------------------------------------------------------
 // Per-ray sorted hit list in registers (static indices only).  Replaces the
 // per-pixel std::vector + std::sort of main.cxx:666-704.
@@ -292,24 +252,6 @@ struct HitList {
         h[0] = fminf(prev, x);
 #pragma unroll
         for (int k = 1; k < kMaxHits; ++k) {
-            const float cur = h[k];
-            h[k] = __builtin_amdgcn_fmed3f(prev, cur, x);
-            prev = cur;
-        }
-        n += hit ? 1u : 0u;
-    }
-
-    // push_if restricted to the first S slots: exact when every lane holds
-    // fewer than S hits before the push (slots >= S stay +inf).  Callers pick
-    // S wave-uniformly (tiered insertion: most rays hold few hits).
-    template <int S>
-    __device__ __forceinline__ void push_if_first(bool hit, float t)
-    {
-        const float x = hit ? t : __builtin_inff();
-        float prev = h[0];
-        h[0] = fminf(prev, x);
-#pragma unroll
-        for (int k = 1; k < S; ++k) {
             const float cur = h[k];
             h[k] = __builtin_amdgcn_fmed3f(prev, cur, x);
             prev = cur;

@@ -938,61 +938,57 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs, uint32_t j0,
                                                  uint32_t j1, bool two, float dx, float dy,
-                                                 float dz, HitList& hl, uint32_t& tier)
+                                                 float dz, HitList& hl)
 {
     const TriRec a = recs[j0];
     bool h0, h1 = false;
-    float t0, t1 = 0.0f;
-#if XRT_PACKED
-    if (two) {
-        const TriRec b = recs[j1];
-        mt_exact2(dx, dy, dz, xrt_f2{a.e1x, b.e1x}, xrt_f2{a.e1y, b.e1y}, xrt_f2{a.e1z, b.e1z},
-                  xrt_f2{a.e2x, b.e2x}, xrt_f2{a.e2y, b.e2y}, xrt_f2{a.e2z, b.e2z},
-                  xrt_f2{a.tvx, b.tvx}, xrt_f2{a.tvy, b.tvy}, xrt_f2{a.tvz, b.tvz},
-                  xrt_f2{a.qvx, b.qvx}, xrt_f2{a.qvy, b.qvy}, xrt_f2{a.qvz, b.qvz},
-                  xrt_f2{a.tnum, b.tnum}, t0, h0, t1, h1);
-    } else {
-        t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz,
-                      a.qvx, a.qvy, a.qvz, a.tnum, h0);
-    }
-#else
-    t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
-                  a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
+    float t1 = 0.0f;
+    const float t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
+                              a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
     if (two) {
         const TriRec b = recs[j1];
         t1 = mt_exact(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
                       b.qvx, b.qvy, b.qvz, b.tnum, h1);
     }
-#endif
-#if XRT_TIERED
-    // Tiered insertion: the network spans only the slots a lane of this wave
-    // can reach (every lane holds <= tier - 2 hits before the pair).
-    while (tier < (uint32_t)kMaxHits && __ballot(hl.n + 2u > tier)) tier *= 2u;   // wave-uniform
-    if (tier == 4u) {
-        hl.push_if_first<4>(h0, t0);
-        hl.push_if_first<4>(h1, t1);
-    } else if (tier == 8u) {
-        hl.push_if_first<8>(h0, t0);
-        hl.push_if_first<8>(h1, t1);
-    } else {
-        hl.push_if(h0, t0);
-        hl.push_if(h1, t1);
-    }
-#else
-    (void)tier;
     hl.push_if(h0, t0);
     hl.push_if(h1, t1);
-#endif
 }
 
-// fetch(k) returns the triangle of the k-th candidate; the wave evaluates its
-// relaxed edges at the tile rectangle, one lane per candidate.
+// Candidates of one region as seen by one wave: load_cand(base) gives this
+// lane's candidate of the 64 starting at `base` (triangle id, relaxed edges).
+struct Cand {
+    uint32_t j;
+    bool valid;
+    float4 e0, e1, e2;
+};
+
 template <typename Fetch>
-__device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Outputs& out,
-                                                 const TriRec* __restrict__ recs,
-                                                 const float4* __restrict__ culls, uint32_t tx0,
-                                                 uint32_t ty0, uint32_t n_cand, Fetch fetch,
-                                                 WaveStats& ws)
+__device__ __forceinline__ Cand load_cand(const float4* __restrict__ culls, uint32_t T, uint32_t n_cand,
+                                          uint32_t base, Fetch fetch)
+{
+    Cand c;
+    const uint32_t k = base + (threadIdx.x & 63u);
+    c.valid = k < n_cand;
+    const uint32_t j = c.valid ? fetch(k) : 0u;
+    c.j = j < T ? j : 0u;                         // (always) never read out of range
+    c.e0 = culls[(size_t)T + c.j];
+    c.e1 = culls[2 * (size_t)T + c.j];
+    c.e2 = culls[3 * (size_t)T + c.j];
+    return c;
+}
+
+// One 8x8 tile: one lane per candidate evaluates the three relaxed edges at
+// the tile rectangle, a ballot keeps the survivors, and each survivor's
+// record is a wave-uniform scalar load tested exactly for all 64 rays (two at
+// a time).  The rays are generated when the first survivor appears; a tile
+// without survivors stores the miss constants (80, +inf, 255) directly.
+// `first` is the region's first chunk of candidates, already loaded.
+template <typename Fetch>
+__device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs& out,
+                                            const TriRec* __restrict__ recs,
+                                            const float4* __restrict__ culls, uint32_t tx0,
+                                            uint32_t ty0, uint32_t n_cand, const Cand& first,
+                                            Fetch fetch, WaveStats& ws)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = p.num_triangles;
@@ -1000,79 +996,43 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
     const uint32_t row = ty0 + (lane >> 3);
     const bool active = col < p.width && row < p.row_end;
     const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
-    if (p.ablate & kAblateCandidates) n_cand = 0;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     bool have_ray = false;                        // wave-uniform
-#if XRT_EAGER_RAY
-    // The directions are computed while the candidate loads are in flight.
-    if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
-#endif
     HitList hl;
     hl.init();
     uint32_t tests = 0;
-    uint32_t tier = 4;                            // wave-uniform insertion tier (XRT_TIERED)
     for (uint32_t base = 0; base < n_cand; base += 64u) {
-        const uint32_t k = base + lane;
-        uint32_t j = k < n_cand ? fetch(k) : 0u;
-        j = j < T ? j : 0u;                       // (always) never read out of range
-        const bool pass = k < n_cand &&
-                          edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
-                                     xc, yc, 3.5f, 3.5f);
+        Cand c;
+        if (base == 0u) {       // the first chunk's ids were loaded once per wave; edges are cache-hot
+            c = first;
+            c.e0 = culls[(size_t)T + c.j];
+            c.e1 = culls[2 * (size_t)T + c.j];
+            c.e2 = culls[3 * (size_t)T + c.j];
+        } else {
+            c = load_cand(culls, T, n_cand, base, fetch);
+        }
+        const bool pass = c.valid && edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f);
         unsigned long long m = __ballot(pass);
         if (!m) continue;
         tests += (uint32_t)__popcll(m);
         if (!have_ray) {
-#if !XRT_EAGER_RAY
             if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
-#endif
             have_ray = true;
         }
         if (p.ablate & kAblateExact) continue;
-#if XRT_VREC
-        // Every survivor lane loads its own record (all in flight together);
-        // the tests broadcast them with v_readlane.
-        TriRec mine = {};
-        if (pass) mine = recs[j];
         while (m) {
             const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            const bool two = m != 0ull;
-            const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m) : k0;
-            if (two) m &= m - 1ull;
-            auto bc = [&](float v, uint32_t l) {
-                return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
-            };
-            bool h0, h1 = false;
-            const float t0 = mt_exact(dx, dy, dz, bc(mine.e1x, k0), bc(mine.e1y, k0), bc(mine.e1z, k0),
-                                      bc(mine.e2x, k0), bc(mine.e2y, k0), bc(mine.e2z, k0),
-                                      bc(mine.tvx, k0), bc(mine.tvy, k0), bc(mine.tvz, k0),
-                                      bc(mine.qvx, k0), bc(mine.qvy, k0), bc(mine.qvz, k0),
-                                      bc(mine.tnum, k0), h0);
-            float t1 = 0.0f;
-            if (two)
-                t1 = mt_exact(dx, dy, dz, bc(mine.e1x, k1), bc(mine.e1y, k1), bc(mine.e1z, k1),
-                              bc(mine.e2x, k1), bc(mine.e2y, k1), bc(mine.e2z, k1),
-                              bc(mine.tvx, k1), bc(mine.tvy, k1), bc(mine.tvz, k1),
-                              bc(mine.qvx, k1), bc(mine.qvy, k1), bc(mine.qvz, k1),
-                              bc(mine.tnum, k1), h1);
-            hl.push_if(h0, t0);
-            hl.push_if(h1, t1);
-        }
-        continue;
-#endif
-        while (m) {
-            const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1ull;
-            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)k0);
+            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k0);
             uint32_t j1 = j0;
             const bool two = m != 0ull;
             if (two) {
                 const uint32_t k1 = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1ull;
-                j1 = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)k1);
+                j1 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k1);
             }
-            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl, tier);
+            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl);
         }
     }
     ws.tile_tests += tests;
@@ -1089,39 +1049,71 @@ __device__ __forceinline__ void render_tile_wave(const RenderParams& p, const Ou
     if (out.image_u8) out.image_u8[o] = 255u;
 }
 
-constexpr uint32_t kTileWaves = XRT_TILE_WAVES;   // tile waves per workgroup (divides 16)
+constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
 
-// One 8x8 tile per wave, kTileWaves waves per workgroup (regions in
-// the binning scan's launch order); each wave stores its own statistics
-// record, so no wave waits for another.  8 waves per SIMD: the tile waves
-// are latency-bound, and occupancy is what hides it.
+// TPW consecutive tiles of one region row (TPW = 1, 2 or 4), rendered in
+// turn; the region's first 64 candidate ids are loaded once for all of them.
+template <uint32_t TPW, typename Fetch>
+__device__ __forceinline__ void render_tiles_wave(const RenderParams& p, const Outputs& out,
+                                                  const TriRec* __restrict__ recs,
+                                                  const float4* __restrict__ culls, uint32_t rx0,
+                                                  uint32_t ry0, uint32_t tile0, uint32_t n_cand,
+                                                  Fetch fetch, WaveStats& ws)
+{
+    if (p.ablate & kAblateCandidates) n_cand = 0;
+    Cand first;                                   // ids only: the edges are re-read per tile
+    {
+        const uint32_t k = threadIdx.x & 63u;
+        first.valid = k < n_cand;
+        const uint32_t j = first.valid ? fetch(k) : 0u;
+        first.j = j < p.num_triangles ? j : 0u;   // (always) never read out of range
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < TPW; ++t) {
+        const uint32_t tile = tile0 + t;
+        const uint32_t tx0 = rx0 + (tile & 3u) * 8u;
+        const uint32_t ty0 = ry0 + (tile >> 2) * 8u;
+        if (tx0 < p.width && ty0 < p.row_end)      // wave-uniform
+            render_tile(p, out, recs, culls, tx0, ty0, n_cand, first, fetch, ws);
+    }
+}
+
+// Binned render: kTileWaves waves per workgroup, TPW 8x8 tiles of one region
+// row per wave (1 by default, see enqueue_render), regions in
+// the launch order of bins.order; each wave stores its own statistics record,
+// so no wave waits for another.  8 waves per SIMD: the tile waves are
+// latency-bound, and occupancy is what hides it.
+template <uint32_t TPW>
 __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins, const BinState* __restrict__ bs)
 {
+    constexpr uint32_t kWavesPerRegion = 16u / TPW;
     const uint64_t t_start = block_start_stamp();
-    const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // tile wave of the grid
-    const uint32_t region = bins.order ? bins.order[g >> 4] : g >> 4;
-    const uint32_t tile = g & 15u;
-    const uint32_t tx0 = (region % bins.regions_x) * kRegion + (tile & 3u) * 8u;
-    const uint32_t ty0 = p.row_begin + (region / bins.regions_x) * kRegion + (tile >> 2) * 8u;
+    const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // wave of the grid
+    const uint32_t slot = g / kWavesPerRegion;
+    const uint32_t region = bins.order ? bins.order[slot] : slot;
+    const uint32_t tile0 = (g % kWavesPerRegion) * TPW;
+    const uint32_t rx0 = (region % bins.regions_x) * kRegion;
+    const uint32_t ry0 = p.row_begin + (region / bins.regions_x) * kRegion;
     WaveStats ws = {};
     uint32_t n_cand = 0;
-    if (tx0 < p.width && ty0 < p.row_end) {                     // wave-uniform
+    if (rx0 + (tile0 & 3u) * 8u < p.width && ry0 + (tile0 >> 2) * 8u < p.row_end) {   // wave-uniform
         const uint32_t n_local = bins.counts[(size_t)region * kCounterStride];
         if (n_local > bins.cap) {   // the region's list overflowed: whole mesh (exact, slower)
             n_cand = p.num_triangles;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand, [](uint32_t k) { return k; }, ws);
+            render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
+                                   [](uint32_t k) { return k; }, ws);
         } else {
             const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
             const uint32_t* __restrict__ glob = bins.global_list;
             n_cand = n_local + bs->global_count;
-            render_tile_wave(p, out, recs, culls, tx0, ty0, n_cand,
-                             [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
+            render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
+                                   [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
         }
     }
-    // candidates are counted once per region (by its tile 0)
-    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
+    // candidates are counted once per region (by the wave holding tile 0)
+    store_wave_stats(ws, tile0 == 0u ? n_cand : 0u, out.block_stats, g, t_start);
 }
 
 // ---------------------------------------------------------------------------

@@ -342,8 +342,16 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.overflow_list = fs.overflow;
     out.stats = fs.stats;
     const uint32_t n_regions = rows ? rx * ry : 0u;
+    // BINNED: 8x8 tiles per render wave.  One (A/B, whole step: 1 wins at
+    // 1024^2, 2048^2 and the 1M-triangle 8192^2 frame; a row of 4 wins by 10 %
+    // at dragon 4096^2); XRT_TPW=2|4 selects the others.
+    static const int tpw_env = [] {
+        const char* e = std::getenv("XRT_TPW");
+        return e ? std::atoi(e) : 0;
+    }();
+    const uint32_t tiles_per_wave = (tpw_env == 2 || tpw_env == 4) ? (uint32_t)tpw_env : 1u;
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
-              : binned                     ? dim3(16 / kTileWaves * n_regions)   // 16 tile waves per region
+              : binned                     ? dim3(16 / tiles_per_wave / kTileWaves * n_regions)
                                            : dim3(rx, ry);
     // stats records: one per workgroup, one per tile wave for BINNED
     const uint32_t n_blocks = rows ? grid.x * grid.y * (binned ? kTileWaves : 1u) : 0u;
@@ -427,7 +435,9 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
                                   fs.recs, fs.cull, p, out);
         else
-            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
+            hipExtLaunchKernelGGL(tiles_per_wave == 4 ? k_render_binned<4>
+                                  : tiles_per_wave == 2 ? k_render_binned<2> : k_render_binned<1>,
+                                  grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
                                   fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         if (t0) {
