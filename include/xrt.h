@@ -231,6 +231,14 @@ int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint
  */
 int xrt_debug_stamps(xrt_context* ctx, uint64_t* dst, uint64_t n);
 
+/*
+ * Test hook (host code, no device): for each i, the culled render's
+ * division-free reject mt_may_hit(det, a, b, tnum) and the exact remainder of
+ * Ray::intersect from the same numerators (hit with t > 1e-7, and t).
+ */
+void xrt_host_mt_check(const float* det, const float* a, const float* b, const float* tnum, uint64_t n,
+                       uint8_t* may_hit, uint8_t* hit, float* t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,6 +97,8 @@ XRT_SYMBOLS = {
     "xrt_probe_math": (ctypes.c_int, [_CtxP, ctypes.c_int, _fp, _fp, _u64]),
     "xrt_probe_prep": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp]),
     "xrt_host_expf_batch": (None, [_fp, _fp, _u64]),
+    "xrt_host_mt_check": (None, [_fp, _fp, _fp, _fp, _u64, ctypes.POINTER(ctypes.c_uint8),
+                                 ctypes.POINTER(ctypes.c_uint8), _fp]),
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),

@@ -47,6 +47,9 @@
 #ifndef XRT_DEFAULT_ORDER
 #define XRT_DEFAULT_ORDER 1    // binned render launch order: 0 raster, 1 centre first
 #endif
+#ifndef XRT_PRE_REJECT
+#define XRT_PRE_REJECT 0     // culled tests: wave-wide division-free reject before the exact test (A/B: slower, off)
+#endif
 #ifndef XRT_STAMPS
 #define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
 #endif
@@ -146,7 +149,7 @@ __device__ __forceinline__ void make_ray(const RenderParams& p, uint32_t row, ui
 // (relative) of an f32 rounding midpoint, so the f64 rounding cannot move it
 // across one.  Checked on all 2^32 inputs (tools/check_fp_identities.c,
 // tests/test_abi.py); the f32 division sequence is about half the f64 one.
-__device__ __forceinline__ float inv_det_of(float det) { return 1.0f / det; }
+__host__ __device__ __forceinline__ float inv_det_of(float det) { return 1.0f / det; }
 
 // Branch-free Ray::intersect for the culled kernels, whose survivors almost
 // always have a hitting lane (so the early reject would not skip the wave's
@@ -194,23 +197,78 @@ __device__ __forceinline__ bool mt_intersect(float dx, float dy, float dz,
 
 // main.cxx:687: (double)t > 0.0000001.  For f32 t that is t > 0x1.ad7f28p-24f,
 // the largest float not above 1e-7 (all 2^32 inputs: tools/check_fp_identities.c).
-__device__ __forceinline__ bool accept_t(float t) { return t > 0x1.ad7f28p-24f; }
+__host__ __device__ __forceinline__ bool accept_t(float t) { return t > 0x1.ad7f28p-24f; }
+
+// The division-free part of Ray::intersect: det (Ray.cxx:93) and the
+// numerators of u (:105, tvec . pvec) and v (:115, dir . qvec), with the
+// reference's operation order.
+__device__ __forceinline__ void mt_numerators(float dx, float dy, float dz, float e1x, float e1y,
+                                              float e1z, float e2x, float e2y, float e2z,
+                                              float tvx, float tvy, float tvz, float qvx,
+                                              float qvy, float qvz, float& det, float& a, float& b)
+{
+    const float px = dy * e2z - dz * e2y;                 // Ray.cxx:90
+    const float py = dz * e2x - dx * e2z;
+    const float pz = dx * e2y - dy * e2x;
+    det = (e1x * px + e1y * py) + e1z * pz;               // Ray.cxx:93
+    a = (tvx * px + tvy * py) + tvz * pz;                 // Ray.cxx:105 (u * det)
+    b = (dx * qvx + dy * qvy) + dz * qvz;                 // Ray.cxx:115 (v * det)
+}
+
+// False only when the reference provably rejects (no division needed): with
+// D = |det| and A, B, T the numerators of u, v, t carrying det's sign,
+//   det == +-0                        Ray.cxx:94
+//   A < -2^-20 D or A > (1+2^-20) D   u < 0 or u > 1   (mt_intersect's bounds)
+//   B < -2^-20 D                      v < 0            (same argument as for u)
+//   A + B > (1+2^-18) D, D normal     u + v > 1: u and v each lose at most 2 ulps
+//                                     to their two roundings, the f32 sum one (for
+//                                     denormal det, 1/det may overflow and u = 0 * inf
+//                                     is NaN, which the reference lets through)
+//   T <= 0                            t <= 0 (t = tnum * RN(1/det), same sign)
+// NaNs fail every compare and are kept.  Used wave-wide: a triangle that
+// every lane rejects skips the division and the hit-list insertion.
+__host__ __device__ __forceinline__ float xrt_flip_sign(float x, uint32_t sgn)
+{
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    u ^= sgn;
+    __builtin_memcpy(&x, &u, 4);
+    return x;
+}
+
+__host__ __device__ __forceinline__ bool mt_may_hit(float det, float a, float b, float tnum)
+{
+    uint32_t bits;
+    __builtin_memcpy(&bits, &det, 4);
+    const uint32_t sgn = bits & 0x80000000u;
+    const float D = fabsf(det);
+    const float A = xrt_flip_sign(a, sgn);
+    const float B = xrt_flip_sign(b, sgn);
+    const float T = xrt_flip_sign(tnum, sgn);
+    const float lo = D * -0x1p-20f;
+    return !(det == 0.0f || A < lo || A > D * 0x1.00001p0f || B < lo ||
+             (D >= 0x1p-126f && A + B > D * 0x1.00004p0f) || T <= 0.0f);
+}
+
+// The rest of Ray::intersect from mt_numerators' values; `hit` includes accept_t.
+__host__ __device__ __forceinline__ float mt_finish(float det, float a, float b, float tnum, bool& hit)
+{
+    const float inv_det = inv_det_of(det);                // Ray.cxx:99
+    const float u = a * inv_det;                          // Ray.cxx:105
+    const float v = b * inv_det;                          // Ray.cxx:115
+    const float t = tnum * inv_det;                       // Ray.cxx:122
+    hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
+    return t;
+}
 
 __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1x, float e1y,
                                          float e1z, float e2x, float e2y, float e2z, float tvx,
                                          float tvy, float tvz, float qvx, float qvy, float qvz,
                                          float tnum, bool& hit)
 {
-    const float px = dy * e2z - dz * e2y;                 // Ray.cxx:90
-    const float py = dz * e2x - dx * e2z;
-    const float pz = dx * e2y - dy * e2x;
-    const float det = (e1x * px + e1y * py) + e1z * pz;   // Ray.cxx:93
-    const float inv_det = inv_det_of(det);                // Ray.cxx:99
-    const float u = ((tvx * px + tvy * py) + tvz * pz) * inv_det;    // Ray.cxx:105
-    const float v = ((dx * qvx + dy * qvy) + dz * qvz) * inv_det;    // Ray.cxx:115
-    const float t = tnum * inv_det;                       // Ray.cxx:122
-    hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
-    return t;
+    float det, a, b;
+    mt_numerators(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tvx, tvy, tvz, qvx, qvy, qvz, det, a, b);
+    return mt_finish(det, a, b, tnum, hit);
 }
 
 // ---------------------------------------------------------------------------

@@ -941,6 +941,34 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
                                                  float dz, HitList& hl)
 {
     const TriRec a = recs[j0];
+#if XRT_PRE_REJECT
+    // Division-free numerators first; a triangle every lane provably rejects
+    // (mt_may_hit) skips the division and the hit-list insertion.
+    float det0, a0, b0, det1 = 0.0f, a1 = 0.0f, b1 = 0.0f, tn1 = 0.0f;
+    mt_numerators(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz, a.qvx,
+                  a.qvy, a.qvz, det0, a0, b0);
+    if (two) {
+        const TriRec b = recs[j1];
+        mt_numerators(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
+                      b.qvx, b.qvy, b.qvz, det1, a1, b1);
+        tn1 = b.tnum;
+    }
+    const bool live0 = __ballot(mt_may_hit(det0, a0, b0, a.tnum)) != 0ull;          // wave-uniform
+    const bool live1 = two && __ballot(mt_may_hit(det1, a1, b1, tn1)) != 0ull;
+    bool h0, h1;
+    if (live0 && live1) {
+        const float t0 = mt_finish(det0, a0, b0, a.tnum, h0);
+        const float t1 = mt_finish(det1, a1, b1, tn1, h1);
+        hl.push_if(h0, t0);
+        hl.push_if(h1, t1);
+    } else if (live0) {
+        const float t0 = mt_finish(det0, a0, b0, a.tnum, h0);
+        hl.push_if(h0, t0);
+    } else if (live1) {
+        const float t1 = mt_finish(det1, a1, b1, tn1, h1);
+        hl.push_if(h1, t1);
+    }
+#else
     bool h0, h1 = false;
     float t1 = 0.0f;
     const float t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
@@ -952,6 +980,7 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
     }
     hl.push_if(h0, t0);
     hl.push_if(h1, t1);
+#endif
 }
 
 // Candidates of one region as seen by one wave: load_cand(base) gives this

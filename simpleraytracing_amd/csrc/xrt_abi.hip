@@ -854,6 +854,20 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
 
 // Host evaluation of the device expf restatement (same source, host-compiled);
 // lets the CPU test suite check it exhaustively against libm without a GPU.
+// Host evaluation of the culled tests' division-free reject (mt_may_hit) and
+// of the exact remainder (mt_finish), same source: the CPU suite checks that
+// the reject never drops a hit.
+void xrt_host_mt_check(const float* det, const float* a, const float* b, const float* tnum, uint64_t n,
+                       uint8_t* may_hit, uint8_t* hit, float* t)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        bool h = false;
+        t[i] = mt_finish(det[i], a[i], b[i], tnum[i], h);
+        hit[i] = h ? 1 : 0;
+        may_hit[i] = mt_may_hit(det[i], a[i], b[i], tnum[i]) ? 1 : 0;
+    }
+}
+
 void xrt_host_expf_batch(const float* in, float* outp, uint64_t n)
 {
     for (uint64_t i = 0; i < n; ++i) outp[i] = xrt_expf(in[i]);

@@ -1,6 +1,7 @@
 """CPU: the C-ABI libraries load, export every declared symbol, and their
 host-side arithmetic (bbox, camera, PLY ingestion, expf restatement) is
 bit-identical to the oracle.  No compute call touches a GPU here."""
+import ctypes
 import os
 import re
 import subprocess
@@ -113,6 +114,50 @@ def test_host_expf_restatement_matches_libm():
     want = oracle.expf(x)
     same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
     assert same.all(), x[~same][:10]
+
+
+def _mt_inputs(n, seed):
+    """(det, a, b, tnum) near every decision boundary of Ray::intersect:
+    u, v, u + v at 0 and 1 within a few ulps, t near 1e-7, det from denormal
+    to huge, signs flipped, zeros, infinities and NaNs."""
+    rng = np.random.default_rng(seed)
+    f32 = np.float32
+    det = (rng.choice([-1, 1], n) * 2.0 ** rng.uniform(-149, 127, n)).astype(f32)
+    det[rng.random(n) < 0.02] = f32(0.0)
+    det[rng.random(n) < 0.01] = f32(-0.0)
+    u = rng.choice([0.0, 1.0, 0.5, 1e-7, -1e-7, 0.999999, 1.000001], n) + rng.normal(0, 1e-7, n)
+    v = rng.choice([0.0, 0.5, 1e-7, -1e-7], n) + rng.normal(0, 1e-7, n)
+    v = np.where(rng.random(n) < 0.5, 1.0 - u + rng.normal(0, 1e-7, n), v)
+    t = rng.choice([1e-7, 1.0, -1.0, 0.0, 1e-30, 1e30], n) * (1 + rng.normal(0, 1e-6, n))
+    a = (det.astype(np.float64) * u).astype(f32)
+    b = (det.astype(np.float64) * v).astype(f32)
+    tn = (det.astype(np.float64) * t).astype(f32)
+    # a few ulps around each numerator
+    for arr in (a, b, tn):
+        arr.view(np.int32)[:] += rng.integers(-4, 5, n).astype(np.int32) * (arr != 0)
+    specials = np.array([np.inf, -np.inf, np.nan, 0.0, -0.0, 1e-45, -1e-45, 3.4e38], f32)
+    for arr in (det, a, b, tn):
+        m = rng.random(n) < 0.003
+        arr[m] = rng.choice(specials, int(m.sum()))
+    return det, a, b, tn
+
+
+def test_host_pre_reject_never_drops_a_hit():
+    """The culled render's division-free reject (mt_may_hit, host-compiled from
+    the device source) may only reject inputs that Ray::intersect rejects."""
+    lib = _abi.load()
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    for seed in range(4):
+        det, a, b, tn = _mt_inputs(1 << 20, seed)
+        may = np.empty(det.size, np.uint8)
+        hit = np.empty(det.size, np.uint8)
+        t = np.empty(det.size, np.float32)
+        lib.xrt_host_mt_check(det.ctypes.data_as(_abi._fp), a.ctypes.data_as(_abi._fp),
+                              b.ctypes.data_as(_abi._fp), tn.ctypes.data_as(_abi._fp), det.size,
+                              may.ctypes.data_as(u8p), hit.ctypes.data_as(u8p), t.ctypes.data_as(_abi._fp))
+        bad = (hit == 1) & (may == 0)
+        assert not bad.any(), list(zip(det[bad][:5], a[bad][:5], b[bad][:5], tn[bad][:5]))
+        assert hit.sum() > 1000 and (may == 0).sum() > det.size // 4     # both sides exercised
 
 
 def test_cli_help_and_bad_option():
