@@ -349,6 +349,43 @@ def test_device_buffers_and_timing(ctx, dragon):
     assert st.rays == W * H
 
 
+def test_pipelined_frames_without_sync(ctx, dragon):
+    """Many frames enqueued back to back on one stream with no host sync --
+    different cameras, image sizes, strips, kernels and output buffers, so the
+    two alternating buffer sets and the prep stream are exercised under
+    overlap -- each equal to its own synchronous render."""
+    import torch
+    dev = torch.device("cuda", ctx.device)
+    stream = torch.cuda.Stream(device=dev)
+    ctx.upload_mesh(dragon)
+    jobs = [(256, 256, 0, 256, xrt.XRT_KERNEL_BINNED), (200, 120, 0, 120, xrt.XRT_KERNEL_BINNED),
+            (256, 256, 64, 200, xrt.XRT_KERNEL_BINNED), (160, 160, 0, 160, xrt.XRT_KERNEL_TILED),
+            (300, 300, 0, 300, xrt.XRT_KERNEL_BINNED), (256, 256, 0, 256, xrt.XRT_KERNEL_AUTO),
+            (96, 320, 10, 300, xrt.XRT_KERNEL_BINNED), (256, 256, 0, 256, xrt.XRT_KERNEL_BINNED)] * 2
+    cams = {}
+    for W, H, *_ in jobs:                  # first frame of each geometry sizes its lists (sync)
+        cams[(W, H)] = xrt.camera_for_mesh(dragon, W, H)
+    refs = []
+    for W, H, r0, r1, k in jobs:
+        ctx.set_kernel(k)
+        refs.append(ctx.render_rows(cams[(W, H)], r0, r1))
+    outs = []
+    with torch.cuda.stream(stream):
+        for W, H, r0, r1, k in jobs:
+            n = (r1 - r0) * W
+            bufs = (torch.full((n,), -1.0, device=dev), torch.full((n,), -1.0, device=dev),
+                    torch.zeros(n, dtype=torch.uint8, device=dev))
+            ctx.set_kernel(k)
+            ctx.render_rows_device(cams[(W, H)], r0, r1, bufs[0].data_ptr(), bufs[1].data_ptr(),
+                                   bufs[2].data_ptr(), stream.cuda_stream)
+            outs.append(bufs)
+    stream.synchronize()
+    for (img, lb, u8), ref, job in zip(outs, refs, jobs):
+        assert np.array_equal(bits(img.cpu().numpy()), bits(ref[0])), job
+        assert np.array_equal(bits(lb.cpu().numpy()), bits(ref[1])), job
+        assert np.array_equal(u8.cpu().numpy(), ref[2]), job
+
+
 def test_cli_golden_text(tmp_path):
     """xrt_main (the reference's CLI over the GPU path) writes the golden text."""
     exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
