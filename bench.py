@@ -4,7 +4,7 @@
 A step renders frames of the configured size (default dragon.ply, 2048x2048,
 every ray tested against the mesh, outputs f32 image + f32 L-buffer + u8
 image).  The mesh is resident in HBM before the timed region; the per-frame
-triangle preparation, the render kernel and its fix-up kernel are inside it.
+triangle preparation (binning) and the render kernel are inside it.
 
   --mode frames  (default) weak scaling: every rank renders one whole frame per
                  step on its own GPU; no collective in the timed loop (the path
@@ -43,8 +43,8 @@ VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2   # CUs x SIMDs x clock / 2 cycles 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, nargs=2, default=[2048, 2048], metavar=("W", "H"))
     ap.add_argument("--kernel", choices=["auto", "binned", "tiled", "brute"], default="auto")
     ap.add_argument("--mode", choices=["frames", "strips"], default="frames")

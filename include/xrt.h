@@ -148,8 +148,13 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
 
 /*
  * Same with DEVICE buffers on HIP stream `stream` (hipStream_t, NULL = default
- * stream).  Asynchronous: returns after enqueueing.  Call xrt_read_stats()
- * (which synchronises the stream) for counters and kernel time.
+ * stream).  Asynchronous with respect to the render: returns once the render
+ * is enqueued.  The frame's preparation (k_prep, on the context's own prep
+ * stream, overlapping earlier renders) has completed by then -- the call waits
+ * for it, typically tens of microseconds -- and when four frames are already
+ * in flight the call first waits for the oldest of them.  Call
+ * xrt_read_stats() (which synchronises the stream) for counters and kernel
+ * time.
  */
 int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
                            uint32_t row_end, float* d_image, float* d_lbuffer,

@@ -41,9 +41,6 @@
 #ifndef XRT_PREP_SETPRIO
 #define XRT_PREP_SETPRIO 1   // preparation kernels raise their wave priority (s_setprio 3)
 #endif
-#ifndef XRT_FINISH_BLOCKS
-#define XRT_FINISH_BLOCKS 64   // k_finish workgroups (statistics slices, overflow rays)
-#endif
 #ifndef XRT_DEFAULT_ORDER
 #define XRT_DEFAULT_ORDER 1    // binned render launch order: 0 raster, 1 centre first
 #endif

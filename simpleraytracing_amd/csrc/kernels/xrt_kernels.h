@@ -15,8 +15,8 @@
 //                    edge functions, a wave ballot keeps the survivors, and
 //                    every survivor runs the exact Moller-Trumbore test for all
 //                    64 rays.  Output is bit-identical to k_render_brute.
-//   k_overflow       exact fix-up for rays whose register hit list overflowed:
-//                    streams the sorted hit sequence by repeated minimum scans.
+//   Rays whose register hit list overflows are recomputed exactly by their
+//   own wave before the tile's stores (wave_overflow_distance).
 //   k_probe_*        device probes of the exact device code paths (tests).
 #pragma once
 
@@ -25,27 +25,13 @@
 
 namespace XRT_KERNEL_NS {
 
-// Binning control block.  Zero on entry to a binned frame: it is cleared when
-// allocated and by every binned frame's k_finish for the next one.
-// Cleared with the region counters before every binned frame's k_prep.
+// Binning control block, cleared with the region counters before every binned
+// frame's k_prep; read back by xrt_read_stats (list sizing).
 struct BinState {
     unsigned int max_count;     // largest region count of the frame (list sizing)
     unsigned int global_count;  // triangles in the global list
     unsigned int overflow;      // some region count exceeded the list capacity
     unsigned int pad;
-};
-
-struct DevStats {
-    unsigned long long rays;
-    unsigned long long hit_rays;
-    unsigned long long odd_rays;
-    unsigned long long overflow_rays;
-    unsigned long long hits;
-    unsigned int max_hits;
-    unsigned int overflow_count;   // entries in the overflow list
-    unsigned long long candidates; // TILED: region candidates (phase 1), summed
-    unsigned long long tile_tests; // wave-level triangle tests (64 rays each)
-    BinState bin;
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -55,9 +41,10 @@ struct CullParams {
     double width, height;
 };
 
-// Per-workgroup statistics, written with plain stores (one record per block)
-// and summed by k_stats_reduce: same-address global atomics from every wave
-// serialise in L2 and dominated short renders.
+// Per-workgroup (BINNED: per-wave) statistics, written with plain stores, one
+// record each, and summed on the host by xrt_read_stats: same-address global
+// atomics from every wave serialise in L2, and a reduction kernel would sit
+// on every frame's critical path.
 // 32 bytes; XRT_STAMPS builds store the start/end s_memrealtime in the first
 // four words (two u64), the HW_ID in `candidates` and the XCC id in `max_hits`.
 struct BlockStats {
@@ -69,9 +56,7 @@ struct Outputs {
     float* image;
     float* lbuffer;
     uint8_t* image_u8;
-    uint32_t* overflow_list;   // capacity = strip rays
-    DevStats* stats;
-    BlockStats* block_stats;   // one per workgroup of the render grid
+    BlockStats* block_stats;   // one per workgroup (BINNED: per wave) of the render grid
 };
 
 // Running counters of one wave: ballot counts (wave-uniform), per-lane hit sum
@@ -102,9 +87,8 @@ __device__ __forceinline__ double l1_d(const double a[3])
 }
 
 // ---------------------------------------------------------------------------
-// Per-ray epilogue shared by the render kernels: L-buffer, shade, LUT, stores,
-// statistics.  Returns true if the ray overflowed (its outputs are then written
-// by k_overflow).
+// Per-ray epilogue shared by the render kernels: statistics, the exact fix-up
+// of overflowed rays, L-buffer, shade, LUT, stores.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t n, bool odd,
                                            bool overflow)
@@ -233,20 +217,153 @@ __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Exact distance of a ray whose hit count exceeded the register list
+// (n > capacity), computed by the whole wave: lane k tests candidates k,
+// k + 64, ... and keeps its accepted distances in a sorted register list of
+// kFixupSlots; the 64 x kFixupSlots lists are bitonic-sorted across the wave
+// (element e = slot * 64 + lane) and the pairs summed in ascending order,
+// sequentially, as main.cxx:703-708 does.  A ray with more hits than one lane
+// can hold streams its sorted sequence instead: repeated wave-wide scans for
+// the next larger distance and its multiplicity.  The candidates are the
+// ones the render tested before its tile cull (the cull is conservative, so
+// the hit set is the same).  Ray and result are wave-uniform; rare path.
+// ---------------------------------------------------------------------------
+constexpr int kFixupSlots = 8;
+
+__device__ __forceinline__ bool fixup_hit(const TriRec* __restrict__ recs, uint32_t j, float dx,
+                                          float dy, float dz, float& t)
+{
+    const TriRec r = recs[j];
+    return mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx, r.tvy, r.tvz,
+                        r.qvx, r.qvy, r.qvz, r.tnum, t) &&
+           accept_t(t);
+}
+
+// Compare-exchange of the slot pairs (r, r | S) (element distance 64 S) of
+// one bitonic stage; ascending where (r & size_slots) == 0.
+template <uint32_t S>
+__device__ __forceinline__ void bitonic_slots(float (&v)[kFixupSlots], uint32_t size_slots)
+{
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kFixupSlots; ++r) {
+        if (r & S) continue;
+        const float a = v[r], b = v[r | S];
+        const bool asc = (r & size_slots) == 0u;
+        v[r] = asc ? fminf(a, b) : fmaxf(a, b);
+        v[r | S] = asc ? fmaxf(a, b) : fminf(a, b);
+    }
+}
+
+template <typename Fetch>
+__device__ float wave_overflow_distance(const TriRec* __restrict__ recs, uint32_t n_cand, Fetch fetch,
+                                        float dx, float dy, float dz)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    float v[kFixupSlots];
+#pragma unroll
+    for (int r = 0; r < kFixupSlots; ++r) v[r] = __builtin_inff();
+    uint32_t cnt = 0;
+    for (uint32_t base = 0; base < n_cand; base += 64u) {
+        const uint32_t k = base + lane;
+        float t = 0.0f;
+        const bool hit = k < n_cand && fixup_hit(recs, fetch(k), dx, dy, dz, t);
+        if (hit) {                                    // sorted insert (drops the largest past 8)
+            float prev = v[0];
+            v[0] = fminf(prev, t);
+#pragma unroll
+            for (int r = 1; r < kFixupSlots; ++r) {
+                const float cur = v[r];
+                v[r] = __builtin_amdgcn_fmed3f(prev, cur, t);
+                prev = cur;
+            }
+            ++cnt;
+        }
+    }
+    uint32_t total = cnt, most = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        total += __shfl_xor(total, off);
+        const uint32_t o = __shfl_xor(most, off);
+        most = most > o ? most : o;
+    }
+    total = (uint32_t)__builtin_amdgcn_readfirstlane((int)total);   // uniform: the loops below
+    most = (uint32_t)__builtin_amdgcn_readfirstlane((int)most);     // index lanes with it
+    if (total & 1u) return 0.0f;                      // odd count: main.cxx:709-713
+    float distance = 0.0f;
+    if (most <= (uint32_t)kFixupSlots) {
+        constexpr uint32_t N = 64u * kFixupSlots;
+        for (uint32_t size = 2; size <= N; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                if (stride >= 64u) {
+                    const uint32_t ss = size >> 6;
+                    if (stride == 64u) bitonic_slots<1>(v, ss);
+                    else if (stride == 128u) bitonic_slots<2>(v, ss);
+                    else bitonic_slots<4>(v, ss);
+                } else {
+                    const bool lower = (lane & stride) == 0u;
+#pragma unroll
+                    for (uint32_t r = 0; r < (uint32_t)kFixupSlots; ++r) {
+                        const float o = __shfl_xor(v[r], (int)stride);
+                        const bool asc = size < 64u ? (lane & size) == 0u : (r & (size >> 6)) == 0u;
+                        v[r] = (lower == asc) ? fminf(v[r], o) : fmaxf(v[r], o);
+                    }
+                }
+            }
+        }
+        // pair differences on the even lanes, then the sequential f32 sum
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kFixupSlots; ++r) {
+            const float d = __shfl_xor(v[r], 1) - v[r];
+            for (uint32_t l = 0; l < 64u && r * 64u + l + 1u < total; l += 2u)
+                distance += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), (int)l));
+        }
+        return distance;
+    }
+    // Streamed: the sorted sequence by repeated scans (value, multiplicity).
+    uint32_t pos = 0;
+    float prev = -__builtin_inff(), pending = 0.0f;
+    while (pos < total) {
+        float cur = __builtin_inff();
+        uint32_t mult = 0;
+        for (uint32_t base = 0; base < n_cand; base += 64u) {
+            const uint32_t k = base + lane;
+            float t = 0.0f;
+            if (k < n_cand && fixup_hit(recs, fetch(k), dx, dy, dz, t) && t > prev) {
+                if (t < cur) { cur = t; mult = 1; }
+                else if (t == cur) ++mult;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float oc = __shfl_xor(cur, off);
+            const uint32_t om = __shfl_xor(mult, off);
+            if (oc < cur) { cur = oc; mult = om; }
+            else if (oc == cur) mult += om;
+        }
+        if (mult == 0) break;                         // cannot happen; keeps the loop bounded
+        for (uint32_t q = 0; q < mult && pos < total; ++q, ++pos) {
+            if ((pos & 1u) == 0) pending = cur;
+            else distance += cur - pending;
+        }
+        prev = cur;
+    }
+    return distance;
+}
+
+// Must be reached by the whole wave (the overflow fix-up is wave-wide).
+// (dx, dy, dz) is this lane's ray; n_cand / fetch the candidates the render
+// tested (fetch(k) = triangle of the k-th).
+template <typename Fetch>
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
                                            uint32_t row, uint32_t col, const HitList& hl,
-                                           WaveStats& ws)
+                                           WaveStats& ws, const TriRec* __restrict__ recs, float dx,
+                                           float dy, float dz, uint32_t n_cand, Fetch fetch)
 {
+    const uint32_t lane = threadIdx.x & 63u;
     bool overflow = hl.n > p.hit_capacity;
     bool odd = (hl.n & 1u) != 0u;
     wave_stats(ws, active, hl.n, odd, overflow);
-    if (!active) return;
-    size_t o = (size_t)(row - p.row_begin) * p.width + col;
-    if (overflow) {
-        uint32_t slot = atomicAdd(&out.stats->overflow_count, 1u);
-        out.overflow_list[slot] = (uint32_t)o;
-        return;
-    }
     // main.cxx:700-718
     float distance = 0.0f;
     float lval = __builtin_inff();
@@ -254,6 +371,21 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         if (!odd) distance = hl.path_length();
         lval = distance;
     }
+    unsigned long long om = __ballot(active && overflow);
+    while (om) {                                      // wave-uniform
+        const uint32_t L = (uint32_t)__builtin_ctzll(om);
+        om &= om - 1ull;
+        const float rx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), (int)L));
+        const float ry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), (int)L));
+        const float rz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), (int)L));
+        const float d = wave_overflow_distance(recs, n_cand, fetch, rx, ry, rz);
+        if (lane == L) {                              // n > capacity >= 1: the ray hit
+            distance = d;
+            lval = d;
+        }
+    }
+    if (!active) return;
+    size_t o = (size_t)(row - p.row_begin) * p.width + col;
     if (p.ablate & (kAblateStores | kAblateShade)) {
         if (!(p.ablate & kAblateStores)) {
             if (out.image) out.image[o] = distance;
@@ -307,7 +439,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
     WaveStats ws = {};
     ws.tile_tests = T;
-    finish_ray(p, out, active, row, col, hl, ws);
+    finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, T, [](uint32_t k) { return k; });
     store_block_stats(ws, 0u, out.block_stats);
 }
 
@@ -464,7 +596,7 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         }
         if (tile_live) {
             ws.tile_tests += tests;
-            finish_ray(p, out, active, row, col, hl, ws);
+            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
         }
     }
 }
@@ -715,6 +847,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
 constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
+constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back count atomics
 
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] cleared before every binned frame
@@ -770,13 +903,12 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 // ---------------------------------------------------------------------------
 // k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
 // terms), cull planes and (binned) the triangle's region list entries.
-// Thread 0 also clears DevStats for the frame.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, uint32_t T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
-                                              BinState* __restrict__ bs, DevStats* __restrict__ st)
+                                              BinState* __restrict__ bs)
 {
     // The preparation of frame N+1 shares the CUs with frame N's render (prep
     // stream): top wave priority keeps this latency-bound chain short.
@@ -784,10 +916,6 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
-    if (i == 0 && st) {
-        DevStats z = {};
-        *st = z;
-    }
     Footprint fp;
     if (valid) {
         const float* P = tris + 9ull * i;
@@ -844,25 +972,29 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ tris, ui
         return edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f);
     };
 
-    // Small rectangles, lane-serial: the passing regions first, then all of
-    // their count atomics back to back, then the entries.
+    // Small rectangles, lane-serial, in batches of kSerialBatch cells: the
+    // passing regions first, then their count atomics back to back, then the
+    // entries.  (Batches keep k_prep within 64 VGPRs, so its waves fit the
+    // holes a retiring render wave leaves while the previous frame renders.)
     if (has && !big) {
-        uint32_t reg[kSerialRegions], slot[kSerialRegions];
         uint32_t cx = x0, cy = y0;
+        for (uint32_t k0 = 0; k0 < cells; k0 += kSerialBatch) {
+            uint32_t reg[kSerialBatch], slot[kSerialBatch];
 #pragma unroll
-        for (uint32_t k = 0; k < kSerialRegions; ++k) {
-            reg[k] = kEmpty;
-            if (k < cells) {
-                if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = cy * bins.regions_x + cx;
-                if (++cx > x1) { cx = x0; ++cy; }
+            for (uint32_t k = 0; k < kSerialBatch; ++k) {
+                reg[k] = kEmpty;
+                if (k0 + k < cells) {
+                    if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = cy * bins.regions_x + cx;
+                    if (++cx > x1) { cx = x0; ++cy; }
+                }
             }
+#pragma unroll
+            for (uint32_t k = 0; k < kSerialBatch; ++k)
+                slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < kSerialBatch; ++k)
+                if (reg[k] != kEmpty) place(reg[k], slot[k], i);
         }
-#pragma unroll
-        for (uint32_t k = 0; k < kSerialRegions; ++k)
-            slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < kSerialRegions; ++k)
-            if (reg[k] != kEmpty) place(reg[k], slot[k], i);
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
@@ -1066,7 +1198,7 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
     }
     ws.tile_tests += tests;
     if (have_ray) {
-        finish_ray(p, out, active, row, col, hl, ws);
+        finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
         return;
     }
     // No survivor: every ray of the tile misses (main.cxx:700-718 with no hit).
@@ -1143,206 +1275,6 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     }
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile0 == 0u ? n_cand : 0u, out.block_stats, g, t_start);
-}
-
-// ---------------------------------------------------------------------------
-// k_finish: (1) every workgroup sums a slice of the per-workgroup statistics;
-// (2) exact result for rays whose hit count exceeded the register list, one
-// ray per workgroup at a time.  The workgroup tests the ray against the
-// candidates of its region (binned: region list + global list; otherwise the
-// whole mesh), collects the accepted distances in LDS, sorts them (bitonic)
-// and sums the pairs in ascending order as main.cxx:703-708 does.  A ray with
-// more than kOverflowLds hits streams its sorted sequence instead: repeated
-// workgroup-wide scans for the next larger distance and its multiplicity.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kOverflowLds = 2048;
-
-__device__ void stats_reduce_slice(const BlockStats* __restrict__ parts, uint32_t n_blocks,
-                                   DevStats* __restrict__ st)
-{
-    __shared__ unsigned long long s_sum[7][4];
-    __shared__ unsigned int s_max[4];
-    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
-    unsigned int mx = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_blocks; i += gridDim.x * blockDim.x) {
-        const BlockStats& b = parts[i];
-        v[0] += b.rays; v[1] += b.hit_rays; v[2] += b.odd_rays; v[3] += b.overflow_rays;
-        v[4] += b.hits; v[5] += b.tile_tests; v[6] += b.candidates;
-        mx = mx > b.max_hits ? mx : b.max_hits;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) v[k] += __shfl_xor(v[k], off);
-        unsigned int o = __shfl_xor(mx, off);
-        mx = mx > o ? mx : o;
-    }
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (lane == 0) {
-        for (int k = 0; k < 7; ++k) s_sum[k][wave] = v[k];
-        s_max[wave] = mx;
-    }
-    __syncthreads();
-    if (threadIdx.x < 8u) {
-        const uint32_t k = threadIdx.x;
-        if (k < 7) {
-            unsigned long long t = 0;
-            for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) t += s_sum[k][w];
-            unsigned long long* dst[7] = {&st->rays, &st->hit_rays, &st->odd_rays, &st->overflow_rays,
-                                          &st->hits, &st->tile_tests, &st->candidates};
-            if (t) atomicAdd(dst[k], t);
-        } else {
-            unsigned int m = 0;
-            for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) m = m > s_max[w] ? m : s_max[w];
-            if (m) atomicMax(&st->max_hits, m);
-        }
-    }
-}
-
-struct OverflowLDS {
-    float t[kOverflowLds];
-    uint32_t n;
-    float red_t[4];
-    uint32_t red_n[4];
-};
-
-// Workgroup min over lanes of `cur` and the number of lanes' `mult` whose cur
-// equals it (sum).  Every thread gets the result.
-__device__ __forceinline__ void block_min_mult(OverflowLDS& s, float& cur, uint32_t& mult)
-{
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float oc = __shfl_xor(cur, off);
-        const uint32_t om = __shfl_xor(mult, off);
-        if (oc < cur) { cur = oc; mult = om; }
-        else if (oc == cur) mult += om;
-    }
-    __syncthreads();
-    if (lane == 0) { s.red_t[wave] = cur; s.red_n[wave] = mult; }
-    __syncthreads();
-    cur = s.red_t[0];
-    mult = s.red_n[0];
-    for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) {
-        if (s.red_t[w] < cur) { cur = s.red_t[w]; mult = s.red_n[w]; }
-        else if (s.red_t[w] == cur) mult += s.red_n[w];
-    }
-}
-
-template <typename Fetch>
-__device__ float overflow_distance(OverflowLDS& s, const TriRec* __restrict__ recs, uint32_t n_cand,
-                                   Fetch fetch, float dx, float dy, float dz, uint32_t& n_hits)
-{
-    auto hit_of = [&](uint32_t k, float& t) {
-        const TriRec& r = recs[fetch(k)];
-        return mt_intersect(dx, dy, dz, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z, r.tvx, r.tvy,
-                            r.tvz, r.qvx, r.qvy, r.qvz, r.tnum, t) &&
-               accept_t(t);
-    };
-    if (threadIdx.x == 0) s.n = 0;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < n_cand; k += blockDim.x) {
-        float t;
-        if (hit_of(k, t)) {
-            const uint32_t idx = atomicAdd(&s.n, 1u);
-            if (idx < kOverflowLds) s.t[idx] = t;
-        }
-    }
-    __syncthreads();
-    const uint32_t n = s.n;
-    n_hits = n;
-    if (n & 1u) return 0.0f;                 // odd count: main.cxx:709-713
-    float distance = 0.0f;
-    if (n <= kOverflowLds) {
-        uint32_t m = 1;
-        while (m < n) m <<= 1;
-        for (uint32_t k = n + threadIdx.x; k < m; k += blockDim.x) s.t[k] = __builtin_inff();
-        __syncthreads();
-        for (uint32_t size = 2; size <= m; size <<= 1) {          // bitonic sort, ascending
-            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-                for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-                    const uint32_t j = i ^ stride;
-                    if (j > i) {
-                        const float a = s.t[i], b = s.t[j];
-                        const bool up = (i & size) == 0;
-                        if (up ? (b < a) : (a < b)) { s.t[i] = b; s.t[j] = a; }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        if (threadIdx.x == 0)
-            for (uint32_t k = 0; k + 1 < n; k += 2) distance += s.t[k + 1] - s.t[k];
-        return distance;                     // valid in thread 0
-    }
-    // Streamed: the sorted sequence by repeated scans (value, multiplicity).
-    uint32_t pos = 0;
-    float prev = -__builtin_inff(), pending = 0.0f;
-    bool first = true;
-    while (pos < n) {
-        float cur = __builtin_inff();
-        uint32_t mult = 0;
-        for (uint32_t k = threadIdx.x; k < n_cand; k += blockDim.x) {
-            float t;
-            if (hit_of(k, t) && (first || t > prev)) {
-                if (t < cur) { cur = t; mult = 1; }
-                else if (t == cur) ++mult;
-            }
-        }
-        block_min_mult(s, cur, mult);
-        if (mult == 0) break;                // cannot happen; keeps the loop bounded
-        for (uint32_t q = 0; q < mult && pos < n; ++q, ++pos) {
-            if ((pos & 1u) == 0) pending = cur;
-            else distance += cur - pending;
-        }
-        prev = cur;
-        first = false;
-    }
-    return distance;
-}
-
-__global__ __launch_bounds__(256) void k_finish(const TriRec* __restrict__ recs, RenderParams p,
-                                                Outputs out, uint32_t n_blocks, BinBuffers bins,
-                                                BinState* __restrict__ bs)
-{
-    __shared__ OverflowLDS s;
-    stats_reduce_slice(out.block_stats, n_blocks, out.stats);
-    const uint32_t count = out.stats->overflow_count;
-    const uint32_t G = bins.counts ? bs->global_count : 0u;
-    for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
-        const uint32_t o = out.overflow_list[e];
-        const uint32_t row = p.row_begin + o / p.width;
-        const uint32_t col = o % p.width;
-        float dx, dy, dz;
-        make_ray(p, row, col, dx, dy, dz);
-        uint32_t n_hits = 0;
-        float distance;
-        const uint32_t region = (o / p.width / kRegion) * bins.regions_x + col / kRegion;
-        const uint32_t n_local = bins.counts ? bins.counts[(size_t)region * kCounterStride] : 0u;
-        if (bins.counts && n_local <= bins.cap) {
-            const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
-            const uint32_t* __restrict__ glob = bins.global_list;
-            distance = overflow_distance(s, recs, n_local + G,
-                                         [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; },
-                                         dx, dy, dz, n_hits);
-        } else {
-            distance = overflow_distance(s, recs, p.num_triangles, [](uint32_t k) { return k; }, dx,
-                                         dy, dz, n_hits);
-        }
-        if (threadIdx.x == 0) {
-            const float photon = shade(distance);
-            if (out.image) out.image[o] = photon;
-            if (out.lbuffer) out.lbuffer[o] = distance;   // n > capacity >= 1, so the ray hit
-            if (out.image_u8) out.image_u8[o] = lut_u8(photon);
-        }
-        __syncthreads();                      // s is reused by the next ray
-    }
-    // Binned frames: the frame's binning state for xrt_read_stats.
-    if (bins.counts && blockIdx.x == 0 && threadIdx.x == 0) {
-        out.stats->bin.max_count = bs->max_count;
-        out.stats->bin.global_count = bs->global_count;
-        out.stats->bin.overflow = bs->overflow;
-    }
 }
 
 // ---------------------------------------------------------------------------

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -26,7 +27,9 @@ constexpr uint32_t kInitialRegionCap = 256;
 constexpr uint32_t kMaxRegionCap = 1u << 16;
 // Timed regions put render timing events on every kTimingStride-th frame.
 constexpr uint64_t kTimingStride = 4;
-constexpr unsigned kFinishBlocks = XRT_FINISH_BLOCKS;   // k_finish workgroups
+// Buffer sets in rotation: frame N's preparation reuses the set of frame
+// N - kFrameSets, whose render the host has seen complete by then.
+constexpr int kFrameSets = 4;
 
 inline uint32_t region_cap_for(uint32_t max_count)
 {
@@ -36,15 +39,23 @@ inline uint32_t region_cap_for(uint32_t max_count)
     return cap;
 }
 
-// Everything one frame's preparation writes and its render reads.  Two sets
-// alternate, so frame N+1's preparation (k_prep, binning) runs on the
-// context's prep stream while frame N renders on the caller's stream.
+// Everything one frame's preparation writes and its render reads or writes.
+// kFrameSets sets rotate, so frame N+1's preparation (k_prep, binning) runs on
+// the context's prep stream while frame N renders on the caller's stream.
+// Ordering is kept by the host, not by cross-queue waits on the device
+// (each costs the render queue several microseconds per frame, DESIGN.md
+// "Pipelining"): the host waits for the preparation's completion event before
+// it launches the render, and for the completion event of the render that
+// last used the set before it prepares into the set again.
 struct FrameSet {
     TriRec* recs = nullptr;        // per-render records
     size_t recs_cap = 0;
     float4* cull = nullptr;        // per-render cull planes (4 x T float4)
     size_t cull_cap = 0;
-    DevStats* stats = nullptr;
+    BlockStats* block_stats = nullptr;   // the render's per-workgroup / per-wave records
+    size_t block_stats_cap = 0;
+    uint32_t n_blocks = 0;         // records of the set's last render
+    bool binned = false;           // the set's last frame was binned (BinState valid)
 
     // binning (XRT_KERNEL_BINNED)
     uint32_t* bin_counts = nullptr;    // BinState line | line-padded region counts
@@ -53,11 +64,13 @@ struct FrameSet {
     size_t bin_list_cap = 0;
     uint32_t* global_list = nullptr;
     size_t global_list_cap = 0;
-    uint32_t* overflow = nullptr;      // rays past the register hit list
-    size_t overflow_cap = 0;
 
-    hipEvent_t ready = nullptr;        // preparation done (prep stream)
-    hipEvent_t done = nullptr;         // render + k_finish done (caller's stream)
+    // Completion events ride on the kernel dispatches themselves
+    // (hipExtLaunchKernel stop events): no separate event packets.
+    hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
+    hipEvent_t t0 = nullptr, t1 = nullptr;   // render start / end (untimed frames)
+    hipEvent_t done = nullptr;         // render end (unsampled frames of a timed region)
+    hipEvent_t done_ev = nullptr;      // the event that marks the set's last render complete
     bool done_valid = false;
 };
 
@@ -69,14 +82,11 @@ struct xrt_context {
     uint64_t num_tris = 0;
     size_t tris_cap = 0;
 
-    FrameSet sets[2];
+    FrameSet sets[kFrameSets];
     int next_set = 0;
     FrameSet* last_set = nullptr;      // set of the last enqueued frame
     hipStream_t prep_stream = nullptr;
 
-    BlockStats* d_block_stats = nullptr;   // written by the render, read by k_finish (caller's stream)
-    size_t block_stats_cap = 0;
-    uint32_t last_blocks = 0;          // workgroups of the last render (diagnostics)
     uint32_t bin_region_cap = kInitialRegionCap;   // list capacity per region (grown by sizing)
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     uint32_t* d_order = nullptr;       // render launch order of the regions (launch_order)
@@ -111,7 +121,17 @@ struct xrt_context {
     bool bin_key_valid = false;
     int last_kernel = XRT_KERNEL_BINNED;
     uint32_t hit_capacity = kMaxHits;
+    // XRT_HOST_PROFILE=1: host time per enqueue, split by wait (printed at destroy)
+    bool host_profile = false;
+    double hp_total = 0, hp_done = 0, hp_prep = 0;
+    uint64_t hp_calls = 0;
 };
+
+using HostClock = std::chrono::steady_clock;
+inline double seconds_since(HostClock::time_point t)
+{
+    return std::chrono::duration<double>(HostClock::now() - t).count();
+}
 
 static std::string g_create_error;
 
@@ -232,11 +252,11 @@ int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, ui
 }
 
 int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const CullParams& cp, bool culled,
-                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream)
+                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
 {
     const uint64_t T = ctx->num_tris;
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, ctx->d_tris,
-                       (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl, fs.stats);
+    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, nullptr, done, 0,
+                          ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl);
     XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
@@ -309,7 +329,6 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
 
     const uint64_t T = ctx->num_tris;
     const uint32_t rows = row_end - row_begin;
-    const uint64_t rays = (uint64_t)rows * cam->width;
     const uint32_t rx = (cam->width + kRegion - 1) / kRegion, ry = (rows + kRegion - 1) / kRegion;
     // AUTO: the per-region footprint sweep of TILED costs T x regions box
     // tests; past kAutoSweep of them binning once per frame is cheaper.
@@ -320,18 +339,23 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     const bool culled = kernel != XRT_KERNEL_BRUTE;
     const bool binned = kernel == XRT_KERNEL_BINNED && rows > 0 && T > 0;
 
-    // This frame's buffer set; its preparation waits (on the prep stream) for
-    // the render that last used the set, the render waits for the preparation.
+    // This frame's buffer set.  The render that last used it (kFrameSets
+    // frames ago) must be complete before the set is prepared again.
     FrameSet& fs = ctx->sets[ctx->next_set];
     static const bool serial = [] {          // A/B only: XRT_PIPELINE=0 prepares on the caller's stream
         const char* e = std::getenv("XRT_PIPELINE");
         return e && std::atoi(e) == 0;
     }();
     hipStream_t ps = serial ? stream : ctx->prep_stream;
+    const auto t_call = HostClock::now();
+    if (fs.done_valid) {
+        const auto t = HostClock::now();
+        XRT_HIP(ctx, hipEventSynchronize(fs.done_ev));
+        fs.done_valid = false;
+        if (ctx->host_profile) ctx->hp_done += seconds_since(t);
+    }
     if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
     if (culled && (rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
-    if ((rc = ensure(ctx, fs.overflow, fs.overflow_cap, rays))) return rc;
-    if (fs.done_valid && ps != stream) XRT_HIP(ctx, hipStreamWaitEvent(ps, fs.done, 0));
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
     CullParams cp = make_cull_params(*cam);
@@ -339,8 +363,6 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.image = d_image;
     out.lbuffer = d_lbuffer;
     out.image_u8 = d_u8;
-    out.overflow_list = fs.overflow;
-    out.stats = fs.stats;
     const uint32_t n_regions = rows ? rx * ry : 0u;
     // BINNED: 8x8 tiles per render wave.  One (A/B, whole step: 1 wins at
     // 1024^2, 2048^2 and the 1M-triangle 8192^2 frame; a row of 4 wins by 10 %
@@ -355,9 +377,10 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
                                            : dim3(rx, ry);
     // stats records: one per workgroup, one per tile wave for BINNED
     const uint32_t n_blocks = rows ? grid.x * grid.y * (binned ? kTileWaves : 1u) : 0u;
-    if ((rc = ensure(ctx, ctx->d_block_stats, ctx->block_stats_cap, n_blocks))) return rc;
-    ctx->last_blocks = n_blocks;
-    out.block_stats = ctx->d_block_stats;
+    if ((rc = ensure(ctx, fs.block_stats, fs.block_stats_cap, n_blocks))) return rc;
+    fs.n_blocks = n_blocks;
+    fs.binned = binned;
+    out.block_stats = fs.block_stats;
 
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
@@ -368,11 +391,8 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
     }
 
-    if (T) {   // k_prep clears DevStats for the frame
-        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps))) return rc;
-    } else {
-        XRT_HIP(ctx, hipMemsetAsync(fs.stats, 0, sizeof(DevStats), ps));
-    }
+    hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
+    if (T && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     if (binned && !ctx->bin_force_cap) {
         // Size the region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of the largest region count, and a
@@ -392,24 +412,30 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             if (h.max_count > bins.cap && ctx->bin_region_cap < kMaxRegionCap) {
                 ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(h.max_count));
                 if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;   // clears
-                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps))) return rc;
+                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
             }
         }
     }
-    if (ps != stream) {
-        XRT_HIP(ctx, hipEventRecord(fs.ready, ps));
-        XRT_HIP(ctx, hipStreamWaitEvent(stream, fs.ready, 0));
+    // The render is launched once the preparation is complete (host-side
+    // order; the caller's queue never waits on the prep queue).
+    if (T && prep_done) {
+        const auto t = HostClock::now();
+        XRT_HIP(ctx, hipEventSynchronize(prep_done));
+        if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
     }
 
-    // The render kernel's own dispatch carries the timing events
-    // (hipExtLaunchKernel): no separate event packets between the kernels.
-    // Inside a timed region (xrt_timing_begin/end) every kTimingStride-th
-    // frame carries them -- each pair costs the frame a few microseconds --
-    // and the mean render duration is taken over those frames.
-    hipEvent_t t0 = ctx->ev_begin, t1 = ctx->ev_end;
+    // Events ride on the render's own dispatch (hipExtLaunchKernel).  Outside
+    // timed regions every frame carries the set's start/end pair (stats
+    // kernel_ms); inside one (xrt_timing_begin/end) every kTimingStride-th
+    // frame carries a timing pair -- a start event costs the frame a few
+    // microseconds -- and the others only the set's end event, which the host
+    // needs to reuse the set.  The mean render duration is taken over the
+    // sampled frames.
+    hipEvent_t t0 = fs.t0, t1 = fs.t1;
     const bool sampled = ctx->timing && (ctx->timed_frames++ % kTimingStride) == 0;
     if (ctx->timing && !sampled) {
-        t0 = t1 = nullptr;
+        t0 = nullptr;
+        t1 = fs.done;
     } else if (ctx->timing) {
         if (ctx->tev_used + 2 > ctx->tev.size()) {
             for (int k = 0; k < 256; ++k) {
@@ -427,7 +453,11 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         const char* e = std::getenv("XRT_NO_EVENTS");
         return e && std::atoi(e) != 0;
     }();
-    if (no_events) t0 = t1 = nullptr;
+    if (no_events) {
+        if (sampled) ctx->tev_used -= 2;
+        t0 = nullptr;
+        t1 = fs.done;
+    }
     if (rows > 0) {
         if (kernel == XRT_KERNEL_BRUTE)
             hipExtLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, t0, t1, 0, fs.recs, p, out);
@@ -443,23 +473,18 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         if (t0) {
             ctx->last_t0 = t0;
             ctx->last_t1 = t1;
-        } else if (sampled) {
-            ctx->tev_used -= 2;     // XRT_NO_EVENTS
         }
-    } else if (sampled) {
+        fs.done_ev = t1;
+        fs.done_valid = true;
+    } else if (sampled && !no_events) {
         ctx->tev_used -= 2;         // nothing launched, nothing to time
     }
-    if (rows > 0) {
-        hipLaunchKernelGGL(k_finish, dim3(kFinishBlocks), dim3(256), 0, stream, fs.recs, p, out, n_blocks,
-                           bins, bin_ctl);
-        XRT_HIP(ctx, hipGetLastError());
-    }
-    if (ps != stream) {
-        XRT_HIP(ctx, hipEventRecord(fs.done, stream));
-        fs.done_valid = true;
+    if (ctx->host_profile) {
+        ctx->hp_total += seconds_since(t_call);
+        ++ctx->hp_calls;
     }
     ctx->last_set = &fs;
-    ctx->next_set ^= 1;
+    ctx->next_set = (ctx->next_set + 1) % kFrameSets;
     ctx->last_stream = stream;
     ctx->pending = true;
     ctx->last_kernel = kernel;
@@ -494,6 +519,8 @@ int xrt_create(int device, xrt_context** out)
         return fail(nullptr, XRT_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
     xrt_context* ctx = new xrt_context();
     ctx->device = device;
+    const char* hp = std::getenv("XRT_HOST_PROFILE");
+    ctx->host_profile = hp && std::atoi(hp) != 0;
     // The prep stream gets the highest queue priority: its small workgroups
     // must find CU slots while the previous frame's render fills the chip.
     int prio_least = 0, prio_greatest = 0;
@@ -502,11 +529,9 @@ int xrt_create(int device, xrt_context** out)
     if (pp && std::atoi(pp) == 0) prio_greatest = prio_least;
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess &&
               hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
-    for (FrameSet& fs : ctx->sets)
-        ok = ok && hipMalloc(&fs.stats, sizeof(DevStats)) == hipSuccess &&
-             hipMemset(fs.stats, 0, sizeof(DevStats)) == hipSuccess &&
-             hipEventCreateWithFlags(&fs.ready, hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&fs.done, hipEventDisableTiming) == hipSuccess;
+    for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
+        ok = ok && hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
+             hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
         return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
@@ -518,6 +543,11 @@ int xrt_create(int device, xrt_context** out)
 void xrt_destroy(xrt_context* ctx)
 {
     if (!ctx) return;
+    if (ctx->host_profile && ctx->hp_calls)
+        std::fprintf(stderr, "xrt host profile: %llu enqueues, per call %.1f us (waiting: set reuse %.1f us, "
+                     "preparation %.1f us)\n", (unsigned long long)ctx->hp_calls,
+                     ctx->hp_total / ctx->hp_calls * 1e6, ctx->hp_done / ctx->hp_calls * 1e6,
+                     ctx->hp_prep / ctx->hp_calls * 1e6);
     (void)hipSetDevice(ctx->device);
     if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
     (void)hipDeviceSynchronize();
@@ -525,16 +555,14 @@ void xrt_destroy(xrt_context* ctx)
     for (FrameSet& fs : ctx->sets) {
         (void)hipFree(fs.recs);
         (void)hipFree(fs.cull);
-        (void)hipFree(fs.stats);
+        (void)hipFree(fs.block_stats);
         (void)hipFree(fs.bin_counts);
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
-        (void)hipFree(fs.overflow);
-        if (fs.ready) (void)hipEventDestroy(fs.ready);
-        if (fs.done) (void)hipEventDestroy(fs.done);
+        for (hipEvent_t e : {fs.ready, fs.t0, fs.t1, fs.done})
+            if (e) (void)hipEventDestroy(e);
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
-    (void)hipFree(ctx->d_block_stats);
     (void)hipFree(ctx->d_order);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
@@ -650,9 +678,10 @@ int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint
         XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
         ctx->pending = false;
     }
-    *n_records = ctx->last_blocks;
-    const size_t bytes = std::min<size_t>((size_t)capacity, (size_t)ctx->last_blocks * sizeof(BlockStats));
-    if (bytes && dst) XRT_HIP(ctx, hipMemcpy(dst, ctx->d_block_stats, bytes, hipMemcpyDeviceToHost));
+    const FrameSet* fs = ctx->last_set;
+    *n_records = fs ? fs->n_blocks : 0u;
+    const size_t bytes = std::min<size_t>((size_t)capacity, (size_t)*n_records * sizeof(BlockStats));
+    if (bytes && dst) XRT_HIP(ctx, hipMemcpy(dst, fs->block_stats, bytes, hipMemcpyDeviceToHost));
     return XRT_OK;
 }
 
@@ -687,29 +716,46 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
         XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
         ctx->pending = false;
     }
-    DevStats s;
-    if (ctx->last_set) XRT_HIP(ctx, hipMemcpy(&s, ctx->last_set->stats, sizeof s, hipMemcpyDeviceToHost));
-    else std::memset(&s, 0, sizeof s);
+    // The last render's per-workgroup (per-wave) records, summed here.
+    std::memset(stats, 0, sizeof *stats);
+    const FrameSet* fs = ctx->last_set;
+    if (fs && fs->n_blocks) {
+        std::vector<BlockStats> rec(fs->n_blocks);
+        XRT_HIP(ctx, hipMemcpy(rec.data(), fs->block_stats, rec.size() * sizeof(BlockStats),
+                               hipMemcpyDeviceToHost));
+        for (const BlockStats& b : rec) {
+            stats->rays += b.rays;
+            stats->hit_rays += b.hit_rays;
+            stats->odd_rays += b.odd_rays;
+            stats->overflow_rays += b.overflow_rays;
+            stats->hits += b.hits;
+            stats->tile_tests += b.tile_tests;
+            stats->candidates += b.candidates;
+            stats->max_hits = std::max(stats->max_hits, b.max_hits);
+        }
+    }
     float ms = 0.0f;
     if (!ctx->last_t0 || hipEventElapsedTime(&ms, ctx->last_t0, ctx->last_t1) != hipSuccess) ms = 0.0f;
-    stats->rays = s.rays;
-    stats->hit_rays = s.hit_rays;
-    stats->odd_rays = s.odd_rays;
-    stats->overflow_rays = s.overflow_rays;
-    stats->hits = s.hits;
-    stats->max_hits = s.max_hits;
     stats->kernel = (uint32_t)ctx->last_kernel;
     stats->kernel_ms = ms;
-    stats->candidates = s.candidates;
-    stats->tile_tests = s.tile_tests;
-    if (s.bin.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
-        ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(s.bin.max_count));
+    if (fs && fs->binned && fs->bin_counts) {
+        BinState bs = {};
+        XRT_HIP(ctx, hipMemcpy(&bs, fs->bin_counts, sizeof bs, hipMemcpyDeviceToHost));
+        if (bs.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
+            ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(bs.max_count));
+    }
     return XRT_OK;
 }
 
 int xrt_timing_begin(xrt_context* ctx)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
+    // Frames in flight may mark their completion with events of the previous
+    // timed region, which this one re-records: wait for them first.
+    for (FrameSet& fs : ctx->sets) {
+        if (fs.done_valid) XRT_HIP(ctx, hipEventSynchronize(fs.done_ev));
+        fs.done_valid = false;
+    }
     ctx->timing = true;
     ctx->tev_used = 0;
     ctx->timed_frames = 0;
@@ -836,7 +882,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr);
+                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, fs.recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));

@@ -209,10 +209,11 @@ def plane_stack(n, spacing=0.01):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("planes,size", [(40, 48), (2100, 8)])
+@pytest.mark.parametrize("planes,size", [(40, 48), (300, 16), (2100, 8)])
 def test_deep_stack_overflow(ctx, kernel, planes, size):
-    """Rays with 40..4200 hits: the cooperative overflow path (LDS sort up to
-    2048 hits, streamed beyond) must equal the oracle's std::sort + pair sum."""
+    """Rays with 40..4200 hits: the wave-wide overflow fix-up (register lists
+    bitonic-sorted across the wave up to 8 hits a lane, streamed beyond) must
+    equal the oracle's std::sort + pair sum."""
     if kernel == xrt.XRT_KERNEL_BRUTE and planes > 100:
         pytest.skip("brute force is covered by the 40-plane case")
     soup = plane_stack(planes)
