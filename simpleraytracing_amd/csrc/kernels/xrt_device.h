@@ -47,6 +47,9 @@
 #ifndef XRT_PRE_REJECT
 #define XRT_PRE_REJECT 0     // culled tests: wave-wide division-free reject before the exact test (A/B: slower, off)
 #endif
+#ifndef XRT_ABLATION
+#define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
+#endif
 #ifndef XRT_STAMPS
 #define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
 #endif
@@ -93,7 +96,9 @@ struct RenderParams {
     uint32_t ablate;        // diagnostics only ($XRT_ABLATE bits, kAblate*); 0 in production
 };
 
-// Ablation bits (timing studies; outputs are wrong when any is set).
+// Ablation bits (timing studies; outputs are wrong when any is set).  Only
+// XRT_ABLATION builds (tools/gpu_ablate.sh) read them: the production kernels
+// carry neither the field nor its branches.
 constexpr uint32_t kAblateCandidates = 1;   // phase 2 sees no candidates
 constexpr uint32_t kAblateSweep = 2;        // tiled: no phase-1 footprint sweep
 constexpr uint32_t kAblateRayGen = 4;       // constant ray direction
@@ -102,12 +107,24 @@ constexpr uint32_t kAblateShade = 16;       // no expf / LUT
 constexpr uint32_t kAblateExact = 32;       // culled kernels: no Moller-Trumbore for survivors
 constexpr uint32_t kAblatePush = 64;        // culled kernels: exact test but no hit-list insert
 
+__device__ __forceinline__ uint32_t ablation(const RenderParams& p)
+{
+#if XRT_ABLATION
+    return p.ablate;
+#else
+    (void)p;
+    return 0u;
+#endif
+}
+
 constexpr int kMaxHits = 16;
 
 // ---------------------------------------------------------------------------
 // Ray generation: src/main.cxx:652-661 and the Ray ctor, include/Ray.inl:74-85.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void make_ray(const RenderParams& p, uint32_t row, uint32_t col,
+// P: RenderParams in any address space (kernel argument or constant memory).
+template <typename P>
+__device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
                                          float& dx, float& dy, float& dz)
 {
     // :655-656  float * (0.5 + unsigned - unsigned / 2.0) in double, narrowed once

@@ -57,6 +57,11 @@ struct Outputs {
     float* lbuffer;
     uint8_t* image_u8;
     BlockStats* block_stats;   // one per workgroup (BINNED: per wave) of the render grid
+    // The frame's parameters in device memory (written by k_prep), read by
+    // make_ray through this constant-address-space pointer: scalar loads where
+    // a tile first needs its rays, instead of camera kernel arguments held in
+    // SGPRs for the whole kernel.
+    const __attribute__((address_space(4))) RenderParams* frame;
 };
 
 // Running counters of one wave: ballot counts (wave-uniform), per-lane hit sum
@@ -68,6 +73,15 @@ struct WaveStats {
 };
 
 constexpr double kEps = 0x1p-24;
+
+// Wave-uniform values the compiler cannot prove uniform (a wave's index in its
+// workgroup, a count loaded through a plain pointer): moved to an SGPR, so the
+// loops they bound are scalar-controlled and what derives from them is scalar.
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t wave_in_block() { return wave_uniform(threadIdx.x >> 6); }
 
 __device__ __forceinline__ void cross_d(const double a[3], const double b[3], double o[3])
 {
@@ -386,8 +400,8 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
     }
     if (!active) return;
     size_t o = (size_t)(row - p.row_begin) * p.width + col;
-    if (p.ablate & (kAblateStores | kAblateShade)) {
-        if (!(p.ablate & kAblateStores)) {
+    if (ablation(p) & (kAblateStores | kAblateShade)) {
+        if (!(ablation(p) & kAblateStores)) {
             if (out.image) out.image[o] = distance;
             if (out.lbuffer) out.lbuffer[o] = lval;
         }
@@ -426,13 +440,13 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
                                                       RenderParams p, Outputs out)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = wave_in_block();
     const uint32_t col = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
     const uint32_t row = p.row_begin + (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
     const bool active = col < p.width && row < p.row_end;
 
     float dx, dy, dz;
-    make_ray(p, row, col, dx, dy, dz);
+    make_ray(*out.frame, row, col, dx, dy, dz);
     HitList hl;
     hl.init();
     const uint32_t T = p.num_triangles;
@@ -560,9 +574,9 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
                                                     Fetch fetch, WaveStats& ws, StageLDS& st)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = wave_in_block();
     const uint32_t T = p.num_triangles;
-    if (p.ablate & kAblateCandidates) n_cand = 0;
+    if (ablation(p) & kAblateCandidates) n_cand = 0;
     const bool once = n_cand <= kStage;
     if (once) {
         stage_candidates(st, recs, culls, T, 0u, n_cand, fetch);
@@ -578,20 +592,20 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
 
         float dx = 0.0f, dy = 0.0f, dz = 0.0f;
-        if (tile_live && !(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+        if (tile_live && !(ablation(p) & kAblateRayGen)) make_ray(*out.frame, row, col, dx, dy, dz);
         else dx = 1.0f;
         HitList hl;
         hl.init();
         uint32_t tests = 0;
         if (once) {
-            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, p.ablate);
+            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, ablation(p));
         } else {
             for (uint32_t first = 0; first < n_cand; first += kStage) {
                 const uint32_t count = min(kStage, n_cand - first);
                 __syncthreads();
                 stage_candidates(st, recs, culls, T, first, count, fetch);
                 __syncthreads();
-                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, p.ablate);
+                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, ablation(p));
             }
         }
         if (tile_live) {
@@ -628,7 +642,7 @@ __global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriR
     // workgroup starts at a different chunk so concurrent reads spread over
     // the L2 channels.
     const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
-    const uint32_t nchunks = (p.ablate & kAblateSweep) ? 0u : (T + 1023u) / 1024u;
+    const uint32_t nchunks = (ablation(p) & kAblateSweep) ? 0u : (T + 1023u) / 1024u;
     uint32_t chunk =
         nchunks ? (uint32_t)(((uint64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 2654435761u) % nchunks) : 0u;
     for (uint32_t c = 0; c < nchunks; ++c, chunk = (chunk + 1u == nchunks) ? 0u : chunk + 1u) {
@@ -657,7 +671,7 @@ __global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriR
         }
     }
     __syncthreads();
-    const uint32_t n_cand = s_count;
+    const uint32_t n_cand = wave_uniform(s_count);
     WaveStats ws = {};
     if (n_cand <= kListCap)
         render_region_tiles(p, out, recs, culls, rx0, ry0, n_cand,
@@ -908,13 +922,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
-                                              BinState* __restrict__ bs)
+                                              BinState* __restrict__ bs,
+                                              RenderParams* __restrict__ frame_out)
 {
     // The preparation of frame N+1 shares the CUs with frame N's render (prep
     // stream): top wave priority keeps this latency-bound chain short.
     XRT_PREP_PRIO();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
+    if (i == 0 && frame_out) *frame_out = p;       // the render's make_ray reads it (Outputs::frame)
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
     Footprint fp;
     if (valid) {
@@ -1178,10 +1194,10 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
         if (!m) continue;
         tests += (uint32_t)__popcll(m);
         if (!have_ray) {
-            if (!(p.ablate & kAblateRayGen)) make_ray(p, row, col, dx, dy, dz);
+            if (!(ablation(p) & kAblateRayGen)) make_ray(*out.frame, row, col, dx, dy, dz);
             have_ray = true;
         }
-        if (p.ablate & kAblateExact) continue;
+        if (ablation(p) & kAblateExact) continue;
         while (m) {
             const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
@@ -1203,7 +1219,7 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
     }
     // No survivor: every ray of the tile misses (main.cxx:700-718 with no hit).
     ws.rays += (uint32_t)__popcll(__ballot(active));
-    if (!active || (p.ablate & kAblateStores)) return;
+    if (!active || (ablation(p) & kAblateStores)) return;
     const size_t o = (size_t)(row - p.row_begin) * p.width + col;
     if (out.image) out.image[o] = 80.0f;
     if (out.lbuffer) out.lbuffer[o] = __builtin_inff();
@@ -1221,7 +1237,7 @@ __device__ __forceinline__ void render_tiles_wave(const RenderParams& p, const O
                                                   uint32_t ry0, uint32_t tile0, uint32_t n_cand,
                                                   Fetch fetch, WaveStats& ws)
 {
-    if (p.ablate & kAblateCandidates) n_cand = 0;
+    if (ablation(p) & kAblateCandidates) n_cand = 0;
     Cand first;                                   // ids only: the edges are re-read per tile
     {
         const uint32_t k = threadIdx.x & 63u;
@@ -1251,16 +1267,16 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 {
     constexpr uint32_t kWavesPerRegion = 16u / TPW;
     const uint64_t t_start = block_start_stamp();
-    const uint32_t g = blockIdx.x * kTileWaves + (threadIdx.x >> 6);     // wave of the grid
+    const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
     const uint32_t slot = g / kWavesPerRegion;
-    const uint32_t region = bins.order ? bins.order[slot] : slot;
+    const uint32_t region = wave_uniform(bins.order ? bins.order[slot] : slot);
     const uint32_t tile0 = (g % kWavesPerRegion) * TPW;
     const uint32_t rx0 = (region % bins.regions_x) * kRegion;
     const uint32_t ry0 = p.row_begin + (region / bins.regions_x) * kRegion;
     WaveStats ws = {};
     uint32_t n_cand = 0;
     if (rx0 + (tile0 & 3u) * 8u < p.width && ry0 + (tile0 >> 2) * 8u < p.row_end) {   // wave-uniform
-        const uint32_t n_local = bins.counts[(size_t)region * kCounterStride];
+        const uint32_t n_local = wave_uniform(bins.counts[(size_t)region * kCounterStride]);
         if (n_local > bins.cap) {   // the region's list overflowed: whole mesh (exact, slower)
             n_cand = p.num_triangles;
             render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
@@ -1268,7 +1284,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         } else {
             const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
             const uint32_t* __restrict__ glob = bins.global_list;
-            n_cand = n_local + bs->global_count;
+            n_cand = n_local + wave_uniform(bs->global_count);
             render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
                                    [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
         }

@@ -52,6 +52,7 @@ struct FrameSet {
     size_t recs_cap = 0;
     float4* cull = nullptr;        // per-render cull planes (4 x T float4)
     size_t cull_cap = 0;
+    RenderParams* frame = nullptr;       // the frame's parameters (k_prep writes, make_ray reads)
     BlockStats* block_stats = nullptr;   // the render's per-workgroup / per-wave records
     size_t block_stats_cap = 0;
     uint32_t n_blocks = 0;         // records of the set's last render
@@ -256,7 +257,8 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
 {
     const uint64_t T = ctx->num_tris;
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, nullptr, done, 0,
-                          ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl);
+                          ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
+                          fs.frame);
     XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
@@ -363,6 +365,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.image = d_image;
     out.lbuffer = d_lbuffer;
     out.image_u8 = d_u8;
+    out.frame = (const __attribute__((address_space(4))) RenderParams*)fs.frame;
     const uint32_t n_regions = rows ? rx * ry : 0u;
     // BINNED: 8x8 tiles per render wave.  One (A/B, whole step: 1 wins at
     // 1024^2, 2048^2 and the 1M-triangle 8192^2 frame; a row of 4 wins by 10 %
@@ -393,6 +396,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
     if (T && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+    if (!T) XRT_HIP(ctx, hipMemcpy(fs.frame, &p, sizeof p, hipMemcpyHostToDevice));   // no k_prep to write it
     if (binned && !ctx->bin_force_cap) {
         // Size the region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of the largest region count, and a
@@ -530,7 +534,8 @@ int xrt_create(int device, xrt_context** out)
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess &&
               hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
-        ok = ok && hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
+        ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
+             hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
              hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
@@ -556,6 +561,7 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.recs);
         (void)hipFree(fs.cull);
         (void)hipFree(fs.block_stats);
+        (void)hipFree(fs.frame);
         (void)hipFree(fs.bin_counts);
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
@@ -882,7 +888,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr);
+                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, fs.recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));
