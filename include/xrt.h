@@ -185,7 +185,8 @@ typedef enum xrt_probe_op {
     XRT_PROBE_EXPF = 0,     /* std::exp(float) == glibc expf                     */
     XRT_PROBE_SQRTF = 1,    /* std::sqrt(float), correctly rounded               */
     XRT_PROBE_RCP = 2,      /* (float)(1.0 / (double)x), src/Ray.cxx:99           */
-    XRT_PROBE_LUT_U8 = 3    /* 8-bit LUT of a photon value (out[i] = (float)u8)  */
+    XRT_PROBE_LUT_U8 = 3,   /* 8-bit LUT of a photon value (out[i] = (float)u8)  */
+    XRT_PROBE_RCP_FAST = 4  /* the culled tests' 1/det (rcp + Newton where exact) */
 } xrt_probe_op;
 
 /* Evaluates one scalar device function elementwise.  Host buffers. */
@@ -208,8 +209,8 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
 void xrt_host_expf_batch(const float* in, float* out, uint64_t n);
 
 /*
- * Test hook: caps the per-ray register hit list at `capacity` (1..16) so the
- * exact overflow path runs.  0 restores the default (16).
+ * Test hook: caps the per-ray register hit list at `capacity` (1..12) so the
+ * exact overflow path runs.  0 restores the default (12).
  */
 int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
 

@@ -47,6 +47,9 @@
 #ifndef XRT_PRE_REJECT
 #define XRT_PRE_REJECT 0     // culled tests: wave-wide division-free reject before the exact test (A/B: slower, off)
 #endif
+#ifndef XRT_FAST_RCP
+#define XRT_FAST_RCP 0    // culled tests: rcp + Newton step for 1/det where exact (A/B: slower, off)
+#endif
 #ifndef XRT_ABLATION
 #define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
 #endif
@@ -117,7 +120,16 @@ __device__ __forceinline__ uint32_t ablation(const RenderParams& p)
 #endif
 }
 
-constexpr int kMaxHits = 16;
+// Register hit list per ray.  Each slot costs every exact test one
+// v_med3_f32; a ray with more hits is recomputed exactly by its wave
+// (finish_ray's fix-up, tens of microseconds for that wave).  dragon.ply rays
+// have at most 12 hits (2048^2: 102 rays above 8): 12 slots render it 3 %
+// faster than 16 with no fix-up; 8 slots would send those 102 rays through
+// it and run 5x slower (DESIGN.md "Hit list").
+#ifndef XRT_MAX_HITS
+#define XRT_MAX_HITS 12
+#endif
+constexpr int kMaxHits = XRT_MAX_HITS;
 
 // ---------------------------------------------------------------------------
 // Ray generation: src/main.cxx:652-661 and the Ray ctor, include/Ray.inl:74-85.
@@ -164,6 +176,36 @@ __device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
 // across one.  Checked on all 2^32 inputs (tools/check_fp_identities.c,
 // tests/test_abi.py); the f32 division sequence is about half the f64 one.
 __host__ __device__ __forceinline__ float inv_det_of(float det) { return 1.0f / det; }
+
+// v_rcp_f32 (within 1 ulp) and one FMA Newton step give the correctly rounded
+// 1.0f / d for every d with biased exponent in [1, 252], i.e. 2^-126 <= |d| <
+// 2^126: checked on all 2^32 inputs on the GPU (tools/probes/rcp_probe.hip,
+// profiles/r01_rcp_exhaustive.txt; the XRT_PROBE_RCP_FAST sweep of
+// tests/test_gpu_parity.py).  Three VALU ops instead of the ten of the IEEE
+// division sequence (div_scale / rcp / 4 fma / div_fmas / div_fixup).
+__device__ __forceinline__ float rcp_newton(float d)
+{
+    const float r = __builtin_amdgcn_rcpf(d);
+    return __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+}
+__device__ __forceinline__ bool rcp_newton_exact_for(float d)
+{
+    const float a = fabsf(d);
+    return a >= 0x1p-126f && a < 0x1p126f;       // false for NaN
+}
+// The culled tests' 1/det: the short sequence, unless some lane of the wave
+// has a det outside its range (zero, denormal, |det| >= 2^126, inf, NaN) --
+// that wave takes the IEEE division on every lane.  Equal to inv_det_of(det)
+// on every lane either way.
+__device__ __forceinline__ float inv_det_fast(float det)
+{
+#if XRT_FAST_RCP
+    if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) return inv_det_of(det);
+    return rcp_newton(det);
+#else
+    return inv_det_of(det);
+#endif
+}
 
 // Branch-free Ray::intersect for the culled kernels, whose survivors almost
 // always have a hitting lane (so the early reject would not skip the wave's
@@ -265,14 +307,19 @@ __host__ __device__ __forceinline__ bool mt_may_hit(float det, float a, float b,
 }
 
 // The rest of Ray::intersect from mt_numerators' values; `hit` includes accept_t.
-__host__ __device__ __forceinline__ float mt_finish(float det, float a, float b, float tnum, bool& hit)
+__host__ __device__ __forceinline__ float mt_finish_inv(float det, float inv_det, float a, float b,
+                                                       float tnum, bool& hit)
 {
-    const float inv_det = inv_det_of(det);                // Ray.cxx:99
     const float u = a * inv_det;                          // Ray.cxx:105
     const float v = b * inv_det;                          // Ray.cxx:115
     const float t = tnum * inv_det;                       // Ray.cxx:122
     hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
     return t;
+}
+
+__host__ __device__ __forceinline__ float mt_finish(float det, float a, float b, float tnum, bool& hit)
+{
+    return mt_finish_inv(det, inv_det_of(det), a, b, tnum, hit);   // Ray.cxx:99
 }
 
 __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1x, float e1y,
@@ -282,7 +329,7 @@ __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1
 {
     float det, a, b;
     mt_numerators(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tvx, tvy, tvz, qvx, qvy, qvz, det, a, b);
-    return mt_finish(det, a, b, tnum, hit);
+    return mt_finish_inv(det, inv_det_fast(det), a, b, tnum, hit);   // Ray.cxx:99
 }
 
 // ---------------------------------------------------------------------------

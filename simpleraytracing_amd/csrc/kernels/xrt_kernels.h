@@ -863,16 +863,26 @@ constexpr uint32_t kCounterStride = 32;
 constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
 constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back count atomics
 
+// Counters and lists are indexed by launch slot, not by region: the render
+// wave of slot s loads its count and list without first looking up which
+// region it renders (order[s], loaded alongside); k_prep maps region -> slot
+// through rank.
 struct BinBuffers {
-    uint32_t* counts;        // [n_regions * kCounterStride] cleared before every binned frame
-    uint32_t* list;          // [n_regions * cap] triangle ids per region
+    uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
+    uint32_t* list;          // [n_regions * cap] triangle ids by slot
     uint32_t* global_list;   // [T]
-    const uint32_t* order;   // [n_regions] render launch order (null: raster order)
+    const uint32_t* order;   // [n_regions] slot -> region, the render launch order (null: raster order)
+    const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
     uint32_t cap;            // list capacity per region
     uint32_t regions_x, regions_y;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t slot_of(const BinBuffers& bins, uint32_t region)
+{
+    return bins.rank ? bins.rank[region] : region;
+}
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
 // footprint box may touch; false when it touches none.
@@ -1000,7 +1010,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             for (uint32_t k = 0; k < kSerialBatch; ++k) {
                 reg[k] = kEmpty;
                 if (k0 + k < cells) {
-                    if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = cy * bins.regions_x + cx;
+                    if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = slot_of(bins, cy * bins.regions_x + cx);
                     if (++cx > x1) { cx = x0; ++cy; }
                 }
             }
@@ -1056,7 +1066,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
             const float4 e0 = s_e[0][lo], e1 = s_e[1][lo], e2 = s_e[2][lo];
             if (cell_pass(e0, e1, e2, rx, ry)) {
-                const uint32_t r = ry * bins.regions_x + rx;
+                const uint32_t r = slot_of(bins, ry * bins.regions_x + rx);
                 place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u), i0 + s_big[lo]);
             }
         }
@@ -1269,6 +1279,8 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint64_t t_start = block_start_stamp();
     const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
     const uint32_t slot = g / kWavesPerRegion;
+    // count and region are independent loads (lists are by slot)
+    const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
     const uint32_t region = wave_uniform(bins.order ? bins.order[slot] : slot);
     const uint32_t tile0 = (g % kWavesPerRegion) * TPW;
     const uint32_t rx0 = (region % bins.regions_x) * kRegion;
@@ -1276,13 +1288,12 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     WaveStats ws = {};
     uint32_t n_cand = 0;
     if (rx0 + (tile0 & 3u) * 8u < p.width && ry0 + (tile0 >> 2) * 8u < p.row_end) {   // wave-uniform
-        const uint32_t n_local = wave_uniform(bins.counts[(size_t)region * kCounterStride]);
         if (n_local > bins.cap) {   // the region's list overflowed: whole mesh (exact, slower)
             n_cand = p.num_triangles;
             render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
                                    [](uint32_t k) { return k; }, ws);
         } else {
-            const uint32_t* __restrict__ local = bins.list + (size_t)region * bins.cap;
+            const uint32_t* __restrict__ local = bins.list + (size_t)slot * bins.cap;
             const uint32_t* __restrict__ glob = bins.global_list;
             n_cand = n_local + wave_uniform(bs->global_count);
             render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
@@ -1338,6 +1349,7 @@ __global__ void k_probe_math(int op, const float* __restrict__ in, float* __rest
     case 0: y = xrt_expf(x); break;
     case 1: y = sqrtf(x); break;
     case 2: y = inv_det_of(x); break;
+    case 4: y = rcp_newton_exact_for(x) ? rcp_newton(x) : inv_det_of(x); break;   // inv_det_fast per lane
     default: y = (float)lut_u8(x); break;
     }
     outp[i] = y;

@@ -299,6 +299,7 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
         return e ? std::atoi(e) : XRT_DEFAULT_ORDER;
     }();
     bins.order = nullptr;
+    bins.rank = nullptr;
     if (mode == 0) return XRT_OK;
     if (ctx->order_rx != rx || ctx->order_ry != ry || !ctx->d_order) {
         const size_t n = (size_t)rx * ry;
@@ -309,14 +310,17 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
             const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
             return ax * ax + ay * ay < bx * bx + by * by;
         });
+        order.resize(2 * n);                     // [slot -> region | region -> slot]
+        for (size_t k = 0; k < n; ++k) order[n + order[k]] = (uint32_t)k;
         XRT_HIP(ctx, hipDeviceSynchronize());   // the previous order may be in use
-        int rc = ensure(ctx, ctx->d_order, ctx->order_cap, n);
+        int rc = ensure(ctx, ctx->d_order, ctx->order_cap, 2 * n);
         if (rc) return rc;
-        XRT_HIP(ctx, hipMemcpy(ctx->d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        XRT_HIP(ctx, hipMemcpy(ctx->d_order, order.data(), 2 * n * sizeof(uint32_t), hipMemcpyHostToDevice));
         ctx->order_rx = rx;
         ctx->order_ry = ry;
     }
     bins.order = ctx->d_order;
+    bins.rank = ctx->d_order + (size_t)rx * ry;
     return XRT_OK;
 }
 
@@ -664,7 +668,8 @@ int xrt_set_kernel(xrt_context* ctx, int kernel)
 int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
-    if (capacity > (uint32_t)kMaxHits) return fail(ctx, XRT_ERR_ARGUMENT, "capacity > 16");
+    if (capacity > (uint32_t)kMaxHits)
+        return fail(ctx, XRT_ERR_ARGUMENT, "capacity > " + std::to_string(kMaxHits));
     ctx->hit_capacity = capacity ? capacity : (uint32_t)kMaxHits;
     return XRT_OK;
 }
@@ -849,7 +854,7 @@ int xrt_probe_intersect(xrt_context* ctx, const float* rays, const float* tris, 
 int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* outp, uint64_t n)
 {
     if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
-    if (op < XRT_PROBE_EXPF || op > XRT_PROBE_LUT_U8) return fail(ctx, XRT_ERR_ARGUMENT, "bad op");
+    if (op < XRT_PROBE_EXPF || op > XRT_PROBE_RCP_FAST) return fail(ctx, XRT_ERR_ARGUMENT, "bad op");
     if (n == 0) return XRT_OK;
     if (!in || !outp) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
     XRT_HIP(ctx, hipSetDevice(ctx->device));

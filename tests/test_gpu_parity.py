@@ -92,6 +92,36 @@ def test_probe_reciprocal_matches_double_division(ctx):
             assert same.all(), xc[~same][:8]
 
 
+@pytest.mark.parametrize("op", [_abi.XRT_PROBE_RCP, _abi.XRT_PROBE_RCP_FAST])
+def test_probe_reciprocal_every_exponent(ctx, op):
+    # every biased exponent x 2^16 mantissas (both signs), incl. the ends of
+    # the short sequence's range (2^-126 and 2^126) and the mantissa extremes
+    rng = np.random.default_rng(20250302)
+    man = np.concatenate([np.arange(64, dtype=np.uint32), (1 << 23) - 1 - np.arange(64, dtype=np.uint32),
+                          rng.integers(0, 1 << 23, (1 << 16) - 128, dtype=np.uint32)])
+    exps = np.arange(256, dtype=np.uint32)
+    x = ((exps[:, None] << 23) | man[None, :]).ravel()
+    x = np.concatenate([x, x | np.uint32(0x80000000)]).view(np.float32)
+    got = ctx.probe_math(op, x)
+    with np.errstate(divide="ignore", over="ignore"):
+        want = (np.float32(1.0) / x).astype(np.float32)
+    same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), x[~same][:8]
+
+
+def test_probe_fast_reciprocal_sweep(ctx):
+    # the culled tests' reciprocal on the stride-61 sweep of all 2^32 patterns
+    sweep = np.arange(0, 1 << 32, 61, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    for x in (special_floats(), sweep):
+        for c in range(0, x.size, 1 << 25):
+            xc = x[c:c + (1 << 25)]
+            got = ctx.probe_math(_abi.XRT_PROBE_RCP_FAST, xc)
+            with np.errstate(divide="ignore", over="ignore"):
+                want = (np.float32(1.0) / xc).astype(np.float32)
+            same = (bits(got) == bits(want)) | (np.isnan(got) & np.isnan(want))
+            assert same.all(), xc[~same][:8]
+
+
 def test_probe_lut_sweep(ctx):
     # every 13th f32 in [0, 80] against Image.inl:195-211's formula in f64
     # (round half away from zero == floor(x + 0.5) here, exactly)
@@ -195,6 +225,9 @@ def test_overflow_path_exact(ctx, dragon, kernel):
         assert_same(got, ref, f"{KNAME[kernel]} cap={cap}")
 
 
+MAX_HITS = 12  # the register hit list (XRT_MAX_HITS); rays past it take the exact fix-up
+
+
 def plane_stack(n, spacing=0.01):
     """n parallel unit squares (2 triangles each) facing the detector: every ray
     through the square hits each plane (twice on the shared diagonal)."""
@@ -220,8 +253,8 @@ def test_deep_stack_overflow(ctx, kernel, planes, size):
     cam = oracle.camera_for_mesh(soup, size, size)
     ref = oracle.render_rows(soup, cam, size, size)
     got = render(ctx, soup, size, size, kernel)
-    assert int(ref[3].max()) > 16
-    assert got[3].overflow_rays == int(np.count_nonzero(ref[3] > 16))
+    assert int(ref[3].max()) > MAX_HITS
+    assert got[3].overflow_rays == int(np.count_nonzero(ref[3] > MAX_HITS))
     assert_same(got, ref, f"{KNAME[kernel]} {planes} planes")
 
 
