@@ -63,7 +63,8 @@ typedef enum xrt_kernel {
                                footprint; per 8x8 ray tile the survivors of a relaxed
                                edge-function test get the exact Moller-Trumbore test */
     XRT_KERNEL_BINNED = 3   /* as TILED, but footprints are binned to regions once per
-                               frame (count, scan, fill) instead of swept per region */
+                               frame (atomic slots in fixed-capacity region lists)
+                               instead of swept per region */
 } xrt_kernel;
 
 /*

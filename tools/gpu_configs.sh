@@ -12,6 +12,8 @@ timeout -k 10 120 $B --kernel binned --size 1024 1024 > $OUT/binned_1024.json 2>
  && timeout -k 10 120 $B --kernel binned --size 4096 4096 > $OUT/binned_4096.json 2> $OUT/binned_4096.err \
  && timeout -k 10 120 $B --kernel tiled --size 4096 4096 > $OUT/tiled_4096.json 2> $OUT/tiled_4096.err \
  && timeout -k 10 200 $B --kernel binned --size 8192 8192 --tile-mesh 7 --steps 5 --warmup 1 > $OUT/binned_1m_8192.json 2> $OUT/binned_1m_8192.err \
+ && timeout -k 10 120 $B --kernel tiled --size 2048 2048 > $OUT/tiled_2048.json 2> $OUT/tiled_2048.err \
+ && timeout -k 10 120 $B --kernel brute --size 2048 2048 --steps 3 --warmup 1 > $OUT/brute_2048.json 2> $OUT/brute_2048.err \
  && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_binned -o run -- python3 bench.py --no-cpu-baseline --kernel binned > $OUT/prof_binned.json 2> $OUT/prof_binned.err
 rc=$?
 for f in $OUT/*.json; do python3 -c "
