@@ -48,7 +48,8 @@
 #define XRT_PRE_REJECT 0     // culled tests: wave-wide division-free reject before the exact test (A/B: slower, off)
 #endif
 #ifndef XRT_FAST_RCP
-#define XRT_FAST_RCP 0    // culled tests: rcp + Newton step for 1/det where exact (A/B: slower, off)
+#define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
+                          // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
 #ifndef XRT_ABLATION
 #define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
@@ -199,12 +200,8 @@ __device__ __forceinline__ bool rcp_newton_exact_for(float d)
 // on every lane either way.
 __device__ __forceinline__ float inv_det_fast(float det)
 {
-#if XRT_FAST_RCP
     if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) return inv_det_of(det);
     return rcp_newton(det);
-#else
-    return inv_det_of(det);
-#endif
 }
 
 // Branch-free Ray::intersect for the culled kernels, whose survivors almost
@@ -329,7 +326,7 @@ __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1
 {
     float det, a, b;
     mt_numerators(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tvx, tvy, tvz, qvx, qvy, qvz, det, a, b);
-    return mt_finish_inv(det, inv_det_fast(det), a, b, tnum, hit);   // Ray.cxx:99
+    return mt_finish_inv(det, XRT_FAST_RCP == 1 ? inv_det_fast(det) : inv_det_of(det), a, b, tnum, hit);   // Ray.cxx:99
 }
 
 // ---------------------------------------------------------------------------

@@ -1126,6 +1126,32 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
         const float t1 = mt_finish(det1, a1, b1, tn1, h1);
         hl.push_if(h1, t1);
     }
+#elif XRT_FAST_RCP == 2
+    // Both numerators, ONE wave-uniform range check for the pair, then the
+    // short reciprocal for both (or the IEEE division for both), with no other
+    // control flow: the two tests interleave in one basic block.  A lone
+    // survivor is tested twice (j1 == j0) and its second result dropped --
+    // cheaper than the branch (A/B: a `two` branch around the second test
+    // made the render 15 % slower).
+    const TriRec b = recs[j1];
+    float det0, a0, b0, det1, a1, b1;
+    mt_numerators(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz, a.qvx,
+                  a.qvy, a.qvz, det0, a0, b0);
+    mt_numerators(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz, b.qvx,
+                  b.qvy, b.qvz, det1, a1, b1);
+    float i0, i1;
+    if (__builtin_expect(__ballot(!(rcp_newton_exact_for(det0) && rcp_newton_exact_for(det1))) == 0ull, 1)) {
+        i0 = rcp_newton(det0);
+        i1 = rcp_newton(det1);
+    } else {
+        i0 = inv_det_of(det0);
+        i1 = inv_det_of(det1);
+    }
+    bool h0, h1;
+    const float t0 = mt_finish_inv(det0, i0, a0, b0, a.tnum, h0);
+    const float t1 = mt_finish_inv(det1, i1, a1, b1, b.tnum, h1);
+    hl.push_if(h0, t0);
+    hl.push_if(two && h1, t1);
 #else
     bool h0, h1 = false;
     float t1 = 0.0f;
@@ -1209,16 +1235,15 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
         }
         if (ablation(p) & kAblateExact) continue;
         while (m) {
+            // the next two survivors, selected without a branch (a lone one
+            // is paired with itself; test_record_pair drops the copy)
             const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k0);
-            uint32_t j1 = j0;
             const bool two = m != 0ull;
-            if (two) {
-                const uint32_t k1 = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1ull;
-                j1 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k1);
-            }
+            const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m | (1ull << 63)) : k0;
+            m &= m - 1ull;                        // no-op once m == 0
+            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k0);
+            const uint32_t j1 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k1);
             test_record_pair(recs, j0, j1, two, dx, dy, dz, hl);
         }
     }
