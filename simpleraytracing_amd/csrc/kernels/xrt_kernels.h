@@ -471,11 +471,14 @@ __device__ __forceinline__ float edge_max(float4 e, float xc, float yc, float hx
     return (e.x * xc + e.y * yc) + (e.z + (fabsf(e.x) * hx + fabsf(e.y) * hy));
 }
 
+// All three edges evaluated, combined with `&` (not `&&`): a short-circuit
+// lets the compiler sink each edge's load behind the previous edge's compare,
+// three dependent memory round trips per candidate chunk instead of one.
 __device__ __forceinline__ bool edges_pass(float4 e0, float4 e1, float4 e2, float xc, float yc,
                                            float hx, float hy)
 {
-    return edge_max(e0, xc, yc, hx, hy) >= 0.0f && edge_max(e1, xc, yc, hx, hy) >= 0.0f &&
-           edge_max(e2, xc, yc, hx, hy) >= 0.0f;
+    return (edge_max(e0, xc, yc, hx, hy) >= 0.0f) & (edge_max(e1, xc, yc, hx, hy) >= 0.0f) &
+           (edge_max(e2, xc, yc, hx, hy) >= 0.0f);
 }
 
 __device__ __forceinline__ bool edge_pass(const float4* __restrict__ culls, uint32_t T, uint32_t j,
