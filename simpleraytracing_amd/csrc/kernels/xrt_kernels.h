@@ -204,18 +204,31 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
     }
 }
 
+// Wave-wide sum / max of a u32 with DPP row shifts and row broadcasts (six
+// VALU ops, the total lands in lane 63) instead of six ds_bpermute rounds.
+// row_shr:n (0x110 + n) reads lane i-n of the same 16-lane row (0 past the
+// row start: bound_ctrl); row_bcast:15 (0x142) adds lane 15 of rows 0 / 2 to
+// rows 1 / 3; row_bcast:31 (0x143) adds lane 31 to rows 2 and 3.
+template <bool kMax>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x)
+{
+    auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : a + b; };
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 // One wave's statistics as one BlockStats record (no LDS, no barrier): the
 // lane sums are reduced across the wave and lane 0 stores the record.
 __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t candidates,
                                                  BlockStats* out, uint32_t index, uint64_t t_start = 0)
 {
-    uint32_t hits = ws.lane_hits, mx = ws.lane_max;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        hits += __shfl_xor(hits, off);
-        const uint32_t o = __shfl_xor(mx, off);
-        mx = mx > o ? mx : o;
-    }
+    const uint32_t hits = wave_reduce_u32<false>(ws.lane_hits);
+    const uint32_t mx = wave_reduce_u32<true>(ws.lane_max);
     if ((threadIdx.x & 63u) == 0u) {
         BlockStats b;
         b.rays = ws.rays;
