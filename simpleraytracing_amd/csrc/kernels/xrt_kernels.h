@@ -887,7 +887,7 @@ struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
     uint32_t* list;          // [n_regions * cap] triangle ids by slot
     uint32_t* global_list;   // [T]
-    const uint32_t* order;   // [n_regions] slot -> region, the render launch order (null: raster order)
+    const uint32_t* order;   // [n_regions] slot -> region (x | y << 16), the render launch order (null: raster)
     const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
     uint32_t cap;            // list capacity per region
     uint32_t regions_x, regions_y;
@@ -1322,10 +1322,18 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t slot = g / kWavesPerRegion;
     // count and region are independent loads (lists are by slot)
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
-    const uint32_t region = wave_uniform(bins.order ? bins.order[slot] : slot);
+    uint32_t reg_x, reg_y;
+    if (bins.order) {
+        const uint32_t xy = wave_uniform(bins.order[slot]);
+        reg_x = xy & 0xFFFFu;
+        reg_y = xy >> 16;
+    } else {
+        reg_x = slot % bins.regions_x;
+        reg_y = slot / bins.regions_x;
+    }
     const uint32_t tile0 = (g % kWavesPerRegion) * TPW;
-    const uint32_t rx0 = (region % bins.regions_x) * kRegion;
-    const uint32_t ry0 = p.row_begin + (region / bins.regions_x) * kRegion;
+    const uint32_t rx0 = reg_x * kRegion;
+    const uint32_t ry0 = p.row_begin + reg_y * kRegion;
     WaveStats ws = {};
     uint32_t n_cand = 0;
     if (rx0 + (tile0 & 3u) * 8u < p.width && ry0 + (tile0 >> 2) * 8u < p.row_end) {   // wave-uniform

@@ -300,7 +300,7 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
     }();
     bins.order = nullptr;
     bins.rank = nullptr;
-    if (mode == 0) return XRT_OK;
+    if (mode == 0 || rx > 0xFFFFu || ry > 0xFFFFu) return XRT_OK;   // raster order
     if (ctx->order_rx != rx || ctx->order_ry != ry || !ctx->d_order) {
         const size_t n = (size_t)rx * ry;
         std::vector<uint32_t> order(n);
@@ -310,8 +310,14 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
             const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
             return ax * ax + ay * ay < bx * bx + by * by;
         });
-        order.resize(2 * n);                     // [slot -> region | region -> slot]
-        for (size_t k = 0; k < n; ++k) order[n + order[k]] = (uint32_t)k;
+        // [slot -> region as (x | y << 16) | region -> slot]: the render takes its
+        // region's coordinates without an integer division
+        order.resize(2 * n);
+        for (size_t k = 0; k < n; ++k) {
+            const uint32_t r = order[k];
+            order[n + r] = (uint32_t)k;
+            order[k] = (r % rx) | ((r / rx) << 16);
+        }
         XRT_HIP(ctx, hipDeviceSynchronize());   // the previous order may be in use
         int rc = ensure(ctx, ctx->d_order, ctx->order_cap, 2 * n);
         if (rc) return rc;
