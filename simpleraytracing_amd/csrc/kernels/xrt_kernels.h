@@ -484,6 +484,13 @@ __device__ __forceinline__ float edge_max(float4 e, float xc, float yc, float hx
     return (e.x * xc + e.y * yc) + (e.z + (fabsf(e.x) * hx + fabsf(e.y) * hy));
 }
 
+// Footprint box (xmin, xmax, ymin, ymax) against the pixel-centre rectangle
+// [x0, x1] x [y0, y1]; an unbounded or NaN box overlaps.
+__device__ __forceinline__ bool box_overlaps(float4 bb, float x0, float x1, float y0, float y1)
+{
+    return !((bb.y < x0) | (bb.x > x1) | (bb.w < y0) | (bb.z > y1));
+}
+
 // All three edges evaluated, combined with `&` (not `&&`): a short-circuit
 // lets the compiler sink each edge's load behind the previous edge's compare,
 // three dependent memory round trips per candidate chunk instead of one.
@@ -1188,7 +1195,7 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
 struct Cand {
     uint32_t j;
     bool valid;
-    float4 e0, e1, e2;
+    float4 bb, e0, e1, e2;
 };
 
 template <typename Fetch>
@@ -1200,6 +1207,7 @@ __device__ __forceinline__ Cand load_cand(const float4* __restrict__ culls, uint
     c.valid = k < n_cand;
     const uint32_t j = c.valid ? fetch(k) : 0u;
     c.j = j < T ? j : 0u;                         // (always) never read out of range
+    c.bb = culls[c.j];
     c.e0 = culls[(size_t)T + c.j];
     c.e1 = culls[2 * (size_t)T + c.j];
     c.e2 = culls[3 * (size_t)T + c.j];
@@ -1235,13 +1243,18 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
         Cand c;
         if (base == 0u) {       // the first chunk's ids were loaded once per wave; edges are cache-hot
             c = first;
+            c.bb = culls[c.j];
             c.e0 = culls[(size_t)T + c.j];
             c.e1 = culls[2 * (size_t)T + c.j];
             c.e2 = culls[3 * (size_t)T + c.j];
         } else {
             c = load_cand(culls, T, n_cand, base, fetch);
         }
-        const bool pass = c.valid && edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f);
+        // the tile rectangle against the footprint box and the three relaxed
+        // edges: with the box's axes this is the full separating-axis test of
+        // the loosened triangle against the tile's pixel centres
+        const bool pass = c.valid & edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f) &
+                          box_overlaps(c.bb, (float)tx0, (float)tx0 + 7.0f, (float)ty0, (float)ty0 + 7.0f);
         unsigned long long m = __ballot(pass);
         if (!m) continue;
         tests += (uint32_t)__popcll(m);
