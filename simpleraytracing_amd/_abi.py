@@ -28,6 +28,7 @@ XRT_PROBE_EXPF = 0
 XRT_PROBE_SQRTF = 1
 XRT_PROBE_RCP = 2
 XRT_PROBE_LUT_U8 = 3
+XRT_PROBE_RCP_FAST = 4
 
 _f = ctypes.c_float
 _fp = ctypes.POINTER(ctypes.c_float)
