@@ -1331,7 +1331,22 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 {
     constexpr uint32_t kWavesPerRegion = 16u / TPW;
     const uint64_t t_start = block_start_stamp();
+#if XRT_XCD_REMAP
+    // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
+    // each run of 8 regions, give XCD x all workgroups of region x, so a region's
+    // candidate list and triangle records are cached by one L2 instead of four.
+    // A bijection on full runs; the tail keeps the identity.
+    constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
+    constexpr uint32_t kRun = 8u * kBlocksPerRegion;
+    uint32_t blk = blockIdx.x;
+    if (blk < (gridDim.x / kRun) * kRun) {
+        const uint32_t within = blk % kRun;
+        blk = (blk - within) + (within & 7u) * kBlocksPerRegion + (within >> 3);
+    }
+    const uint32_t g = blk * kTileWaves + wave_in_block();                // wave of the grid
+#else
     const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
+#endif
     const uint32_t slot = g / kWavesPerRegion;
     // count and region are independent loads (lists are by slot)
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
