@@ -36,7 +36,7 @@
 #define XRT_WAVES_PER_EU 0   // >0: occupancy hint for the culled render kernels
 #endif
 #ifndef XRT_XCD_REMAP
-#define XRT_XCD_REMAP 1  // binned render: one XCD per region (A/B: render 55.1 -> 53.8 us)
+#define XRT_XCD_REMAP 1  // binned render: >0 = regions per XCD per run of 8 XCDs, all of a region on one XCD (A/B: render 55.1 -> 53.8 us); 0 off
 #endif
 #ifndef XRT_TILE_WAVES
 #define XRT_TILE_WAVES 4  // binned render: tile waves per workgroup

@@ -1337,11 +1337,12 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     // candidate list and triangle records are cached by one L2 instead of four.
     // A bijection on full runs; the tail keeps the identity.
     constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
-    constexpr uint32_t kRun = 8u * kBlocksPerRegion;
+    constexpr uint32_t kPerXcd = XRT_XCD_REMAP * kBlocksPerRegion;   // XRT_XCD_REMAP regions per XCD per run
+    constexpr uint32_t kRun = 8u * kPerXcd;
     uint32_t blk = blockIdx.x;
     if (blk < (gridDim.x / kRun) * kRun) {
         const uint32_t within = blk % kRun;
-        blk = (blk - within) + (within & 7u) * kBlocksPerRegion + (within >> 3);
+        blk = (blk - within) + (within & 7u) * kPerXcd + (within >> 3);
     }
     const uint32_t g = blk * kTileWaves + wave_in_block();                // wave of the grid
 #else
