@@ -107,6 +107,65 @@ def cpu_baseline(tris, W, H, budget_s, gpu_rows):
     }
 
 
+def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_s, launches):
+    """The dominant kernel's roofline (DESIGN.md "Measurement").
+
+    The culled render is bound by vector-instruction issue, not by HBM: the
+    top-level entry is its VALU issue rate -- SQ_INSTS_VALU per launch (rocprofv3
+    PMC, profiles/traffic.json) / the live mean launch duration -- against the
+    chip's issue peak (one wave64 VALU op per SIMD every 2 cycles).  Beside it
+    (flat hbm_* keys) the HBM rate on the bytes the culled algorithm must move
+    per launch (outputs, each candidate triangle's cull planes and record, the
+    region-list entries) and the counter-measured HBM bytes.  The brute-force
+    definition of SURVEY 8(d) (36 B per ray-triangle test) only gives the work
+    avoided by the cull, `work_avoided_x`."""
+    traffic = valu = None
+    try:
+        with open(args.traffic_json) as f:
+            tr = json.load(f).get(f"{kernel}:{workload}")
+        if tr:
+            traffic = tr.get("hbm_bytes_per_launch")
+            valu = tr.get("valu_wave_instr_per_launch")
+    except (OSError, ValueError):
+        pass
+    tests = stats.tile_tests * 64 if kernel != "brute" else rays_per_launch * T
+    if kernel == "brute":
+        alg_bytes = rays_per_launch * BYTES_OUT_PER_RAY + 64 * T
+    else:
+        # outputs + cull planes (4 float4) and TriRec (64 B) of every triangle
+        # + one u32 per region-list entry (tiled: the LDS list is built from the
+        # footprint boxes, 16 B per triangle per region swept)
+        alg_bytes = rays_per_launch * BYTES_OUT_PER_RAY + 128 * T + 4 * stats.candidates
+    hbm_rate = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+    r = {
+        "kernel": "k_render_" + kernel,
+        "avg_kernel_ms": avg_kernel_s * 1e3,
+        "launches": launches,
+        "traffic": traffic,
+        "hbm_bound": "hbm",
+        "hbm_achieved": hbm_rate,
+        "hbm_peak": HBM_PEAK_GBS,
+        "hbm_unit": "GB/s",
+        "hbm_frac": hbm_rate / HBM_PEAK_GBS,
+        "hbm_algorithmic_bytes_per_launch": alg_bytes,
+        "hbm_traffic_GBs": traffic / avg_kernel_s / 1e9 if traffic and avg_kernel_s > 0 else None,
+        "ray_triangle_tests_per_launch": tests,
+        "brute_force_tests_per_launch": rays_per_launch * T,
+        "brute_force_bytes_per_launch": rays_per_launch * (BYTES_PER_TEST * T + BYTES_OUT_PER_RAY),
+        "work_avoided_x": rays_per_launch * T / max(tests, 1),
+    }
+    if valu and avg_kernel_s > 0:
+        rate = valu / avg_kernel_s
+        r.update({"bound": "valu", "achieved": rate, "peak": VALU_PEAK_WAVE_INSTR_S,
+                  "unit": "wave-instr/s", "frac": rate / VALU_PEAK_WAVE_INSTR_S,
+                  "valu_wave_instr_per_launch": valu})
+    else:     # no PMC record for this workload: the HBM entry leads
+        r.update({"bound": "hbm", "achieved": hbm_rate, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": hbm_rate / HBM_PEAK_GBS})
+    assert r["frac"] <= 1.0 and r["hbm_frac"] <= 1.0, r
+    return r
+
+
 def main():
     args = parse()
     import numpy as np
@@ -220,30 +279,11 @@ def main():
         value = rays_total / elapsed_max / 1e6
         rays_per_launch = (r1 - r0) * W
         avg_kernel_s = kernel_ms / max(launches, 1) / 1e3
-        bytes_per_ray = BYTES_PER_TEST * T + BYTES_OUT_PER_RAY
-        achieved = rays_per_launch * bytes_per_ray / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
         result_kernel = {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel]
         workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
                                                          if args.tile_mesh > 1 else "") + f" {W}x{H}"
-        traffic = None
-        valu_instr = None
-        try:
-            with open(args.traffic_json) as f:
-                tr = json.load(f).get(f"{result_kernel}:{workload}")
-            if tr:
-                traffic = tr.get("hbm_bytes_per_launch")
-                valu_instr = tr.get("valu_wave_instr_per_launch")
-        except (OSError, ValueError):
-            pass
-        # The culled render is instruction-bound, not HBM-bound: its VALU issue
-        # rate (PMC instruction count per launch / live mean duration) against
-        # the chip's issue peak (a wave64 VALU op every 2 cycles per SIMD).
-        compute = None
-        if valu_instr and avg_kernel_s > 0:
-            rate = valu_instr / avg_kernel_s
-            compute = {"bound": "valu", "achieved": rate, "peak": VALU_PEAK_WAVE_INSTR_S,
-                       "unit": "wave-instr/s", "frac": rate / VALU_PEAK_WAVE_INSTR_S,
-                       "valu_wave_instr_per_launch": valu_instr}
+        roofline = make_roofline(args, result_kernel, workload, stats, T, rays_per_launch, avg_kernel_s,
+                                 launches)
         result = {
             "metric": "Mrays/s (dragon.ply render, whole job)",
             "value": value,
@@ -268,19 +308,7 @@ def main():
                 "parallelism": (f"row strips x{world}, RCCL gather to rank 0" if strips
                                 else f"one frame per rank x{world} (weak)"),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "algorithmic_bytes_per_ray": bytes_per_ray,
-                "kernel": "k_render_" + {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel],
-                "avg_kernel_ms": avg_kernel_s * 1e3,
-                "launches": launches,
-                "compute": compute,
-            },
+            "roofline": roofline,
             "render_stats": {
                 "hit_rays": stats.hit_rays, "odd_rays": stats.odd_rays, "max_hits": stats.max_hits,
                 "overflow_rays": stats.overflow_rays,

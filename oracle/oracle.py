@@ -67,7 +67,10 @@ def ref_lib():
         path = os.path.join(HERE, "_ref", "libxrt_ref.so")
         if not os.path.exists(path):
             return None
-        R = ctypes.CDLL(path)
+        # RTLD_DEEPBIND: the reference's classes (TriangleMesh, Vec3, ...) bind
+        # to their own definitions, not to the same-named drop-in classes of
+        # libxrt_host.so when that is already loaded RTLD_GLOBAL.
+        R = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_DEEPBIND)
         R.ref_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
         R.ref_mesh_bbox.argtypes = [_F, ctypes.c_uint64, _F, _F]
         R.ref_camera.argtypes = [_F, _F, ctypes.c_uint32, ctypes.c_uint32, _F]

@@ -461,9 +461,27 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     return (float)y;
 }
 
+__host__ __device__ __forceinline__ float xrt_f32_from_bits(uint32_t u)
+{
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+// NaN path lengths.  The only NaN the reference's pair sum can produce is
+// inf - inf (two t = +inf "hits", which Ray.cxx records when 1/det overflows,
+// DESIGN.md "Tile cull" step 0); x86 SSE returns its default NaN for it
+// (0xFFC00000) and every later add propagates that operand.  The device's NaN
+// encodings differ, so the kernels store the x86 bits explicitly.
+constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
+// shade() of that NaN on x86: (double) and * 0.1 keep it, the negation in
+// -(0.3971f * cm) flips its sign, expf(x) returns x + x and 80 * x keeps it.
+constexpr uint32_t kX86ShadeNaN = 0x7FC00000u;
+
 // Beer-Lambert shade, main.cxx:725 and :739.
 __host__ __device__ __forceinline__ float shade(float distance)
 {
+    if (distance != distance) return xrt_f32_from_bits(kX86ShadeNaN);
     float cm = (float)((double)distance * 0.1);
     return 80.000f * xrt_expf(-(0.3971f * cm));
 }

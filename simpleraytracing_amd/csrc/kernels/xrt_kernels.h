@@ -39,7 +39,22 @@ struct CullParams {
     double dmax;      // upper bound of |D| (unnormalised ray direction) over the image
     double mag;       // upper bound of the magnitudes summed while forming D
     double width, height;
+    int dir_grid;     // every nonzero component of every ray direction of the image is a
+                      // multiple of 2^dir_grid (DESIGN.md "Tile cull", step 0)
+    int pad;
 };
+
+// Grid exponent of a float: a nonzero x is a multiple of 2^grid_exp(x) (its
+// ulp; 2^-149 for denormals).  Zero lies on every grid (kNoGrid).
+constexpr int kNoGrid = 1000;
+__host__ __device__ __forceinline__ int grid_exp(float x)
+{
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    if ((u & 0x7FFFFFFFu) == 0u) return kNoGrid;
+    const int e = (int)((u >> 23) & 0xFFu);
+    return e == 0 ? -149 : e - 150;
+}
 
 // Per-workgroup (BINNED: per-wave) statistics, written with plain stores, one
 // record each, and summed on the host by xrt_read_stats: same-address global
@@ -412,6 +427,10 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         }
     }
     if (!active) return;
+    if (distance != distance) {                       // inf - inf: x86's default NaN (xrt_device.h)
+        distance = xrt_f32_from_bits(kX86DefaultNaN);
+        lval = distance;
+    }
     size_t o = (size_t)(row - p.row_begin) * p.width + col;
     if (ablation(p) & (kAblateStores | kAblateShade)) {
         if (!(ablation(p) & kAblateStores)) {
@@ -775,6 +794,22 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
                 l1tv > 0x1p-60 && l1tv < 0x1p60;
     if (!sane) {
         return c;
+    }
+    // Step 0: every nonzero intermediate of Ray::intersect must be a normal
+    // float, so that each rounding is relative (the bounds below) and
+    // |det_f| >= 2^-126 keeps 1/det finite.  The terms are multiples of the
+    // products of their operands' grids (a rounded sum or product of
+    // multiples of 2^k is a multiple of 2^k), so a nonzero one is at least
+    // 2^(sum of grids).  Triangles this cannot prove for (geometry at the
+    // 1e-20 scale, where the reference records t = +inf "hits" through
+    // 1/det overflowing) are never culled.
+    {
+        auto gmin3 = [](float x, float y, float z) { return min(grid_exp(x), min(grid_exp(y), grid_exp(z))); };
+        const int g1 = gmin3(r.e1x, r.e1y, r.e1z), g2 = gmin3(r.e2x, r.e2y, r.e2z);
+        const int gt = gmin3(r.tvx, r.tvy, r.tvz), gd = cp.dir_grid;
+        const int lowest = min(min(gd + g2, g1 + gd + g2), min(min(gt + gd + g2, gt + g1),
+                                                              min(gd + gt + g1, g2 + gt + g1)));
+        if (lowest < -126) return c;
     }
     double s = r.tnum > 0.0f ? 1.0 : -1.0;
 
@@ -1330,6 +1365,8 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     BinBuffers bins, const BinState* __restrict__ bs)
 {
     constexpr uint32_t kWavesPerRegion = 16u / TPW;
+    static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
+                  "a workgroup's waves render tiles of one region");
     const uint64_t t_start = block_start_stamp();
 #if XRT_XCD_REMAP
     // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within

@@ -118,7 +118,14 @@ struct xrt_context {
         xrt_camera cam;
         uint32_t row_begin, row_end;
         uint64_t T, gen;
+        // field by field (the struct has padding; the camera's floats by bits)
+        bool same(const BinKey& o) const
+        {
+            return std::memcmp(&cam, &o.cam, sizeof cam) == 0 && row_begin == o.row_begin &&
+                   row_end == o.row_end && T == o.T && gen == o.gen;
+        }
     } bin_key = {};
+    static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
     int last_kernel = XRT_KERNEL_BINNED;
     uint32_t hit_capacity = kMaxHits;
@@ -216,6 +223,37 @@ RenderParams make_params(const xrt_camera& c, uint32_t row_begin, uint32_t row_e
     return p;
 }
 
+// Grid exponent shared by every float of magnitude >= m > 0 (their ulps are
+// at least 2^(floor(log2 m) - 23); 2^-149 at worst).
+inline int grid_floor(double m)
+{
+    if (!(m > 0.0) || !std::isfinite(m)) return -149;
+    return std::max(std::ilogb(m) - 23, -149);
+}
+
+// A grid 2^g such that every nonzero component of every ray direction of the
+// image (make_ray: main.cxx:652-661 and Ray.inl:80-84) is a multiple of it.
+// X_k = ((detector_k + up_k v) + right_k u) - origin_k is a rounded sum of
+// floats on the grids of detector_k, origin_k and the products up_k v,
+// right_k u, where every nonzero pixel offset is >= spacing / 2 (0.5 + row -
+// H/2.0 is a nonzero half-integer or integer); so a nonzero |X_k| is >= 2^gX.
+// The two normalisations divide by |X| <= dmax and by ~1, so a nonzero
+// component is >= 2^gX / (1.001 dmax), and its grid follows.
+int direction_grid(const xrt_camera& c, double dmax)
+{
+    const double ps = std::fabs((double)c.pixel_spacing);
+    const int goff = ps > 0.0 ? grid_floor(0.5 * ps * (1.0 - 0x1p-23)) : kNoGrid;
+    int g = kNoGrid;
+    for (int k = 0; k < 3; ++k) {
+        int gx = std::min(grid_exp(c.detector[k]), grid_exp(c.origin[k]));
+        if (c.up[k] != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(c.up[k]) + goff, -149));
+        if (c.right[k] != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(c.right[k]) + goff, -149));
+        if (gx == kNoGrid) continue;                       // X_k is 0 at every pixel
+        g = std::min(g, grid_floor(std::ldexp(1.0, gx) / (1.001 * dmax)));
+    }
+    return g;
+}
+
 // Bounds used by the cull derivation (DESIGN.md "Tile cull"): over every pixel
 // of the image, |D| <= dmax and the terms summed into D are <= mag.
 CullParams make_cull_params(const xrt_camera& c)
@@ -235,6 +273,8 @@ CullParams make_cull_params(const xrt_camera& c)
     cp.mag = mag;
     cp.width = c.width;
     cp.height = c.height;
+    cp.dir_grid = direction_grid(c, cp.dmax);
+    cp.pad = 0;
     return cp;
 }
 
@@ -349,7 +389,9 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
                        : sweep > kAutoSweep          ? XRT_KERNEL_BINNED
                                                      : XRT_KERNEL_TILED;
     const bool culled = kernel != XRT_KERNEL_BRUTE;
-    const bool binned = kernel == XRT_KERNEL_BINNED && rows > 0 && T > 0;
+    // k_prep packs a footprint's region rectangle in 16-bit fields: grids past
+    // 65535 regions a side render TILED (exact, slower).
+    const bool binned = kernel == XRT_KERNEL_BINNED && rows > 0 && T > 0 && rx <= 0xFFFFu && ry <= 0xFFFFu;
 
     // This frame's buffer set.  The render that last used it (kFrameSets
     // frames ago) must be complete before the set is prepared again.
@@ -417,7 +459,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
         key.row_end = row_end;
         key.T = T;
         key.gen = ctx->mesh_gen;
-        if (!ctx->bin_key_valid || std::memcmp(&key, &ctx->bin_key, sizeof key) != 0) {
+        if (!ctx->bin_key_valid || !key.same(ctx->bin_key)) {
             BinState h = {};
             XRT_HIP(ctx, hipMemcpyAsync(&h, bin_ctl, sizeof h, hipMemcpyDeviceToHost, ps));
             XRT_HIP(ctx, hipStreamSynchronize(ps));

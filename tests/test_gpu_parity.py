@@ -13,7 +13,7 @@ from simpleraytracing_amd import _abi
 from simpleraytracing_amd.scenes import tiled_mesh
 from oracle import oracle
 from conftest import DRAGON, GOLDEN, ROOT, bits
-from test_oracle import kat_vectors
+from kat import kat_vectors
 
 pytestmark = pytest.mark.gpu
 KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED]
@@ -301,6 +301,96 @@ def test_custom_camera_triangles_around_source(ctx, kernel):
     got = ctx.render_rows(cam)
     ref = oracle.render_rows(soup, cam13(cam), 64, 48)
     assert_same(got, ref, KNAME[kernel])
+
+
+def corner_soup():
+    """Triangles with 1e-20 edges one unit in front of the source, on the image's
+    centre column (odd W: the ray direction's y component is exactly 0 there):
+    det is a nonzero denormal, 1/det overflows to inf, a = u * det is exactly
+    0, so Ray.cxx:99-122 computes u = 0 * inf = NaN (passes both u tests),
+    v = +inf, u + v = NaN (passes) and t = +inf > 1e-7: the reference records
+    a hit at infinity for rays nowhere near the triangle.  The frame triangles
+    fix a bbox symmetric about y = 0 and z = 0 (the source's y and z)."""
+    tris = [[40, -10, -10, 40, 10, -10, 40, 10, 10], [60, -10, -10, 60, 10, 10, 60, -10, 10]]
+    for x0, sz in [(45, 1), (47, -1), (50, 1), (52, -1), (55, 1)]:
+        tris.append([x0, 0, 0, x0, 1e-20, 0, x0, 0, sz * 1e-20])
+        tris.append([x0, 0, 0, x0, 0, sz * 1e-20, x0, 1e-20, 0])
+    return np.array(tris, np.float32)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_infinite_hit_corner(ctx, kernel):
+    """The cull's former non-conservative corner (DESIGN.md "Tile cull", step 0):
+    t = +inf hits, inf - inf = NaN path lengths (x86's default NaN bits) --
+    every kernel equal to the oracle bit for bit."""
+    soup = corner_soup()
+    W, H = 33, 31
+    cam = oracle.camera_for_mesh(soup, W, H)
+    ref = oracle.render_rows(soup, cam, W, H)
+    assert np.isnan(ref[1]).sum() > 0 and ref[3].reshape(H, W)[:, W // 2].max() > 2
+    got = render(ctx, soup, W, H, kernel)
+    assert_same(got, ref, f"{KNAME[kernel]} corner")
+
+
+def strip_boundary_rows(H, n=8):
+    """SURVEY.md 8(c)'s fixture rows: 0, H/n*k - 1, H/n*k, H/2, H - 1."""
+    rows = {0, H // 2, H - 1}
+    for k in range(1, n):
+        rows |= {H // n * k - 1, H // n * k}
+    return sorted(rows)
+
+
+def test_dragon_1024_full_frame(ctx, dragon):
+    """BASELINE configs[1] (dragon 1024^2, one GPU): binned == brute over the whole
+    frame, strip-boundary rows vs the oracle, SURVEY facts as properties."""
+    W = H = 1024
+    a = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED)
+    b = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BRUTE)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    assert (a[3].hit_rays, a[3].odd_rays, a[3].max_hits) == (b[3].hit_rays, b[3].odd_rays, b[3].max_hits)
+    rows = strip_boundary_rows(H)
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    ref = oracle.render_row_list(dragon, cam, W, H, rows)
+    for plane, want in zip(a[:3], ref[:3]):
+        assert np.array_equal(bits(plane.reshape(H, W)[rows].ravel()), bits(want))
+    miss = np.isinf(a[1])
+    assert np.all(a[0][miss] == np.float32(80.0)) and np.all(a[2][miss] == 255)
+    assert np.all(a[1][~miss] >= 0) and np.all(a[0] <= np.float32(80.0)) and np.all(a[0] > 0)
+
+
+def test_tiled_mesh_8192_strip_rows(ctx, dragon):
+    """BASELINE configs[4] at full size: the 1,120,434-triangle tiled dragon at
+    8192^2.  The binned frame, rendered whole and as the 8 row strips of the
+    8-GPU split (rows_per = H/8), is bit-equal on every strip-boundary row to
+    the literal brute-force kernel, and to the CPU oracle on sampled columns."""
+    big = tiled_mesh(dragon, 7)
+    W = H = 8192
+    ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+    ctx.upload_mesh(big)
+    cam = xrt.camera_for_mesh(big, W, H)
+    full = ctx.render_rows(cam, lbuffer=True, u8=True)
+    assert full[3].overflow_rays == 0
+    rows = strip_boundary_rows(H)
+    for g in range(8):                                   # the 8 strips of the 8-GPU split
+        r0, r1 = g * H // 8, (g + 1) * H // 8
+        part = ctx.render_rows(cam, r0, r1)
+        for plane, whole in zip(part[:3], full[:3]):
+            assert np.array_equal(bits(plane), bits(whole[r0 * W:r1 * W])), (r0, r1)
+        del part
+    ctx.set_kernel(xrt.XRT_KERNEL_BRUTE)
+    for r in rows:
+        one = ctx.render_rows(cam, r, r + 1)
+        for plane, whole in zip(one[:3], full[:3]):
+            assert np.array_equal(bits(plane), bits(whole[r * W:(r + 1) * W])), r
+    cam13 = oracle.camera_for_mesh(big, W, H)
+    for r in rows:                                       # both image edges and the centre
+        for c0, c1 in [(0, 32), (W // 2 - 128, W // 2 + 128), (W - 32, W)]:
+            img, lb, u8, _, _ = oracle.render_span(big, cam13, W, H, r, c0, c1, threads=16)
+            o = r * W
+            assert np.array_equal(bits(img), bits(full[0][o + c0:o + c1])), (r, c0)
+            assert np.array_equal(bits(lb), bits(full[1][o + c0:o + c1])), (r, c0)
+            assert np.array_equal(u8, full[2][o + c0:o + c1]), (r, c0)
 
 
 def test_all_kernels_equal_2048(ctx, dragon):

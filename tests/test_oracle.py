@@ -7,9 +7,17 @@ import pytest
 
 from oracle import oracle
 from conftest import DRAGON, GOLDEN, bits
+from kat import kat_vectors
 
-REF = oracle.ref_lib()
-needs_ref = pytest.mark.skipif(REF is None, reason="oracle/_ref not built (needs /root/reference)")
+
+@pytest.fixture(scope="module")
+def REF():
+    """The reference's own compiled classes (oracle/_ref), mapped only by the
+    CPU tests that use them; skipped where it has not been built."""
+    r = oracle.ref_lib()
+    if r is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    return r
 
 
 def test_dragon_facts(dragon):
@@ -33,8 +41,7 @@ def test_golden_128_text_byte_exact(dragon):
     assert odd == 0
 
 
-@needs_ref
-def test_camera_matches_reference_classes(dragon):
+def test_camera_matches_reference_classes(REF, dragon):
     lo, hi = oracle.bbox(dragon)
     lo2 = np.zeros(3, np.float32)
     hi2 = np.zeros(3, np.float32)
@@ -47,47 +54,7 @@ def test_camera_matches_reference_classes(dragon):
         assert np.array_equal(bits(c1), bits(c2)), (w, h)
 
 
-def kat_vectors(seed=20250302, n=65536):
-    """Seeded random + crafted (ray, triangle) pairs."""
-    rng = np.random.default_rng(seed)
-    rays = np.zeros((n, 6), np.float32)
-    tris = np.zeros((n, 9), np.float32)
-    # random triangles near the origin of a random ray aimed at them
-    tris[:] = rng.normal(0, 1, (n, 9)).astype(np.float32)
-    rays[:, :3] = rng.normal(0, 5, (n, 3)).astype(np.float32)
-    centre = tris.reshape(n, 3, 3).mean(axis=1)
-    jitter = rng.normal(0, 0.7, (n, 3)).astype(np.float32)
-    rays[:, 3:] = (centre + jitter - rays[:, :3]).astype(np.float32)
-    k = 0
-    # crafted: axis-aligned unit triangle, rays through vertices / edges / u+v = 1
-    base = np.array([0, 0, 0, 1, 0, 0, 0, 1, 0], np.float32)
-    for (u, v) in [(0, 0), (1, 0), (0, 1), (0.5, 0.5), (0.25, 0.75), (0, 0.5), (0.5, 0),
-                   (1e-8, 1e-8), (-1e-8, 0.5), (0.5, -1e-8), (0.5000001, 0.5), (0.3, 0.7000001)]:
-        tris[k] = base
-        rays[k] = [u, v, 5, 0, 0, -1]
-        k += 1
-    # ray in the triangle's plane (det = +-0)
-    tris[k] = base; rays[k] = [-1, 0.25, 0, 1, 0, 0]; k += 1
-    tris[k] = base; rays[k] = [0.2, 0.2, 0, 0, 0, 1]; k += 1   # origin on the triangle (t = 0)
-    tris[k] = base; rays[k] = [0.2, 0.2, 1e-7, 0, 0, -1]; k += 1  # t ~ 1e-7
-    tris[k] = base; rays[k] = [0.2, 0.2, 1.1e-7, 0, 0, -1]; k += 1
-    tris[k] = base; rays[k] = [0.2, 0.2, -5, 0, 0, -1]; k += 1   # behind the origin
-    # tiny / denormal determinants
-    tiny = np.array([0, 0, 0, 1e-20, 0, 0, 0, 1e-20, 0], np.float32)
-    tris[k] = tiny; rays[k] = [1e-21, 1e-21, 1, 0, 0, -1]; k += 1
-    tris[k] = tiny * np.float32(1e-5); rays[k] = [1e-27, 1e-27, 1, 0, 0, -1]; k += 1
-    # degenerate triangles
-    tris[k] = [0, 0, 0, 1, 1, 1, 2, 2, 2]; rays[k] = [0.5, 0.5, 5, 0, 0, -1]; k += 1
-    tris[k] = [1, 1, 1, 1, 1, 1, 1, 1, 1]; rays[k] = [1, 1, 5, 0, 0, -1]; k += 1
-    # zero direction
-    tris[k] = base; rays[k] = [0.2, 0.2, 1, 0, 0, 0]; k += 1
-    # huge coordinates
-    tris[k] = base * np.float32(1e18); rays[k] = [1e17, 1e17, 1e19, 0, 0, -1]; k += 1
-    return rays, tris
-
-
-@needs_ref
-def test_intersect_kat_vs_reference():
+def test_intersect_kat_vs_reference(REF):
     rays, tris = kat_vectors()
     h1, t1 = oracle.intersect_batch(rays, tris)
     h2, t2 = oracle.ref_intersect_batch(rays, tris)
@@ -96,8 +63,7 @@ def test_intersect_kat_vs_reference():
     assert 0.05 < h1.mean() < 0.95
 
 
-@needs_ref
-def test_render_rows_vs_reference_classes(dragon):
+def test_render_rows_vs_reference_classes(REF, dragon):
     """Oracle renderLoop vs the same loop over the reference's compiled classes."""
     W = H = 48
     cam = oracle.camera_for_mesh(dragon, W, H)
