@@ -370,7 +370,9 @@ def test_tiled_mesh_8192_strip_rows(ctx, dragon):
     ctx.upload_mesh(big)
     cam = xrt.camera_for_mesh(big, W, H)
     full = ctx.render_rows(cam, lbuffer=True, u8=True)
-    assert full[3].overflow_rays == 0
+    # oblique rays at the frame's edges cross two neighbouring copies: more
+    # hits than the register list holds, resolved by the exact in-wave fix-up
+    assert full[3].max_hits > 12 and full[3].overflow_rays > 0
     rows = strip_boundary_rows(H)
     for g in range(8):                                   # the 8 strips of the 8-GPU split
         r0, r1 = g * H // 8, (g + 1) * H // 8
