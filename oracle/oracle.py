@@ -48,6 +48,10 @@ def lib():
         L.orc_render_span.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _F, _F, _U8,
                                       _I32, ctypes.c_int]
+        L.orc_render_row_list_span.restype = ctypes.c_int64
+        L.orc_render_row_list_span.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                               _U32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               _F, _F, _U8, _I32, ctypes.c_int]
         L.orc_hit_pairs.restype = ctypes.c_int64
         L.orc_hit_pairs.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32, _U32,
                                     ctypes.c_uint32, _U32, _U32, ctypes.c_uint64, ctypes.c_int]
@@ -149,6 +153,26 @@ def render_row_list(tris, cam13, width, height, rows, threads=None):
     odd = lib().orc_render_row_list(_fp(tris), len(tris), _fp(cam13), width, height,
                                     rows.ctypes.data_as(_U32), len(rows), _fp(img), _fp(lb),
                                     u8.ctypes.data_as(_U8), nh.ctypes.data_as(_I32), threads)
+    return img, lb, u8, nh, odd
+
+
+def render_row_list_span(tris, cam13, width, height, rows, col_begin, col_end, threads=None):
+    """Columns [col_begin, col_end) of each row in `rows`: (image, lbuffer, u8, nhits, odd),
+    row-major (len(rows), col_end - col_begin)."""
+    rows = np.ascontiguousarray(rows, np.uint32)
+    tris = np.ascontiguousarray(tris, np.float32)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    n = len(rows) * (col_end - col_begin)
+    img = np.empty(n, np.float32)
+    lb = np.empty(n, np.float32)
+    u8 = np.empty(n, np.uint8)
+    nh = np.empty(n, np.int32)
+    odd = lib().orc_render_row_list_span(_fp(tris), len(tris), _fp(cam13), width, height,
+                                         rows.ctypes.data_as(_U32), len(rows), col_begin, col_end,
+                                         _fp(img), _fp(lb), u8.ctypes.data_as(_U8),
+                                         nh.ctypes.data_as(_I32), threads or os.cpu_count() or 1)
+    if odd < 0:
+        raise ValueError("bad rows or span")
     return img, lb, u8, nh, odd
 
 

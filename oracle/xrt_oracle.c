@@ -611,6 +611,17 @@ int64_t orc_render_row_list(const float* tris, uint64_t ntris, const float cam[1
                        image_u8, nhits, nthreads);
 }
 
+/* Columns [col_begin, col_end) of a list of rows (sampled checks of huge frames). */
+int64_t orc_render_row_list_span(const float* tris, uint64_t ntris, const float cam[13],
+                                 uint32_t width, uint32_t height, const uint32_t* rows,
+                                 uint32_t nrows, uint32_t col_begin, uint32_t col_end,
+                                 float* image, float* lbuffer, uint8_t* image_u8,
+                                 int32_t* nhits, int nthreads)
+{
+    return render_list(tris, ntris, cam, width, height, rows, nrows, col_begin, col_end, image,
+                       lbuffer, image_u8, nhits, nthreads);
+}
+
 /* Columns [col_begin, col_end) of one row (bounded CPU timing samples). */
 int64_t orc_render_span(const float* tris, uint64_t ntris, const float cam[13], uint32_t width,
                         uint32_t height, uint32_t row, uint32_t col_begin, uint32_t col_end,
