@@ -44,8 +44,8 @@ struct CullParams {
     int pad;
 };
 
-// Grid exponent of a float: a nonzero x is a multiple of 2^grid_exp(x) (its
-// ulp; 2^-149 for denormals).  Zero lies on every grid (kNoGrid).
+// Grid exponent of a float: x is a multiple of 2^grid_exp(x), the weight of
+// its lowest set bit.  Zero lies on every grid (kNoGrid).
 constexpr int kNoGrid = 1000;
 __host__ __device__ __forceinline__ int grid_exp(float x)
 {
@@ -53,7 +53,8 @@ __host__ __device__ __forceinline__ int grid_exp(float x)
     __builtin_memcpy(&u, &x, 4);
     if ((u & 0x7FFFFFFFu) == 0u) return kNoGrid;
     const int e = (int)((u >> 23) & 0xFFu);
-    return e == 0 ? -149 : e - 150;
+    const uint32_t m = (u & 0x7FFFFFu) | (e ? 0x800000u : 0u);
+    return (e ? e - 150 : -149) + __builtin_ctz(m);
 }
 
 // Per-workgroup (BINNED: per-wave) statistics, written with plain stores, one
@@ -795,21 +796,20 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     if (!sane) {
         return c;
     }
-    // Step 0: every nonzero intermediate of Ray::intersect must be a normal
-    // float, so that each rounding is relative (the bounds below) and
-    // |det_f| >= 2^-126 keeps 1/det finite.  The terms are multiples of the
-    // products of their operands' grids (a rounded sum or product of
-    // multiples of 2^k is a multiple of 2^k), so a nonzero one is at least
-    // 2^(sum of grids).  Triangles this cannot prove for (geometry at the
-    // 1e-20 scale, where the reference records t = +inf "hits" through
-    // 1/det overflowing) are never culled.
+    // Step 0: 1/det must stay finite.  Where a nonzero |det_f| falls to
+    // 2^-128, (float)(1.0 / det) overflows and Ray.cxx records t = +inf
+    // "hits" (u = 0 * inf = NaN passes its tests) for rays nowhere near the
+    // triangle, which no footprint bounds.  det_f = e1 . RN(d x e2) is a
+    // rounded sum of products of multiples of 2^g1, 2^gd and 2^g2 (a rounded
+    // sum or product of multiples of 2^k is a multiple of 2^k), so a nonzero
+    // one is >= 2^(g1 + gd + g2).  Triangles this cannot bound above 2^-128
+    // (geometry at the 1e-20 scale) are never culled.  (Denormal
+    // intermediates elsewhere add absolute errors of 2^-150, far below the
+    // bounds B_k >= 2^-139 that the l1 ranges above guarantee.)
     {
         auto gmin3 = [](float x, float y, float z) { return min(grid_exp(x), min(grid_exp(y), grid_exp(z))); };
         const int g1 = gmin3(r.e1x, r.e1y, r.e1z), g2 = gmin3(r.e2x, r.e2y, r.e2z);
-        const int gt = gmin3(r.tvx, r.tvy, r.tvz), gd = cp.dir_grid;
-        const int lowest = min(min(gd + g2, g1 + gd + g2), min(min(gt + gd + g2, gt + g1),
-                                                              min(gd + gt + g1, g2 + gt + g1)));
-        if (lowest < -126) return c;
+        if (g1 + cp.dir_grid + g2 < -127) return c;
     }
     double s = r.tnum > 0.0f ? 1.0 : -1.0;
 

@@ -127,6 +127,9 @@ struct xrt_context {
     } bin_key = {};
     static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
+    xrt_camera cull_cam = {};          // camera of the cached cull parameters
+    CullParams cull = {};
+    bool cull_valid = false;
     int last_kernel = XRT_KERNEL_BINNED;
     uint32_t hit_capacity = kMaxHits;
     // XRT_HOST_PROFILE=1: host time per enqueue, split by wait (printed at destroy)
@@ -231,25 +234,54 @@ inline int grid_floor(double m)
     return std::max(std::ilogb(m) - 23, -149);
 }
 
+// The f32 pixel offset of make_ray (main.cxx:655-656).
+inline float pixel_offset(float spacing, uint32_t i, uint32_t n)
+{
+    return (float)((double)spacing * ((0.5 + (double)i) - (double)n / 2.0));
+}
+
+// Smallest nonzero |X_k| over the image, X_k = ((detector_k + up_k v) +
+// right_k u) - origin_k in f32 as make_ray forms it (main.cxx:659): exact over
+// the rows (right_k == 0) or the columns (up_k == 0) it varies with.  When it
+// varies with both, a grid bound: X_k is a rounded sum of multiples of the
+// grids of its terms, every nonzero offset being >= spacing / 2.  0 when X_k
+// is 0 at every pixel.
+double min_nonzero_x(const xrt_camera& c, int k)
+{
+    const float cu = c.up[k], cr = c.right[k], cc = c.detector[k], co = c.origin[k];
+    auto x_of = [&](float v, float u) { return ((cc + cu * v) + cr * u) - co; };
+    const uint32_t kMaxScan = 1u << 20;
+    double best = std::numeric_limits<double>::infinity();
+    auto take = [&](float x) {
+        if (x != 0.0f) best = std::min(best, (double)std::fabs(x));
+    };
+    if (cr == 0.0f && c.height <= kMaxScan) {
+        const float u0 = pixel_offset(c.pixel_spacing, 0, c.width);
+        for (uint32_t row = 0; row < c.height; ++row) take(x_of(pixel_offset(c.pixel_spacing, row, c.height), u0));
+    } else if (cu == 0.0f && c.width <= kMaxScan) {
+        const float v0 = pixel_offset(c.pixel_spacing, 0, c.height);
+        for (uint32_t col = 0; col < c.width; ++col) take(x_of(v0, pixel_offset(c.pixel_spacing, col, c.width)));
+    } else {
+        const double ps = std::fabs((double)c.pixel_spacing);
+        const int goff = ps > 0.0 ? grid_floor(0.5 * ps * (1.0 - 0x1p-23)) : kNoGrid;
+        int gx = std::min(grid_exp(cc), grid_exp(co));
+        if (cu != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(cu) + goff, -149));
+        if (cr != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(cr) + goff, -149));
+        if (gx != kNoGrid) best = std::ldexp(1.0, gx);
+    }
+    return std::isfinite(best) ? best : 0.0;
+}
+
 // A grid 2^g such that every nonzero component of every ray direction of the
-// image (make_ray: main.cxx:652-661 and Ray.inl:80-84) is a multiple of it.
-// X_k = ((detector_k + up_k v) + right_k u) - origin_k is a rounded sum of
-// floats on the grids of detector_k, origin_k and the products up_k v,
-// right_k u, where every nonzero pixel offset is >= spacing / 2 (0.5 + row -
-// H/2.0 is a nonzero half-integer or integer); so a nonzero |X_k| is >= 2^gX.
-// The two normalisations divide by |X| <= dmax and by ~1, so a nonzero
-// component is >= 2^gX / (1.001 dmax), and its grid follows.
+// image (make_ray: main.cxx:652-661 and Ray.inl:80-84) is a multiple of it:
+// the two normalisations divide X_k by |X| <= dmax and by ~1, so a nonzero
+// component is >= min|X_k| / (1.001 dmax), a float whose ulp is the grid.
 int direction_grid(const xrt_camera& c, double dmax)
 {
-    const double ps = std::fabs((double)c.pixel_spacing);
-    const int goff = ps > 0.0 ? grid_floor(0.5 * ps * (1.0 - 0x1p-23)) : kNoGrid;
     int g = kNoGrid;
     for (int k = 0; k < 3; ++k) {
-        int gx = std::min(grid_exp(c.detector[k]), grid_exp(c.origin[k]));
-        if (c.up[k] != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(c.up[k]) + goff, -149));
-        if (c.right[k] != 0.0f && goff != kNoGrid) gx = std::min(gx, std::max(grid_exp(c.right[k]) + goff, -149));
-        if (gx == kNoGrid) continue;                       // X_k is 0 at every pixel
-        g = std::min(g, grid_floor(std::ldexp(1.0, gx) / (1.001 * dmax)));
+        const double xmin = min_nonzero_x(c, k);
+        if (xmin > 0.0) g = std::min(g, grid_floor(xmin / (1.001 * dmax)));
     }
     return g;
 }
@@ -412,7 +444,12 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (culled && (rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
-    CullParams cp = make_cull_params(*cam);
+    if (!ctx->cull_valid || std::memcmp(&ctx->cull_cam, cam, sizeof *cam) != 0) {
+        ctx->cull = make_cull_params(*cam);      // a scan over the rows / columns: once per camera
+        ctx->cull_cam = *cam;
+        ctx->cull_valid = true;
+    }
+    const CullParams cp = ctx->cull;
     Outputs out;
     out.image = d_image;
     out.lbuffer = d_lbuffer;

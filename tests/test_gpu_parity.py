@@ -410,6 +410,8 @@ def test_all_kernels_equal_2048(ctx, dragon):
             assert np.array_equal(bits(x), bits(y)), KNAME[k]
     st = a[3]
     assert (st.hit_rays, st.odd_rays, st.max_hits) == (1365802, 24, 12)
+    # the cull is effective: ~75k region-list entries and ~3 exact tests per ray
+    assert st.candidates < 200000 and st.tile_tests * 64 < 5 * W * H, (st.candidates, st.tile_tests)
     rows = [0, 255, 256, 511, 512, 1023, 1024, 1535, 1536, 1792, 2047]
     cam = oracle.camera_for_mesh(dragon, W, H)
     ref = oracle.render_row_list(dragon, cam, W, H, rows)
