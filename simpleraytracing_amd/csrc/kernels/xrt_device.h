@@ -54,6 +54,9 @@
 #define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
                           // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
+#ifndef XRT_STAGED_PAIRS
+#define XRT_STAGED_PAIRS 0   // binned render: LDS-staged survivors tested two at a time (else one)
+#endif
 #ifndef XRT_ABLATION
 #define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
 #endif
@@ -138,14 +141,50 @@ constexpr int kMaxHits = XRT_MAX_HITS;
 // ---------------------------------------------------------------------------
 // Ray generation: src/main.cxx:652-661 and the Ray ctor, include/Ray.inl:74-85.
 // ---------------------------------------------------------------------------
+// :655-656  float * (0.5 + unsigned - unsigned / 2.0) in double, narrowed once.
+// A function of one pixel index: k_prep tabulates it per frame (pixel_offsets)
+// for the render kernels.
+__host__ __device__ __forceinline__ float pixel_offset(float spacing, uint32_t i, uint32_t n)
+{
+    return (float)((double)spacing * ((0.5 + (double)i) - (double)n / 2.0));
+}
+
+// The frame's pixel offsets: v_off of every image row, then u_off of every
+// column (H + W floats, written by k_prep next to the frame's RenderParams).
+struct PixelOffsets {
+    const float* __restrict__ v;   // [height]
+    const float* __restrict__ u;   // [width]
+};
+
 // P: RenderParams in any address space (kernel argument or constant memory).
+template <typename P>
+__device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
+                                         float& dx, float& dy, float& dz);
+
+template <typename P>
+__device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_off, float& dx,
+                                              float& dy, float& dz);
+
 template <typename P>
 __device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
                                          float& dx, float& dy, float& dz)
 {
-    // :655-656  float * (0.5 + unsigned - unsigned / 2.0) in double, narrowed once
-    float v_off = (float)((double)p.spacing * ((0.5 + (double)row) - (double)p.height / 2.0));
-    float u_off = (float)((double)p.spacing * ((0.5 + (double)col) - (double)p.width / 2.0));
+    make_ray_from(p, pixel_offset(p.spacing, row, p.height), pixel_offset(p.spacing, col, p.width), dx,
+                  dy, dz);
+}
+
+// The same ray with the offsets read from the frame's tables.
+template <typename P>
+__device__ __forceinline__ void make_ray(const P& p, const PixelOffsets& off, uint32_t row,
+                                         uint32_t col, float& dx, float& dy, float& dz)
+{
+    make_ray_from(p, off.v[row], off.u[col], dx, dy, dz);
+}
+
+template <typename P>
+__device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_off, float& dx,
+                                              float& dy, float& dz)
+{
     // :659  detector + up*v + right*u - origin  (Vec3 ops left to right, f32)
     float X = ((p.cx + p.ux * v_off) + p.rx * u_off) - p.ox;
     float Y = ((p.cy + p.uy * v_off) + p.ry * u_off) - p.oy;

@@ -78,7 +78,16 @@ struct Outputs {
     // a tile first needs its rays, instead of camera kernel arguments held in
     // SGPRs for the whole kernel.
     const __attribute__((address_space(4))) RenderParams* frame;
+    PixelOffsets off;          // the frame's pixel-offset tables (k_prep)
 };
+
+// A pixel inside the image for the offset tables (lanes of a partial tile
+// outside it compute a ray nobody stores).
+__device__ __forceinline__ void make_tile_ray(const RenderParams& p, const Outputs& out, uint32_t row,
+                                              uint32_t col, float& dx, float& dy, float& dz)
+{
+    make_ray(*out.frame, out.off, min(row, p.height - 1u), min(col, p.width - 1u), dx, dy, dz);
+}
 
 // Running counters of one wave: ballot counts (wave-uniform), per-lane hit sum
 // and maximum (reduced across the wave once, in store_block_stats).
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     const bool active = col < p.width && row < p.row_end;
 
     float dx, dy, dz;
-    make_ray(*out.frame, row, col, dx, dy, dz);
+    make_tile_ray(p, out, row, col, dx, dy, dz);
     HitList hl;
     hl.init();
     const uint32_t T = p.num_triangles;
@@ -635,7 +644,7 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
 
         float dx = 0.0f, dy = 0.0f, dz = 0.0f;
-        if (tile_live && !(ablation(p) & kAblateRayGen)) make_ray(*out.frame, row, col, dx, dy, dz);
+        if (tile_live && !(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
         else dx = 1.0f;
         HitList hl;
         hl.init();
@@ -925,9 +934,30 @@ constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back 
 // wave of slot s loads its count and list without first looking up which
 // region it renders (order[s], loaded alongside); k_prep maps region -> slot
 // through rank.
+// Region-list entry: the triangle's conservative footprint, copied into every
+// region list it joins, so a render wave reads its candidates with one
+// coalesced 64-B load per lane (no id -> footprint indirection).
+struct alignas(16) RegionEntry {
+    float4 e0;   // relaxed edge 0 (a, b, c); w = triangle id (bits)
+    float4 e1;   // relaxed edge 1
+    float4 e2;   // relaxed edge 2
+    float4 bb;   // footprint box (xmin, xmax, ymin, ymax)
+};
+static_assert(sizeof(RegionEntry) == 64, "RegionEntry must be 64 bytes");
+
+__device__ __forceinline__ RegionEntry make_entry(float4 e0, float4 e1, float4 e2, float4 bb, uint32_t tri)
+{
+    RegionEntry r;
+    r.e0 = make_float4(e0.x, e0.y, e0.z, __uint_as_float(tri));
+    r.e1 = e1;
+    r.e2 = e2;
+    r.bb = bb;
+    return r;
+}
+
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
-    uint32_t* list;          // [n_regions * cap] triangle ids by slot
+    RegionEntry* list;       // [n_regions * cap] entries by slot
     uint32_t* global_list;   // [T]
     const uint32_t* order;   // [n_regions] slot -> region (x | y << 16), the render launch order (null: raster)
     const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
@@ -991,7 +1021,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
                                               BinState* __restrict__ bs,
-                                              RenderParams* __restrict__ frame_out)
+                                              RenderParams* __restrict__ frame_out,
+                                              float* __restrict__ offsets_out)
 {
     // The preparation of frame N+1 shares the CUs with frame N's render (prep
     // stream): top wave priority keeps this latency-bound chain short.
@@ -999,6 +1030,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < T;
     if (i == 0 && frame_out) *frame_out = p;       // the render's make_ray reads it (Outputs::frame)
+    if (offsets_out) {                             // v_off of every row, then u_off of every column
+        if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
+        else if (i - p.height < p.width) offsets_out[i] = pixel_offset(p.spacing, i - p.height, p.width);
+    }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
     Footprint fp;
     if (valid) {
@@ -1028,7 +1063,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
     if (!bins.counts) return;                      // kernel-uniform
 
-    __shared__ float4 s_e[3][256];                 // relaxed edges (big triangles)
+    __shared__ float4 s_e[4][256];                 // relaxed edges and box (big triangles)
     __shared__ uint2 s_rect[256];                  // (x0 | x1 << 16, y0 | y1 << 16)
     __shared__ uint32_t s_big[256];                // big triangles (local index)
     __shared__ uint32_t s_cum[256];                // inclusive prefix of their cell counts
@@ -1046,9 +1081,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     if (tid == 0) s_max = 0u;
 
     uint32_t my_max = 0;                           // 1 + the largest slot this thread took
-    auto place = [&](uint32_t r, uint32_t slot, uint32_t tri) {
+    auto place = [&](uint32_t r, uint32_t slot, const RegionEntry& e) {
         my_max = max(my_max, slot + 1u);
-        if (slot < bins.cap) bins.list[(size_t)r * bins.cap + slot] = tri;
+        if (slot < bins.cap) bins.list[(size_t)r * bins.cap + slot] = e;
     };
     auto cell_pass = [&](float4 e0, float4 e1, float4 e2, uint32_t rx, uint32_t ry) {
         const float xc = (float)(rx * kRegion) + 15.5f;
@@ -1061,6 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     // entries.  (Batches keep k_prep within 64 VGPRs, so its waves fit the
     // holes a retiring render wave leaves while the previous frame renders.)
     if (has && !big) {
+        const RegionEntry entry = make_entry(fp.e0, fp.e1, fp.e2, fp.bbox, i);
         uint32_t cx = x0, cy = y0;
         for (uint32_t k0 = 0; k0 < cells; k0 += kSerialBatch) {
             uint32_t reg[kSerialBatch], slot[kSerialBatch];
@@ -1077,7 +1113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
 #pragma unroll
             for (uint32_t k = 0; k < kSerialBatch; ++k)
-                if (reg[k] != kEmpty) place(reg[k], slot[k], i);
+                if (reg[k] != kEmpty) place(reg[k], slot[k], entry);
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
@@ -1097,6 +1133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         s_e[0][bslot] = fp.e0;
         s_e[1][bslot] = fp.e1;
         s_e[2][bslot] = fp.e2;
+        s_e[3][bslot] = fp.bbox;
         s_rect[bslot] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
     }
     __syncthreads();
@@ -1125,7 +1162,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const float4 e0 = s_e[0][lo], e1 = s_e[1][lo], e2 = s_e[2][lo];
             if (cell_pass(e0, e1, e2, rx, ry)) {
                 const uint32_t r = slot_of(bins, ry * bins.regions_x + rx);
-                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u), i0 + s_big[lo]);
+                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u),
+                      make_entry(e0, e1, e2, s_e[3][lo], i0 + s_big[lo]));
             }
         }
     }
@@ -1142,61 +1180,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 
 // ---------------------------------------------------------------------------
 // k_render_binned: wave-per-tile render over the binned region lists.
-// Each wavefront owns one 8x8 ray tile and walks its region's candidate list
-// straight from global memory (no LDS staging, no barrier until the block's
-// statistics): one lane per candidate evaluates the three relaxed edges at
-// the tile rectangle, a ballot keeps the survivors, and every survivor's
-// record is a wave-uniform scalar load tested exactly for all 64 rays.  The
-// ray directions are generated only when the first survivor appears: a tile
-// without survivors stores the miss constants (80, +inf, 255) directly.
-// The four waves of a workgroup take four tiles of one region, regions in
-// the launch order of the binning scan (heaviest first).
+//
+// One wavefront owns one 8x8 ray tile of a 32x32 region.  Its candidates are
+// the region's list entries (64-B footprints, read directly: the first 64
+// speculatively, beside the count) followed by the global list (ids, read
+// through the SoA cull planes).  Per chunk of 64 candidates, one lane per
+// candidate tests the tile rectangle against the footprint box and the three
+// relaxed edges and a ballot keeps the survivors.  The survivors' triangle
+// records are gathered in ONE vector-load round trip into the wave's slice of
+// LDS, then read back as wave-uniform broadcasts and tested exactly for all
+// 64 rays, two at a time -- no dependent memory round trip per survivor.
+// Rays are generated when the first survivor appears (pixel offsets from the
+// frame's tables); a tile without survivors stores the miss constants.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs, uint32_t j0,
-                                                 uint32_t j1, bool two, float dx, float dy,
-                                                 float dz, HitList& hl)
+constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
+constexpr uint32_t kWavesPerRegion = 16u;               // one 8x8 tile per wave
+
+// A chunk of 64 candidates as seen by one wave: this lane's candidate.
+struct Cand {
+    uint32_t j;          // triangle id (always a valid index)
+    bool valid;
+    float4 e0, e1, e2, bb;
+};
+
+// Region-list entries [base, base + 64): direct 64-B loads; `bound` (the
+// wave-uniform list length or capacity) keeps the reads inside the list.
+__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t bound,
+                                             uint32_t n_valid, uint32_t base, uint32_t T)
 {
-    const TriRec a = recs[j0];
-#if XRT_PRE_REJECT
-    // Division-free numerators first; a triangle every lane provably rejects
-    // (mt_may_hit) skips the division and the hit-list insertion.
-    float det0, a0, b0, det1 = 0.0f, a1 = 0.0f, b1 = 0.0f, tn1 = 0.0f;
-    mt_numerators(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz, a.qvx,
-                  a.qvy, a.qvz, det0, a0, b0);
-    if (two) {
-        const TriRec b = recs[j1];
-        mt_numerators(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
-                      b.qvx, b.qvy, b.qvz, det1, a1, b1);
-        tn1 = b.tnum;
-    }
-    const bool live0 = __ballot(mt_may_hit(det0, a0, b0, a.tnum)) != 0ull;          // wave-uniform
-    const bool live1 = two && __ballot(mt_may_hit(det1, a1, b1, tn1)) != 0ull;
-    bool h0, h1;
-    if (live0 && live1) {
-        const float t0 = mt_finish(det0, a0, b0, a.tnum, h0);
-        const float t1 = mt_finish(det1, a1, b1, tn1, h1);
-        hl.push_if(h0, t0);
-        hl.push_if(h1, t1);
-    } else if (live0) {
-        const float t0 = mt_finish(det0, a0, b0, a.tnum, h0);
-        hl.push_if(h0, t0);
-    } else if (live1) {
-        const float t1 = mt_finish(det1, a1, b1, tn1, h1);
-        hl.push_if(h1, t1);
-    }
-#elif XRT_FAST_RCP == 2
-    // Both numerators, ONE wave-uniform range check for the pair, then the
-    // short reciprocal for both (or the IEEE division for both), with no other
-    // control flow: the two tests interleave in one basic block.  A lone
-    // survivor is tested twice (j1 == j0) and its second result dropped --
-    // cheaper than the branch (A/B: a `two` branch around the second test
-    // made the render 15 % slower).
-    const TriRec b = recs[j1];
-    float det0, a0, b0, det1, a1, b1;
-    mt_numerators(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy, a.tvz, a.qvx,
-                  a.qvy, a.qvz, det0, a0, b0);
-    mt_numerators(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz, b.qvx,
-                  b.qvy, b.qvz, det1, a1, b1);
+    Cand c;
+    const uint32_t k = base + (threadIdx.x & 63u);
+    c.valid = k < n_valid;
+    const RegionEntry* e = list + (k < bound ? k : 0u);
+    c.e0 = e->e0;
+    c.e1 = e->e1;
+    c.e2 = e->e2;
+    c.bb = e->bb;
+    const uint32_t j = __float_as_uint(c.e0.w);
+    c.j = c.valid && j < T ? j : 0u;
+    return c;
+}
+
+// Candidates by triangle id (global list, whole-mesh fallback): the SoA cull planes.
+template <typename Fetch>
+__device__ __forceinline__ Cand load_ids(const float4* __restrict__ culls, uint32_t T, uint32_t n,
+                                         uint32_t base, Fetch fetch)
+{
+    Cand c;
+    const uint32_t k = base + (threadIdx.x & 63u);
+    c.valid = k < n;
+    const uint32_t j = c.valid ? fetch(k) : 0u;
+    c.j = j < T ? j : 0u;
+    c.bb = culls[c.j];
+    c.e0 = culls[(size_t)T + c.j];
+    c.e1 = culls[2 * (size_t)T + c.j];
+    c.e2 = culls[3 * (size_t)T + c.j];
+    return c;
+}
+
+// The survivors of one chunk, staged in the wave's LDS slice (one TriRec each,
+// in ascending candidate order).
+struct WaveStage {
+    float4 r[4][64];     // r[q][s] = quarter q of survivor s's TriRec
+};
+
+__device__ __forceinline__ void test_staged_pair(const WaveStage& st, uint32_t s0, uint32_t s1,
+                                                 bool two, float dx, float dy, float dz, HitList& hl)
+{
+    const float4 a0 = st.r[0][s0], a1 = st.r[1][s0], a2 = st.r[2][s0], a3 = st.r[3][s0];
+    const float4 b0 = st.r[0][s1], b1 = st.r[1][s1], b2 = st.r[2][s1], b3 = st.r[3][s1];
+    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (a3.x)
+    float det0, u0, v0, det1, u1, v1;
+    mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
+                  det0, u0, v0);
+    mt_numerators(dx, dy, dz, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w,
+                  det1, u1, v1);
     float i0, i1;
     if (__builtin_expect(__ballot(!(rcp_newton_exact_for(det0) && rcp_newton_exact_for(det1))) == 0ull, 1)) {
         i0 = rcp_newton(det0);
@@ -1206,61 +1264,70 @@ __device__ __forceinline__ void test_record_pair(const TriRec* __restrict__ recs
         i1 = inv_det_of(det1);
     }
     bool h0, h1;
-    const float t0 = mt_finish_inv(det0, i0, a0, b0, a.tnum, h0);
-    const float t1 = mt_finish_inv(det1, i1, a1, b1, b.tnum, h1);
+    const float t0 = mt_finish_inv(det0, i0, u0, v0, a3.x, h0);
+    const float t1 = mt_finish_inv(det1, i1, u1, v1, b3.x, h1);
     hl.push_if(h0, t0);
     hl.push_if(two && h1, t1);
-#else
-    bool h0, h1 = false;
-    float t1 = 0.0f;
-    const float t0 = mt_exact(dx, dy, dz, a.e1x, a.e1y, a.e1z, a.e2x, a.e2y, a.e2z, a.tvx, a.tvy,
-                              a.tvz, a.qvx, a.qvy, a.qvz, a.tnum, h0);
-    if (two) {
-        const TriRec b = recs[j1];
-        t1 = mt_exact(dx, dy, dz, b.e1x, b.e1y, b.e1z, b.e2x, b.e2y, b.e2z, b.tvx, b.tvy, b.tvz,
-                      b.qvx, b.qvy, b.qvz, b.tnum, h1);
-    }
-    hl.push_if(h0, t0);
-    hl.push_if(h1, t1);
-#endif
 }
 
-// Candidates of one region as seen by one wave: load_cand(base) gives this
-// lane's candidate of the 64 starting at `base` (triangle id, relaxed edges).
-struct Cand {
-    uint32_t j;
-    bool valid;
-    float4 bb, e0, e1, e2;
-};
-
-template <typename Fetch>
-__device__ __forceinline__ Cand load_cand(const float4* __restrict__ culls, uint32_t T, uint32_t n_cand,
-                                          uint32_t base, Fetch fetch)
+__device__ __forceinline__ void test_staged_one(const WaveStage& st, uint32_t s, float dx, float dy,
+                                                float dz, HitList& hl)
 {
-    Cand c;
-    const uint32_t k = base + (threadIdx.x & 63u);
-    c.valid = k < n_cand;
-    const uint32_t j = c.valid ? fetch(k) : 0u;
-    c.j = j < T ? j : 0u;                         // (always) never read out of range
-    c.bb = culls[c.j];
-    c.e0 = culls[(size_t)T + c.j];
-    c.e1 = culls[2 * (size_t)T + c.j];
-    c.e2 = culls[3 * (size_t)T + c.j];
-    return c;
+    const float4 a0 = st.r[0][s], a1 = st.r[1][s], a2 = st.r[2][s];
+    const float tnum = st.r[3][s].x;
+    float det, u, v;
+    mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
+                  det, u, v);
+    const float inv = __builtin_expect(__ballot(!rcp_newton_exact_for(det)) == 0ull, 1) ? rcp_newton(det)
+                                                                                      : inv_det_of(det);
+    bool h;
+    const float t = mt_finish_inv(det, inv, u, v, tnum, h);
+    hl.push_if(h, t);
 }
 
-// One 8x8 tile: one lane per candidate evaluates the three relaxed edges at
-// the tile rectangle, a ballot keeps the survivors, and each survivor's
-// record is a wave-uniform scalar load tested exactly for all 64 rays (two at
-// a time).  The rays are generated when the first survivor appears; a tile
-// without survivors stores the miss constants (80, +inf, 255) directly.
-// `first` is the region's first chunk of candidates, already loaded.
+// One chunk's survivors (mask m, this lane's candidate j): gather their
+// records into LDS, then test them two at a time.
+__device__ __forceinline__ void test_survivors(WaveStage& st, const TriRec* __restrict__ recs,
+                                               unsigned long long m, bool pass, uint32_t j, float dx,
+                                               float dy, float dz, HitList& hl)
+{
+    const uint32_t idx =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (pass) {
+        const float4* q = reinterpret_cast<const float4*>(recs + j);
+        const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+        st.r[0][idx] = r0;
+        st.r[1][idx] = r1;
+        st.r[2][idx] = r2;
+        st.r[3][idx] = r3;
+    }
+    // the wave reads what its own lanes wrote: LDS keeps one wave's order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t ns = (uint32_t)__popcll(m);
+#if XRT_STAGED_PAIRS
+    for (uint32_t s = 0; s < ns; s += 2u) {
+        const bool two = s + 1u < ns;
+        test_staged_pair(st, s, two ? s + 1u : s, two, dx, dy, dz, hl);
+    }
+#else
+    for (uint32_t s = 0; s < ns; ++s) test_staged_one(st, s, dx, dy, dz, hl);
+#endif
+    // the next chunk overwrites the slice only after every lane's reads
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <typename Fetch>
-__device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs& out,
-                                            const TriRec* __restrict__ recs,
-                                            const float4* __restrict__ culls, uint32_t tx0,
-                                            uint32_t ty0, uint32_t n_cand, const Cand& first,
-                                            Fetch fetch, WaveStats& ws)
+__device__ __forceinline__ void render_binned_tile(const RenderParams& p, const Outputs& out,
+                                                   const TriRec* __restrict__ recs,
+                                                   const float4* __restrict__ culls,
+                                                   uint32_t tx0, uint32_t ty0,
+                                                   const RegionEntry* __restrict__ local,
+                                                   uint32_t n_local, uint32_t bound, const Cand& first,
+                                                   const uint32_t* __restrict__ glob, uint32_t n_glob,
+                                                   bool whole_mesh, Fetch fetch, WaveStage& st,
+                                                   WaveStats& ws)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = p.num_triangles;
@@ -1268,48 +1335,44 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
     const uint32_t row = ty0 + (lane >> 3);
     const bool active = col < p.width && row < p.row_end;
     const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
+    const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     bool have_ray = false;                        // wave-uniform
     HitList hl;
     hl.init();
     uint32_t tests = 0;
-    for (uint32_t base = 0; base < n_cand; base += 64u) {
-        Cand c;
-        if (base == 0u) {       // the first chunk's ids were loaded once per wave; edges are cache-hot
-            c = first;
-            c.bb = culls[c.j];
-            c.e0 = culls[(size_t)T + c.j];
-            c.e1 = culls[2 * (size_t)T + c.j];
-            c.e2 = culls[3 * (size_t)T + c.j];
-        } else {
-            c = load_cand(culls, T, n_cand, base, fetch);
-        }
-        // the tile rectangle against the footprint box and the three relaxed
-        // edges: with the box's axes this is the full separating-axis test of
-        // the loosened triangle against the tile's pixel centres
+    const uint32_t n_cand = whole_mesh ? T : n_local + n_glob;
+    // One loop over the chunks of all sources (one copy of its body): the
+    // region's entries, then the global list's ids, or every triangle id.
+    const uint32_t local_chunks = whole_mesh ? 0u : (n_local + 63u) / 64u;
+    const uint32_t id_count = whole_mesh ? T : n_glob;
+    const uint32_t chunks = local_chunks + (id_count + 63u) / 64u;
+    auto body = [&](const Cand& c) {
         const bool pass = c.valid & edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f) &
-                          box_overlaps(c.bb, (float)tx0, (float)tx0 + 7.0f, (float)ty0, (float)ty0 + 7.0f);
-        unsigned long long m = __ballot(pass);
-        if (!m) continue;
+                          box_overlaps(c.bb, fx0, fx1, fy0, fy1);
+        const unsigned long long m = __ballot(pass);
+        if (!m) return;
         tests += (uint32_t)__popcll(m);
         if (!have_ray) {
-            if (!(ablation(p) & kAblateRayGen)) make_ray(*out.frame, row, col, dx, dy, dz);
+            if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
             have_ray = true;
         }
-        if (ablation(p) & kAblateExact) continue;
-        while (m) {
-            // the next two survivors, selected without a branch (a lone one
-            // is paired with itself; test_record_pair drops the copy)
-            const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1ull;
-            const bool two = m != 0ull;
-            const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m | (1ull << 63)) : k0;
-            m &= m - 1ull;                        // no-op once m == 0
-            const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k0);
-            const uint32_t j1 = (uint32_t)__builtin_amdgcn_readlane((int)c.j, (int)k1);
-            test_record_pair(recs, j0, j1, two, dx, dy, dz, hl);
-        }
+        if (ablation(p) & kAblateExact) return;
+        test_survivors(st, recs, m, pass, c.j, dx, dy, dz, hl);
+    };
+    // the first chunk of entries was loaded beside the region's count
+    uint32_t ci = 0;
+    if (local_chunks) {
+        body(first);
+        ci = 1;
+    }
+    for (; ci < chunks; ++ci) {
+        Cand c;
+        if (ci < local_chunks) c = load_entries(local, bound, n_local, ci * 64u, T);   // wave-uniform switch
+        else c = load_ids(culls, T, id_count, (ci - local_chunks) * 64u,
+                          [&](uint32_t k) { return whole_mesh ? k : glob[k]; });
+        body(c);
     }
     ws.tile_tests += tests;
     if (have_ray) {
@@ -1325,48 +1388,17 @@ __device__ __forceinline__ void render_tile(const RenderParams& p, const Outputs
     if (out.image_u8) out.image_u8[o] = 255u;
 }
 
-constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
-
-// TPW consecutive tiles of one region row (TPW = 1, 2 or 4), rendered in
-// turn; the region's first 64 candidate ids are loaded once for all of them.
-template <uint32_t TPW, typename Fetch>
-__device__ __forceinline__ void render_tiles_wave(const RenderParams& p, const Outputs& out,
-                                                  const TriRec* __restrict__ recs,
-                                                  const float4* __restrict__ culls, uint32_t rx0,
-                                                  uint32_t ry0, uint32_t tile0, uint32_t n_cand,
-                                                  Fetch fetch, WaveStats& ws)
-{
-    if (ablation(p) & kAblateCandidates) n_cand = 0;
-    Cand first;                                   // ids only: the edges are re-read per tile
-    {
-        const uint32_t k = threadIdx.x & 63u;
-        first.valid = k < n_cand;
-        const uint32_t j = first.valid ? fetch(k) : 0u;
-        first.j = j < p.num_triangles ? j : 0u;   // (always) never read out of range
-    }
-#pragma unroll
-    for (uint32_t t = 0; t < TPW; ++t) {
-        const uint32_t tile = tile0 + t;
-        const uint32_t tx0 = rx0 + (tile & 3u) * 8u;
-        const uint32_t ty0 = ry0 + (tile >> 2) * 8u;
-        if (tx0 < p.width && ty0 < p.row_end)      // wave-uniform
-            render_tile(p, out, recs, culls, tx0, ty0, n_cand, first, fetch, ws);
-    }
-}
-
-// Binned render: kTileWaves waves per workgroup, TPW 8x8 tiles of one region
-// row per wave (1 by default, see enqueue_render), regions in
-// the launch order of bins.order; each wave stores its own statistics record,
-// so no wave waits for another.  8 waves per SIMD: the tile waves are
+// Binned render: kTileWaves waves per workgroup, one 8x8 tile each, regions
+// in the launch order of bins.order; each wave stores its own statistics
+// record, so no wave waits for another.  8 waves per SIMD: the tile waves are
 // latency-bound, and occupancy is what hides it.
-template <uint32_t TPW>
 __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins, const BinState* __restrict__ bs)
 {
-    constexpr uint32_t kWavesPerRegion = 16u / TPW;
     static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
                   "a workgroup's waves render tiles of one region");
+    __shared__ WaveStage s_stage[kTileWaves];
     const uint64_t t_start = block_start_stamp();
 #if XRT_XCD_REMAP
     // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
@@ -1386,8 +1418,15 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
 #endif
     const uint32_t slot = g / kWavesPerRegion;
-    // count and region are independent loads (lists are by slot)
+    const uint32_t tile = g % kWavesPerRegion;
+    WaveStage& st = s_stage[wave_in_block()];
+    // the count, the region and the first 64 entries are independent loads
+    // (lists are by slot; entries past the count are masked)
+    const RegionEntry* __restrict__ local = bins.list + (size_t)slot * bins.cap;
+    const uint32_t bound = wave_uniform(min(bins.cap, 64u));
+    const Cand first_raw = load_entries(local, bound, bound, 0u, p.num_triangles);
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
+    const uint32_t n_glob = wave_uniform(bs->global_count);
     uint32_t reg_x, reg_y;
     if (bins.order) {
         const uint32_t xy = wave_uniform(bins.order[slot]);
@@ -1397,26 +1436,30 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         reg_x = slot % bins.regions_x;
         reg_y = slot / bins.regions_x;
     }
-    const uint32_t tile0 = (g % kWavesPerRegion) * TPW;
-    const uint32_t rx0 = reg_x * kRegion;
-    const uint32_t ry0 = p.row_begin + reg_y * kRegion;
+    const uint32_t tx0 = reg_x * kRegion + (tile & 3u) * 8u;
+    const uint32_t ty0 = p.row_begin + reg_y * kRegion + (tile >> 2) * 8u;
     WaveStats ws = {};
     uint32_t n_cand = 0;
-    if (rx0 + (tile0 & 3u) * 8u < p.width && ry0 + (tile0 >> 2) * 8u < p.row_end) {   // wave-uniform
-        if (n_local > bins.cap) {   // the region's list overflowed: whole mesh (exact, slower)
-            n_cand = p.num_triangles;
-            render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
-                                   [](uint32_t k) { return k; }, ws);
-        } else {
-            const uint32_t* __restrict__ local = bins.list + (size_t)slot * bins.cap;
-            const uint32_t* __restrict__ glob = bins.global_list;
-            n_cand = n_local + wave_uniform(bs->global_count);
-            render_tiles_wave<TPW>(p, out, recs, culls, rx0, ry0, tile0, n_cand,
-                                   [&](uint32_t k) { return k < n_local ? local[k] : glob[k - n_local]; }, ws);
-        }
+    if (tx0 < p.width && ty0 < p.row_end) {           // wave-uniform
+        const bool whole = n_local > bins.cap;        // the region's list overflowed: whole mesh (exact, slower)
+        Cand first = first_raw;
+        first.valid = first.valid && (threadIdx.x & 63u) < n_local;
+        if (!first.valid) first.j = 0u;
+        const uint32_t* __restrict__ glob = bins.global_list;
+        n_cand = whole ? p.num_triangles : n_local + n_glob;
+        // candidate k's triangle (the overflow fix-up re-reads the candidates)
+        const RegionEntry* __restrict__ lst = local;
+        const uint32_t nl = whole ? 0u : n_local;
+        const bool all = whole;
+        render_binned_tile(p, out, recs, culls, tx0, ty0, local, n_local, bins.cap, first, glob, n_glob,
+                           whole,
+                           [=](uint32_t k) {
+                               return all ? k : k < nl ? __float_as_uint(lst[k].e0.w) : glob[k - nl];
+                           },
+                           st, ws);
     }
     // candidates are counted once per region (by the wave holding tile 0)
-    store_wave_stats(ws, tile0 == 0u ? n_cand : 0u, out.block_stats, g, t_start);
+    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
 }
 
 // ---------------------------------------------------------------------------

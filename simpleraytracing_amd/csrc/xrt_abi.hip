@@ -53,6 +53,8 @@ struct FrameSet {
     float4* cull = nullptr;        // per-render cull planes (4 x T float4)
     size_t cull_cap = 0;
     RenderParams* frame = nullptr;       // the frame's parameters (k_prep writes, make_ray reads)
+    float* offsets = nullptr;            // the frame's pixel offsets, rows then columns (k_prep)
+    size_t offsets_cap = 0;
     BlockStats* block_stats = nullptr;   // the render's per-workgroup / per-wave records
     size_t block_stats_cap = 0;
     uint32_t n_blocks = 0;         // records of the set's last render
@@ -61,7 +63,7 @@ struct FrameSet {
     // binning (XRT_KERNEL_BINNED)
     uint32_t* bin_counts = nullptr;    // BinState line | line-padded region counts
     size_t bin_counts_cap = 0;
-    uint32_t* bin_list = nullptr;      // regions x capacity triangle ids
+    RegionEntry* bin_list = nullptr;   // regions x capacity footprint entries
     size_t bin_list_cap = 0;
     uint32_t* global_list = nullptr;
     size_t global_list_cap = 0;
@@ -324,13 +326,16 @@ int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, ui
     return XRT_OK;
 }
 
+// k_prep: one thread per triangle, and at least one per image row and column
+// (the pixel-offset tables).
 int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const CullParams& cp, bool culled,
                 const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
 {
     const uint64_t T = ctx->num_tris;
-    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, nullptr, done, 0,
+    const uint64_t threads = std::max<uint64_t>(T, (uint64_t)p.height + p.width);
+    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, nullptr, done, 0,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
-                          fs.frame);
+                          fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
@@ -442,6 +447,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     }
     if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
     if (culled && (rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
+    if ((rc = ensure(ctx, fs.offsets, fs.offsets_cap, (size_t)cam->height + cam->width))) return rc;
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
     if (!ctx->cull_valid || std::memcmp(&ctx->cull_cam, cam, sizeof *cam) != 0) {
@@ -455,17 +461,12 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     out.lbuffer = d_lbuffer;
     out.image_u8 = d_u8;
     out.frame = (const __attribute__((address_space(4))) RenderParams*)fs.frame;
+    out.off.v = fs.offsets;
+    out.off.u = fs.offsets + cam->height;
     const uint32_t n_regions = rows ? rx * ry : 0u;
-    // BINNED: 8x8 tiles per render wave.  One (A/B, whole step: 1 wins at
-    // 1024^2, 2048^2 and the 1M-triangle 8192^2 frame; a row of 4 wins by 10 %
-    // at dragon 4096^2); XRT_TPW=2|4 selects the others.
-    static const int tpw_env = [] {
-        const char* e = std::getenv("XRT_TPW");
-        return e ? std::atoi(e) : 0;
-    }();
-    const uint32_t tiles_per_wave = (tpw_env == 2 || tpw_env == 4) ? (uint32_t)tpw_env : 1u;
+    // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
-              : binned                     ? dim3(16 / tiles_per_wave / kTileWaves * n_regions)
+              : binned                     ? dim3(kWavesPerRegion / kTileWaves * n_regions)
                                            : dim3(rx, ry);
     // stats records: one per workgroup, one per tile wave for BINNED
     const uint32_t n_blocks = rows ? grid.x * grid.y * (binned ? kTileWaves : 1u) : 0u;
@@ -484,8 +485,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     }
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
-    if (T && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
-    if (!T) XRT_HIP(ctx, hipMemcpy(fs.frame, &p, sizeof p, hipMemcpyHostToDevice));   // no k_prep to write it
+    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     if (binned && !ctx->bin_force_cap) {
         // Size the region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of the largest region count, and a
@@ -511,7 +511,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     }
     // The render is launched once the preparation is complete (host-side
     // order; the caller's queue never waits on the prep queue).
-    if (T && prep_done) {
+    if (rows > 0 && prep_done) {
         const auto t = HostClock::now();
         XRT_HIP(ctx, hipEventSynchronize(prep_done));
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
@@ -558,9 +558,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
                                   fs.recs, fs.cull, p, out);
         else
-            hipExtLaunchKernelGGL(tiles_per_wave == 4 ? k_render_binned<4>
-                                  : tiles_per_wave == 2 ? k_render_binned<2> : k_render_binned<1>,
-                                  grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
+            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
                                   fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         if (t0) {
@@ -651,6 +649,7 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.cull);
         (void)hipFree(fs.block_stats);
         (void)hipFree(fs.frame);
+        (void)hipFree(fs.offsets);
         (void)hipFree(fs.bin_counts);
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
@@ -978,7 +977,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr);
+                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, fs.recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));

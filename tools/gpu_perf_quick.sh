@@ -1,0 +1,14 @@
+#!/bin/bash
+# Parity subset on the binned path, then bench lines at 2048^2 / 1024^2 / 4096^2
+# and the 1.12M-tri 8192^2 frame (no CPU baseline).  Logs under gpurun_out/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PAT="${1:-golden or full_256 or ragged or overflow or deep_stack or corner or 2048 or 1024 or pipelined or device_buffers}"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread -k "$PAT" > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+for cfg in "--size 2048 2048" "--size 1024 1024" "--size 4096 4096" "--size 8192 8192 --tile-mesh 7 --steps 20 --warmup 3"; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline $cfg > gpurun_out/perf.json 2> gpurun_out/perf.err || { cat gpurun_out/perf.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/perf.json')); r=d['roofline']; print('$cfg', 'Mrays/s %.0f'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'kernel_ms %.4f'%r['avg_kernel_ms'], 'tests/ray %.2f'%d['render_stats']['ray_triangle_tests_per_ray'], 'overflow', d['render_stats']['overflow_rays'])"
+done
