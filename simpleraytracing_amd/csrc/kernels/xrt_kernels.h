@@ -928,7 +928,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
 constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
-constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back count atomics
+constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -944,16 +944,6 @@ struct alignas(16) RegionEntry {
     float4 bb;   // footprint box (xmin, xmax, ymin, ymax)
 };
 static_assert(sizeof(RegionEntry) == 64, "RegionEntry must be 64 bytes");
-
-__device__ __forceinline__ RegionEntry make_entry(float4 e0, float4 e1, float4 e2, float4 bb, uint32_t tri)
-{
-    RegionEntry r;
-    r.e0 = make_float4(e0.x, e0.y, e0.z, __uint_as_float(tri));
-    r.e1 = e1;
-    r.e2 = e2;
-    r.bb = bb;
-    return r;
-}
 
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
@@ -1016,7 +1006,7 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 // k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
 // terms), cull planes and (binned) the triangle's region list entries.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_prep(const float* __restrict__ tris, uint32_t T,
+__global__ __launch_bounds__(256, 8) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
@@ -1058,6 +1048,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             culls[(size_t)T + i] = fp.e0;
             culls[2 * (size_t)T + i] = fp.e1;
             culls[3 * (size_t)T + i] = fp.e2;
+            fp.e0.w = __uint_as_float(i);          // the region entries carry the id (make_entry's layout)
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
@@ -1081,9 +1072,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     if (tid == 0) s_max = 0u;
 
     uint32_t my_max = 0;                           // 1 + the largest slot this thread took
-    auto place = [&](uint32_t r, uint32_t slot, const RegionEntry& e) {
+    auto place = [&](uint32_t r, uint32_t slot, float4 e0, float4 e1, float4 e2, float4 bb) {
         my_max = max(my_max, slot + 1u);
-        if (slot < bins.cap) bins.list[(size_t)r * bins.cap + slot] = e;
+        if (slot < bins.cap) {
+            RegionEntry* e = bins.list + (size_t)r * bins.cap + slot;
+            e->e0 = e0;
+            e->e1 = e1;
+            e->e2 = e2;
+            e->bb = bb;
+        }
     };
     auto cell_pass = [&](float4 e0, float4 e1, float4 e2, uint32_t rx, uint32_t ry) {
         const float xc = (float)(rx * kRegion) + 15.5f;
@@ -1096,7 +1093,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     // entries.  (Batches keep k_prep within 64 VGPRs, so its waves fit the
     // holes a retiring render wave leaves while the previous frame renders.)
     if (has && !big) {
-        const RegionEntry entry = make_entry(fp.e0, fp.e1, fp.e2, fp.bbox, i);
         uint32_t cx = x0, cy = y0;
         for (uint32_t k0 = 0; k0 < cells; k0 += kSerialBatch) {
             uint32_t reg[kSerialBatch], slot[kSerialBatch];
@@ -1113,7 +1109,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
 #pragma unroll
             for (uint32_t k = 0; k < kSerialBatch; ++k)
-                if (reg[k] != kEmpty) place(reg[k], slot[k], entry);
+                if (reg[k] != kEmpty) place(reg[k], slot[k], fp.e0, fp.e1, fp.e2, fp.bbox);
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
@@ -1162,8 +1158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const float4 e0 = s_e[0][lo], e1 = s_e[1][lo], e2 = s_e[2][lo];
             if (cell_pass(e0, e1, e2, rx, ry)) {
                 const uint32_t r = slot_of(bins, ry * bins.regions_x + rx);
-                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u),
-                      make_entry(e0, e1, e2, s_e[3][lo], i0 + s_big[lo]));
+                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u), e0, e1, e2, s_e[3][lo]);
             }
         }
     }
@@ -1205,17 +1200,20 @@ struct Cand {
 
 // Region-list entries [base, base + 64): direct 64-B loads; `bound` (the
 // wave-uniform list length or capacity) keeps the reads inside the list.
-__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t bound,
-                                             uint32_t n_valid, uint32_t base, uint32_t T)
+__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t n_valid,
+                                             uint32_t base, uint32_t T)
 {
     Cand c;
     const uint32_t k = base + (threadIdx.x & 63u);
     c.valid = k < n_valid;
-    const RegionEntry* e = list + (k < bound ? k : 0u);
-    c.e0 = e->e0;
-    c.e1 = e->e1;
-    c.e2 = e->e2;
-    c.bb = e->bb;
+    c.e0 = c.e1 = c.e2 = c.bb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (c.valid) {                                // lanes past the count load nothing
+        const RegionEntry* e = list + k;
+        c.e0 = e->e0;
+        c.e1 = e->e1;
+        c.e2 = e->e2;
+        c.bb = e->bb;
+    }
     const uint32_t j = __float_as_uint(c.e0.w);
     c.j = c.valid && j < T ? j : 0u;
     return c;
@@ -1324,7 +1322,7 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
                                                    const float4* __restrict__ culls,
                                                    uint32_t tx0, uint32_t ty0,
                                                    const RegionEntry* __restrict__ local,
-                                                   uint32_t n_local, uint32_t bound, const Cand& first,
+                                                   uint32_t n_local,
                                                    const uint32_t* __restrict__ glob, uint32_t n_glob,
                                                    bool whole_mesh, Fetch fetch, WaveStage& st,
                                                    WaveStats& ws)
@@ -1361,15 +1359,9 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
         if (ablation(p) & kAblateExact) return;
         test_survivors(st, recs, m, pass, c.j, dx, dy, dz, hl);
     };
-    // the first chunk of entries was loaded beside the region's count
-    uint32_t ci = 0;
-    if (local_chunks) {
-        body(first);
-        ci = 1;
-    }
-    for (; ci < chunks; ++ci) {
+    for (uint32_t ci = 0; ci < chunks; ++ci) {
         Cand c;
-        if (ci < local_chunks) c = load_entries(local, bound, n_local, ci * 64u, T);   // wave-uniform switch
+        if (ci < local_chunks) c = load_entries(local, n_local, ci * 64u, T);   // wave-uniform switch
         else c = load_ids(culls, T, id_count, (ci - local_chunks) * 64u,
                           [&](uint32_t k) { return whole_mesh ? k : glob[k]; });
         body(c);
@@ -1420,11 +1412,8 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t slot = g / kWavesPerRegion;
     const uint32_t tile = g % kWavesPerRegion;
     WaveStage& st = s_stage[wave_in_block()];
-    // the count, the region and the first 64 entries are independent loads
-    // (lists are by slot; entries past the count are masked)
+    // the count and the region are independent loads (lists are by slot)
     const RegionEntry* __restrict__ local = bins.list + (size_t)slot * bins.cap;
-    const uint32_t bound = wave_uniform(min(bins.cap, 64u));
-    const Cand first_raw = load_entries(local, bound, bound, 0u, p.num_triangles);
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
     const uint32_t n_glob = wave_uniform(bs->global_count);
     uint32_t reg_x, reg_y;
@@ -1442,17 +1431,13 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     uint32_t n_cand = 0;
     if (tx0 < p.width && ty0 < p.row_end) {           // wave-uniform
         const bool whole = n_local > bins.cap;        // the region's list overflowed: whole mesh (exact, slower)
-        Cand first = first_raw;
-        first.valid = first.valid && (threadIdx.x & 63u) < n_local;
-        if (!first.valid) first.j = 0u;
         const uint32_t* __restrict__ glob = bins.global_list;
         n_cand = whole ? p.num_triangles : n_local + n_glob;
         // candidate k's triangle (the overflow fix-up re-reads the candidates)
         const RegionEntry* __restrict__ lst = local;
         const uint32_t nl = whole ? 0u : n_local;
         const bool all = whole;
-        render_binned_tile(p, out, recs, culls, tx0, ty0, local, n_local, bins.cap, first, glob, n_glob,
-                           whole,
+        render_binned_tile(p, out, recs, culls, tx0, ty0, local, n_local, glob, n_glob, whole,
                            [=](uint32_t k) {
                                return all ? k : k < nl ? __float_as_uint(lst[k].e0.w) : glob[k - nl];
                            },

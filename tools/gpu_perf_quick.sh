@@ -12,3 +12,5 @@ for cfg in "--size 2048 2048" "--size 1024 1024" "--size 4096 4096" "--size 8192
   timeout -k 10 300 python bench.py --no-cpu-baseline $cfg > gpurun_out/perf.json 2> gpurun_out/perf.err || { cat gpurun_out/perf.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('gpurun_out/perf.json')); r=d['roofline']; print('$cfg', 'Mrays/s %.0f'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'kernel_ms %.4f'%r['avg_kernel_ms'], 'tests/ray %.2f'%d['render_stats']['ray_triangle_tests_per_ray'], 'overflow', d['render_stats']['overflow_rays'])"
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pq_prof -o run -- python3 bench.py --no-cpu-baseline --steps 100 > /dev/null 2> gpurun_out/pq_prof.err || exit 1
+f=$(find gpurun_out/pq_prof -name "*kernel_stats.csv" | head -1); cut -d, -f1-8 "$f" | head -6
