@@ -57,6 +57,9 @@
 #ifndef XRT_STAGED_PAIRS
 #define XRT_STAGED_PAIRS 0   // binned render: LDS-staged survivors tested two at a time (else one)
 #endif
+#ifndef XRT_PREP_THREADS
+#define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)
+#endif
 #ifndef XRT_ABLATION
 #define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
 #endif

@@ -953,6 +953,8 @@ struct BinBuffers {
     const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
     uint32_t cap;            // list capacity per region
     uint32_t regions_x, regions_y;
+    uint32_t* clear;         // the other half's counters (its BinState line precedes them), cleared by k_prep
+    uint32_t clear_regions;  // counters to clear there
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -1006,7 +1008,13 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 // k_prep: one thread per triangle -- TriRec (Ray.cxx:86-122's ray-independent
 // terms), cull planes and (binned) the triangle's region list entries.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 8) void k_prep(const float* __restrict__ tris, uint32_t T,
+// k_prep runs beside the previous frame's render: single-wave workgroups fit
+// the holes that retiring render waves leave (a 4-wave one needs a free slot
+// on all four SIMDs of a CU at once).
+constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
+constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
+
+__global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
@@ -1053,12 +1061,16 @@ __global__ __launch_bounds__(256, 8) void k_prep(const float* __restrict__ tris,
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
     if (!bins.counts) return;                      // kernel-uniform
+    if (bins.clear) {                              // the other half, for the set's next frame
+        if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
+        if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
+    }
 
-    __shared__ float4 s_e[4][256];                 // relaxed edges and box (big triangles)
-    __shared__ uint2 s_rect[256];                  // (x0 | x1 << 16, y0 | y1 << 16)
-    __shared__ uint32_t s_big[256];                // big triangles (local index)
-    __shared__ uint32_t s_cum[256];                // inclusive prefix of their cell counts
-    __shared__ uint32_t s_wave[4];
+    __shared__ float4 s_e[4][kPrepThreads];        // relaxed edges and box (big triangles)
+    __shared__ uint2 s_rect[kPrepThreads];         // (x0 | x1 << 16, y0 | y1 << 16)
+    __shared__ uint32_t s_big[kPrepThreads];       // big triangles (local index)
+    __shared__ uint32_t s_cum[kPrepThreads];       // inclusive prefix of their cell counts
+    __shared__ uint32_t s_wave[kPrepWaves];
     __shared__ uint32_t s_max;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1119,7 +1131,7 @@ __global__ __launch_bounds__(256, 8) void k_prep(const float* __restrict__ tris,
     if (lane == 0) s_wave[wave] = (uint32_t)__popcll(mb);
     __syncthreads();
     uint32_t nbig = 0, bslot = 0;
-    for (uint32_t w = 0; w < 4; ++w) {
+    for (uint32_t w = 0; w < kPrepWaves; ++w) {
         bslot += w < wave ? s_wave[w] : 0u;
         nbig += s_wave[w];
     }

@@ -47,6 +47,8 @@ inline uint32_t region_cap_for(uint32_t max_count)
 // "Pipelining"): the host waits for the preparation's completion event before
 // it launches the render, and for the completion event of the render that
 // last used the set before it prepares into the set again.
+constexpr uint32_t kDirtyAll = 0xFFFFFFFFu;
+
 struct FrameSet {
     TriRec* recs = nullptr;        // per-render records
     size_t recs_cap = 0;
@@ -61,8 +63,18 @@ struct FrameSet {
     bool binned = false;           // the set's last frame was binned (BinState valid)
 
     // binning (XRT_KERNEL_BINNED)
-    uint32_t* bin_counts = nullptr;    // BinState line | line-padded region counts
-    size_t bin_counts_cap = 0;
+    // Two halves (parities), each [BinState line | line-padded region counts].
+    // A frame counts into one half while its k_prep clears the other, which
+    // the set's previous frame used (its render is complete: the host waited
+    // for it before reusing the set) -- no memset on the per-frame path.
+    uint32_t* bin_counts = nullptr;
+    size_t bin_counts_cap = 0;         // words, both halves
+    size_t bin_half_words = 0;         // words per half
+    uint32_t half = 0;                 // half of the set's last frame
+    // Per half: the counters past dirty[h] are zero, and so is its BinState
+    // when dirty[h] == 0; kDirtyAll = unknown (fresh allocation).
+    uint32_t dirty[2] = {kDirtyAll, kDirtyAll};
+    BinState* last_state = nullptr;    // BinState of the set's last binned frame
     RegionEntry* bin_list = nullptr;   // regions x capacity footprint entries
     size_t bin_list_cap = 0;
     uint32_t* global_list = nullptr;
@@ -332,32 +344,51 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                 const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
 {
     const uint64_t T = ctx->num_tris;
-    const uint64_t threads = std::max<uint64_t>(T, (uint64_t)p.height + p.width);
-    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, nullptr, done, 0,
+    const uint64_t threads =
+        std::max<uint64_t>(std::max<uint64_t>(T, (uint64_t)p.height + p.width), bins.clear ? bins.clear_regions : 0u);
+    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads),
+                          0, stream, nullptr, done, 0,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
 
-// Region buffers of a binned frame.  The control block and the line-padded
-// counters are cleared on the prep stream in front of every binned k_prep
-// (off the critical path when frames are pipelined).
+// Region buffers of a binned frame.  The frame counts into one half of the
+// set's counters (FrameSet::bin_counts); k_prep clears the other half.  A half
+// is cleared here, on the prep stream, only when it is not known clean for
+// this many regions (the first frames, a larger region grid, a re-run).
 int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& bins, BinState*& ctl,
-                hipStream_t stream)
+                hipStream_t stream, bool rerun = false)
 {
     const uint64_t T = ctx->num_tris;
     static_assert(sizeof(BinState) <= kCounterStride * sizeof(uint32_t), "BinState fits its line");
     int rc;
-    // control block padded to a line, then one line-padded counter per region
-    const size_t counter_words = kCounterStride + (size_t)kCounterStride * n_regions;
-    if ((rc = ensure(ctx, fs.bin_counts, fs.bin_counts_cap, counter_words))) return rc;
+    // per half: control block padded to a line, then one line-padded counter per region
+    const size_t half_words = kCounterStride + (size_t)kCounterStride * n_regions;
+    if (!fs.bin_counts || fs.bin_half_words < half_words) {
+        if ((rc = ensure(ctx, fs.bin_counts, fs.bin_counts_cap, 2 * half_words))) return rc;
+        fs.bin_half_words = half_words;
+        fs.dirty[0] = fs.dirty[1] = kDirtyAll;
+    }
     const uint32_t cap = ctx->bin_region_cap;
     if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, (size_t)n_regions * cap))) return rc;
     if ((rc = ensure(ctx, fs.global_list, fs.global_list_cap, T))) return rc;
-    XRT_HIP(ctx, hipMemsetAsync(fs.bin_counts, 0, counter_words * sizeof(uint32_t), stream));
-    ctl = reinterpret_cast<BinState*>(fs.bin_counts);
-    bins.counts = fs.bin_counts + kCounterStride;
+    const uint32_t q = rerun ? fs.half : fs.half ^ 1u;     // a re-run recounts into the same half
+    uint32_t* mine = fs.bin_counts + (size_t)q * fs.bin_half_words;
+    uint32_t* other = fs.bin_counts + (size_t)(q ^ 1u) * fs.bin_half_words;
+    if (rerun || fs.dirty[q] != 0u)
+        XRT_HIP(ctx, hipMemsetAsync(mine, 0, half_words * sizeof(uint32_t), stream));
+    fs.half = q;
+    fs.dirty[q] = n_regions;                                // this frame counts into it
+    // k_prep clears the other half: its control block and its dirty counters
+    const uint32_t alloc_regions = (uint32_t)((fs.bin_half_words - kCounterStride) / kCounterStride);
+    bins.clear = other + kCounterStride;
+    bins.clear_regions = fs.dirty[q ^ 1u] == kDirtyAll ? alloc_regions : fs.dirty[q ^ 1u];
+    fs.dirty[q ^ 1u] = 0u;
+    ctl = reinterpret_cast<BinState*>(mine);
+    fs.last_state = ctl;
+    bins.counts = mine + kCounterStride;
     bins.list = fs.bin_list;
     bins.global_list = fs.global_list;
     bins.cap = cap;
@@ -504,7 +535,7 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             ctx->bin_key_valid = true;
             if (h.max_count > bins.cap && ctx->bin_region_cap < kMaxRegionCap) {
                 ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(h.max_count));
-                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;   // clears
+                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, true))) return rc;   // clears
                 if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
             }
         }
@@ -833,9 +864,9 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     if (!ctx->last_t0 || hipEventElapsedTime(&ms, ctx->last_t0, ctx->last_t1) != hipSuccess) ms = 0.0f;
     stats->kernel = (uint32_t)ctx->last_kernel;
     stats->kernel_ms = ms;
-    if (fs && fs->binned && fs->bin_counts) {
+    if (fs && fs->binned && fs->last_state) {
         BinState bs = {};
-        XRT_HIP(ctx, hipMemcpy(&bs, fs->bin_counts, sizeof bs, hipMemcpyDeviceToHost));
+        XRT_HIP(ctx, hipMemcpy(&bs, fs->last_state, sizeof bs, hipMemcpyDeviceToHost));
         if (bs.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
             ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(bs.max_count));
     }
@@ -976,7 +1007,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     RenderParams p = make_params(*camera, 0, camera->height, T, ctx->hit_capacity);
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, 0, ctx->d_tris,
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads), 0, 0, ctx->d_tris,
                        (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
