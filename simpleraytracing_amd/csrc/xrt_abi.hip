@@ -341,13 +341,14 @@ int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, ui
 // k_prep: one thread per triangle, and at least one per image row and column
 // (the pixel-offset tables).
 int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const CullParams& cp, bool culled,
-                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
+                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done,
+                unsigned flags)
 {
     const uint64_t T = ctx->num_tris;
     const uint64_t threads =
         std::max<uint64_t>(std::max<uint64_t>(T, (uint64_t)p.height + p.width), bins.clear ? bins.clear_regions : 0u);
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads),
-                          0, stream, nullptr, done, 0,
+                          0, stream, nullptr, done, flags,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
@@ -359,8 +360,9 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
 // is cleared here, on the prep stream, only when it is not known clean for
 // this many regions (the first frames, a larger region grid, a re-run).
 int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& bins, BinState*& ctl,
-                hipStream_t stream, bool rerun = false)
+                hipStream_t stream, bool& cleared, bool rerun = false)
 {
+    cleared = false;
     const uint64_t T = ctx->num_tris;
     static_assert(sizeof(BinState) <= kCounterStride * sizeof(uint32_t), "BinState fits its line");
     int rc;
@@ -377,8 +379,10 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
     const uint32_t q = rerun ? fs.half : fs.half ^ 1u;     // a re-run recounts into the same half
     uint32_t* mine = fs.bin_counts + (size_t)q * fs.bin_half_words;
     uint32_t* other = fs.bin_counts + (size_t)(q ^ 1u) * fs.bin_half_words;
-    if (rerun || fs.dirty[q] != 0u)
+    if (rerun || fs.dirty[q] != 0u) {
         XRT_HIP(ctx, hipMemsetAsync(mine, 0, half_words * sizeof(uint32_t), stream));
+        cleared = true;                                     // k_prep must not overtake it
+    }
     fs.half = q;
     fs.dirty[q] = n_regions;                                // this frame counts into it
     // k_prep clears the other half: its control block and its dirty counters
@@ -464,11 +468,21 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     // This frame's buffer set.  The render that last used it (kFrameSets
     // frames ago) must be complete before the set is prepared again.
     FrameSet& fs = ctx->sets[ctx->next_set];
-    static const bool serial = [] {          // A/B only: XRT_PIPELINE=0 prepares on the caller's stream
+    // Where the preparation runs (DESIGN.md "Pipelining"; XRT_PIPELINE selects
+    // the others for A/B):
+    //   2 (default) on the caller's stream as an any-order dispatch: its AQL
+    //     packet has no barrier bit, so it runs beside the previous frame's
+    //     render, and the render behind it (barrier bit) waits for both --
+    //     the ordering is the queue's, with no host wait and no cross-queue event;
+    //   1 on the context's prep stream, the host waiting for its completion
+    //     before it launches the render;
+    //   0 serial on the caller's stream.
+    static const int pipeline = [] {
         const char* e = std::getenv("XRT_PIPELINE");
-        return e && std::atoi(e) == 0;
+        return e ? std::atoi(e) : 2;
     }();
-    hipStream_t ps = serial ? stream : ctx->prep_stream;
+    hipStream_t ps = pipeline == 1 ? ctx->prep_stream : stream;
+    unsigned prep_flags = pipeline == 2 ? hipExtAnyOrderLaunch : 0u;
     const auto t_call = HostClock::now();
     if (fs.done_valid) {
         const auto t = HostClock::now();
@@ -511,12 +525,14 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
-        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps))) return rc;
+        bool cleared = false;
+        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared))) return rc;
+        if (cleared) prep_flags = 0u;              // an any-order k_prep could start before the memset
         if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
     }
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
-    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, prep_flags))) return rc;
     if (binned && !ctx->bin_force_cap) {
         // Size the region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of the largest region count, and a
@@ -535,8 +551,9 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             ctx->bin_key_valid = true;
             if (h.max_count > bins.cap && ctx->bin_region_cap < kMaxRegionCap) {
                 ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(h.max_count));
-                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, true))) return rc;   // clears
-                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+                bool cleared = false;
+                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
+                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
             }
         }
     }
