@@ -504,7 +504,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
 constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
-constexpr uint32_t kGlobalRegions = 4096;     // footprints over more regions go to the global list
+constexpr uint32_t kGlobalRegions = 512;      // footprints over more regions go to the global list
 
 // Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
 // function a*col + b*row + c.
@@ -927,8 +927,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // Region counters touched by atomics are padded to one 128-B L2 line each:
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
-constexpr uint32_t kSerialRegions = 16;      // footprints over up to this many regions: lane-serial
-constexpr uint32_t kSerialBatch = 8;         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
+constexpr uint32_t kBinBatch = 4;            // cells per lane per binning round (their atomics in flight together)         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -948,7 +947,7 @@ static_assert(sizeof(RegionEntry) == 64, "RegionEntry must be 64 bytes");
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
     RegionEntry* list;       // [n_regions * cap] entries by slot
-    uint32_t* global_list;   // [T]
+    RegionEntry* global_list;   // [T] entries of the footprints over > kGlobalRegions regions
     const uint32_t* order;   // [n_regions] slot -> region (x | y << 16), the render launch order (null: raster)
     const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
     uint32_t cap;            // list capacity per region
@@ -1066,121 +1065,93 @@ __global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restric
         if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
     }
 
-    __shared__ float4 s_e[4][kPrepThreads];        // relaxed edges and box (big triangles)
-    __shared__ uint2 s_rect[kPrepThreads];         // (x0 | x1 << 16, y0 | y1 << 16)
-    __shared__ uint32_t s_big[kPrepThreads];       // big triangles (local index)
-    __shared__ uint32_t s_cum[kPrepThreads];       // inclusive prefix of their cell counts
-    __shared__ uint32_t s_wave[kPrepWaves];
-    __shared__ uint32_t s_max;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const unsigned long long lt = (1ull << lane) - 1ull;
+    // Binning.  Each wave flattens the region rectangles of its 64 triangles
+    // into one list of cells (inclusive scan of the cell counts) and deals
+    // them out kBinBatch per lane per round, so a wave's work does not hinge
+    // on its largest footprint: per round, every lane's region tests, launch
+    // slots, count atomics and entry stores are in flight together.
+    __shared__ float4 s_fp[kPrepWaves][4][64];     // footprint (e0.w = triangle id), per lane
+    __shared__ uint2 s_rect[kPrepWaves][64];       // (x0 | x1 << 16, y0 | y1 << 16)
+    __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the cell counts
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
     const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
-    if (valid && global) bins.global_list[atomicAdd(&bs->global_count, 1u)] = i;
-    const uint32_t wr = x1 - x0 + 1u;
-    const uint32_t cells = has ? wr * (y1 - y0 + 1u) : 0u;
-    const bool big = cells > kSerialRegions;
-    if (tid == 0) s_max = 0u;
-
-    uint32_t my_max = 0;                           // 1 + the largest slot this thread took
-    auto place = [&](uint32_t r, uint32_t slot, float4 e0, float4 e1, float4 e2, float4 bb) {
-        my_max = max(my_max, slot + 1u);
-        if (slot < bins.cap) {
-            RegionEntry* e = bins.list + (size_t)r * bins.cap + slot;
-            e->e0 = e0;
-            e->e1 = e1;
-            e->e2 = e2;
-            e->bb = bb;
-        }
-    };
-    auto cell_pass = [&](float4 e0, float4 e1, float4 e2, uint32_t rx, uint32_t ry) {
-        const float xc = (float)(rx * kRegion) + 15.5f;
-        const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
-        return edges_pass(e0, e1, e2, xc, yc, 15.5f, 15.5f);
-    };
-
-    // Small rectangles, lane-serial, in batches of kSerialBatch cells: the
-    // passing regions first, then their count atomics back to back, then the
-    // entries.  (Batches keep k_prep within 64 VGPRs, so its waves fit the
-    // holes a retiring render wave leaves while the previous frame renders.)
-    if (has && !big) {
-        uint32_t cx = x0, cy = y0;
-        for (uint32_t k0 = 0; k0 < cells; k0 += kSerialBatch) {
-            uint32_t reg[kSerialBatch], slot[kSerialBatch];
-#pragma unroll
-            for (uint32_t k = 0; k < kSerialBatch; ++k) {
-                reg[k] = kEmpty;
-                if (k0 + k < cells) {
-                    if (cell_pass(fp.e0, fp.e1, fp.e2, cx, cy)) reg[k] = slot_of(bins, cy * bins.regions_x + cx);
-                    if (++cx > x1) { cx = x0; ++cy; }
-                }
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kSerialBatch; ++k)
-                slot[k] = reg[k] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[k] * kCounterStride], 1u) : 0u;
-#pragma unroll
-            for (uint32_t k = 0; k < kSerialBatch; ++k)
-                if (reg[k] != kEmpty) place(reg[k], slot[k], fp.e0, fp.e1, fp.e2, fp.bbox);
-        }
+    if (valid && global) {                         // footprint over > kGlobalRegions regions
+        RegionEntry* e = bins.global_list + atomicAdd(&bs->global_count, 1u);
+        e->e0 = fp.e0;
+        e->e1 = fp.e1;
+        e->e2 = fp.e2;
+        e->bb = fp.bbox;
     }
+    uint32_t cum = has ? (x1 - x0 + 1u) * (y1 - y0 + 1u) : 0u;
+#pragma unroll
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)cum, off);
+        if (lane >= off) cum += o;
+    }
+    const uint32_t total = wave_uniform((uint32_t)__builtin_amdgcn_readlane((int)cum, 63));
+    s_fp[wave][0][lane] = fp.e0;
+    s_fp[wave][1][lane] = fp.e1;
+    s_fp[wave][2][lane] = fp.e2;
+    s_fp[wave][3][lane] = fp.bbox;
+    s_rect[wave][lane] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
+    s_cum[wave][lane] = cum;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
-    // Big rectangles: their cells flattened over the whole workgroup.
-    const unsigned long long mb = __ballot(big);
-    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(mb);
-    __syncthreads();
-    uint32_t nbig = 0, bslot = 0;
-    for (uint32_t w = 0; w < kPrepWaves; ++w) {
-        bslot += w < wave ? s_wave[w] : 0u;
-        nbig += s_wave[w];
-    }
-    bslot += (uint32_t)__popcll(mb & lt);
-    if (big) {
-        s_big[bslot] = tid;
-        s_e[0][bslot] = fp.e0;
-        s_e[1][bslot] = fp.e1;
-        s_e[2][bslot] = fp.e2;
-        s_e[3][bslot] = fp.bbox;
-        s_rect[bslot] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
-    }
-    __syncthreads();
-    if (nbig) {                                    // workgroup-uniform
-        if (tid == 0) {
-            uint32_t run = 0;
-            for (uint32_t b = 0; b < nbig; ++b) {
-                const uint2 rc = s_rect[b];
-                run += ((rc.x >> 16) - (rc.x & 0xFFFFu) + 1u) * ((rc.y >> 16) - (rc.y & 0xFFFFu) + 1u);
-                s_cum[b] = run;
+    uint32_t my_max = 0;                           // 1 + the largest slot this lane took
+    for (uint32_t base = 0; base < total; base += 64u * kBinBatch) {
+        uint32_t reg[kBinBatch], own[kBinBatch], slot[kBinBatch];
+#pragma unroll
+        for (uint32_t b = 0; b < kBinBatch; ++b) {
+            const uint32_t c = base + b * 64u + lane;
+            reg[b] = kEmpty;
+            own[b] = 0u;
+            if (c < total) {
+                uint32_t lo = 0, hi = 63u;          // the first lane whose prefix exceeds c
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_cum[wave][mid] > c) hi = mid; else lo = mid + 1u;
+                }
+                const uint2 rc = s_rect[wave][lo];
+                const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+                const uint32_t k = c - (lo ? s_cum[wave][lo - 1u] : 0u);
+                const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
+                const float xc = (float)(rx * kRegion) + 15.5f;
+                const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
+                if (edges_pass(s_fp[wave][0][lo], s_fp[wave][1][lo], s_fp[wave][2][lo], xc, yc, 15.5f, 15.5f)) {
+                    reg[b] = slot_of(bins, ry * bins.regions_x + rx);
+                    own[b] = lo;
+                }
             }
         }
-        __syncthreads();
-        const uint32_t total_cells = s_cum[nbig - 1u];
-        const uint32_t i0 = blockIdx.x * blockDim.x;
-        for (uint32_t c = tid; c < total_cells; c += blockDim.x) {
-            uint32_t lo = 0, hi = nbig - 1u;        // first b with s_cum[b] > c
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_cum[mid] > c) hi = mid; else lo = mid + 1u;
-            }
-            const uint2 rc = s_rect[lo];
-            const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
-            const uint32_t k = c - (lo ? s_cum[lo - 1u] : 0u);
-            const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
-            const float4 e0 = s_e[0][lo], e1 = s_e[1][lo], e2 = s_e[2][lo];
-            if (cell_pass(e0, e1, e2, rx, ry)) {
-                const uint32_t r = slot_of(bins, ry * bins.regions_x + rx);
-                place(r, atomicAdd(&bins.counts[(size_t)r * kCounterStride], 1u), e0, e1, e2, s_e[3][lo]);
+#pragma unroll
+        for (uint32_t b = 0; b < kBinBatch; ++b)
+            slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
+#pragma unroll
+        for (uint32_t b = 0; b < kBinBatch; ++b) {
+            if (reg[b] == kEmpty) continue;
+            my_max = max(my_max, slot[b] + 1u);
+            if (slot[b] < bins.cap) {
+                RegionEntry* e = bins.list + (size_t)reg[b] * bins.cap + slot[b];
+                e->e0 = s_fp[wave][0][own[b]];
+                e->e1 = s_fp[wave][1][own[b]];
+                e->e2 = s_fp[wave][2][own[b]];
+                e->bb = s_fp[wave][3][own[b]];
             }
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
-    // the frame's largest region count (list sizing; > cap flags the overflow)
-    if (my_max) atomicMax(&s_max, my_max);
-    __syncthreads();
-    if (tid == 0 && s_max) {
-        atomicMax(&bs->max_count, s_max);
-        if (s_max > bins.cap) atomicOr(&bs->overflow, 1u);
+    // A region count past the list capacity: the render of that region falls
+    // back to the whole mesh, and the host grows the lists for the next frame
+    // (xrt_read_stats / the sizing read).  No global atomic otherwise.
+    my_max = wave_reduce_u32<true>(my_max);
+    if (lane == 0 && my_max > bins.cap) {
+        atomicMax(&bs->max_count, my_max);
+        atomicOr(&bs->overflow, 1u);
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 4);
 }
@@ -1212,7 +1183,9 @@ struct Cand {
 
 // Region-list entries [base, base + 64): direct 64-B loads; `bound` (the
 // wave-uniform list length or capacity) keeps the reads inside the list.
-__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t n_valid,
+// Candidate k < n_local is the region's entry k, then the global list's.
+__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t n_local,
+                                             const RegionEntry* __restrict__ glob, uint32_t n_valid,
                                              uint32_t base, uint32_t T)
 {
     Cand c;
@@ -1220,7 +1193,7 @@ __device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ lis
     c.valid = k < n_valid;
     c.e0 = c.e1 = c.e2 = c.bb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (c.valid) {                                // lanes past the count load nothing
-        const RegionEntry* e = list + k;
+        const RegionEntry* e = k < n_local ? list + k : glob + (k - n_local);
         c.e0 = e->e0;
         c.e1 = e->e1;
         c.e2 = e->e2;
@@ -1335,7 +1308,7 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
                                                    uint32_t tx0, uint32_t ty0,
                                                    const RegionEntry* __restrict__ local,
                                                    uint32_t n_local,
-                                                   const uint32_t* __restrict__ glob, uint32_t n_glob,
+                                                   const RegionEntry* __restrict__ glob, uint32_t n_glob,
                                                    bool whole_mesh, Fetch fetch, WaveStage& st,
                                                    WaveStats& ws)
 {
@@ -1353,11 +1326,9 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
     hl.init();
     uint32_t tests = 0;
     const uint32_t n_cand = whole_mesh ? T : n_local + n_glob;
-    // One loop over the chunks of all sources (one copy of its body): the
-    // region's entries, then the global list's ids, or every triangle id.
-    const uint32_t local_chunks = whole_mesh ? 0u : (n_local + 63u) / 64u;
-    const uint32_t id_count = whole_mesh ? T : n_glob;
-    const uint32_t chunks = local_chunks + (id_count + 63u) / 64u;
+    // One loop over the chunks (one copy of its body): the region's entries
+    // followed by the global list's, or every triangle id.
+    const uint32_t chunks = (n_cand + 63u) / 64u;
     auto body = [&](const Cand& c) {
         const bool pass = c.valid & edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f) &
                           box_overlaps(c.bb, fx0, fx1, fy0, fy1);
@@ -1373,9 +1344,8 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
     };
     for (uint32_t ci = 0; ci < chunks; ++ci) {
         Cand c;
-        if (ci < local_chunks) c = load_entries(local, n_local, ci * 64u, T);   // wave-uniform switch
-        else c = load_ids(culls, T, id_count, (ci - local_chunks) * 64u,
-                          [&](uint32_t k) { return whole_mesh ? k : glob[k]; });
+        if (!whole_mesh) c = load_entries(local, n_local, glob, n_cand, ci * 64u, T);   // wave-uniform switch
+        else c = load_ids(culls, T, T, ci * 64u, [](uint32_t k) { return k; });
         body(c);
     }
     ws.tile_tests += tests;
@@ -1443,7 +1413,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     uint32_t n_cand = 0;
     if (tx0 < p.width && ty0 < p.row_end) {           // wave-uniform
         const bool whole = n_local > bins.cap;        // the region's list overflowed: whole mesh (exact, slower)
-        const uint32_t* __restrict__ glob = bins.global_list;
+        const RegionEntry* __restrict__ glob = bins.global_list;
         n_cand = whole ? p.num_triangles : n_local + n_glob;
         // candidate k's triangle (the overflow fix-up re-reads the candidates)
         const RegionEntry* __restrict__ lst = local;
@@ -1451,7 +1421,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         const bool all = whole;
         render_binned_tile(p, out, recs, culls, tx0, ty0, local, n_local, glob, n_glob, whole,
                            [=](uint32_t k) {
-                               return all ? k : k < nl ? __float_as_uint(lst[k].e0.w) : glob[k - nl];
+                               return all ? k : __float_as_uint((k < nl ? lst[k] : glob[k - nl]).e0.w);
                            },
                            st, ws);
     }

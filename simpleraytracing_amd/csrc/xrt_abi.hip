@@ -77,7 +77,7 @@ struct FrameSet {
     BinState* last_state = nullptr;    // BinState of the set's last binned frame
     RegionEntry* bin_list = nullptr;   // regions x capacity footprint entries
     size_t bin_list_cap = 0;
-    uint32_t* global_list = nullptr;
+    RegionEntry* global_list = nullptr;
     size_t global_list_cap = 0;
 
     // Completion events ride on the kernel dispatches themselves
