@@ -312,7 +312,8 @@ def main():
             "render_stats": {
                 "hit_rays": stats.hit_rays, "odd_rays": stats.odd_rays, "max_hits": stats.max_hits,
                 "overflow_rays": stats.overflow_rays,
-                "region_candidates": stats.candidates, "wave_tile_tests": stats.tile_tests,
+                "region_candidates": stats.candidates, "global_triangles": stats.global_triangles,
+                "wave_tile_tests": stats.tile_tests,
                 "ray_triangle_tests_per_ray": stats.tile_tests * 64 / max(stats.rays, 1),
             },
             "cpu_baseline": None,

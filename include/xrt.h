@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 1
+#define XRT_ABI_VERSION 2
 
 typedef enum xrt_status {
     XRT_OK = 0,
@@ -94,6 +94,7 @@ typedef struct xrt_stats {
     double kernel_ms;       /* device time of the main render kernel (HIP events) */
     uint64_t candidates;    /* TILED: triangles kept by the region footprint test, summed over regions */
     uint64_t tile_tests;    /* triangle tests issued per 8x8 wave tile (64 ray-triangle tests each) */
+    uint64_t global_triangles; /* BINNED: footprints too large for the region lists (every region's candidates) */
 } xrt_stats;
 
 typedef struct xrt_context xrt_context;

@@ -64,6 +64,7 @@ class Stats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("candidates", _u64),
         ("tile_tests", _u64),
+        ("global_triangles", _u64),
     ]
 
     def as_dict(self):

@@ -504,7 +504,10 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
 constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
-constexpr uint32_t kGlobalRegions = 512;      // footprints over more regions go to the global list
+#ifndef XRT_GLOBAL_REGIONS
+#define XRT_GLOBAL_REGIONS 4096
+#endif
+constexpr uint32_t kGlobalRegions = XRT_GLOBAL_REGIONS;   // footprints over more regions go to the global list
 
 // Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
 // function a*col + b*row + c.

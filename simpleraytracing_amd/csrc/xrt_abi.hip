@@ -470,16 +470,16 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     FrameSet& fs = ctx->sets[ctx->next_set];
     // Where the preparation runs (DESIGN.md "Pipelining"; XRT_PIPELINE selects
     // the others for A/B):
-    //   2 (default) on the caller's stream as an any-order dispatch: its AQL
-    //     packet has no barrier bit, so it runs beside the previous frame's
-    //     render, and the render behind it (barrier bit) waits for both --
-    //     the ordering is the queue's, with no host wait and no cross-queue event;
-    //   1 on the context's prep stream, the host waiting for its completion
-    //     before it launches the render;
+    //   1 (default) on the context's prep stream, beside the previous frame's
+    //     render; the host waits for its completion before it launches the
+    //     render (no cross-queue event on the render queue);
+    //   2 on the caller's stream as an any-order dispatch (no barrier bit in
+    //     its AQL packet).  Measured: it did not overlap the previous render
+    //     on ROCm 7.2 -- the same per-frame time as serial;
     //   0 serial on the caller's stream.
     static const int pipeline = [] {
         const char* e = std::getenv("XRT_PIPELINE");
-        return e ? std::atoi(e) : 2;
+        return e ? std::atoi(e) : 1;
     }();
     hipStream_t ps = pipeline == 1 ? ctx->prep_stream : stream;
     unsigned prep_flags = pipeline == 2 ? hipExtAnyOrderLaunch : 0u;
@@ -877,6 +877,7 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
             stats->max_hits = std::max(stats->max_hits, b.max_hits);
         }
     }
+    stats->global_triangles = 0;
     float ms = 0.0f;
     if (!ctx->last_t0 || hipEventElapsedTime(&ms, ctx->last_t0, ctx->last_t1) != hipSuccess) ms = 0.0f;
     stats->kernel = (uint32_t)ctx->last_kernel;
@@ -884,6 +885,7 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     if (fs && fs->binned && fs->last_state) {
         BinState bs = {};
         XRT_HIP(ctx, hipMemcpy(&bs, fs->last_state, sizeof bs, hipMemcpyDeviceToHost));
+        stats->global_triangles = bs.global_count;
         if (bs.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
             ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(bs.max_count));
     }
