@@ -442,8 +442,26 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
     return XRT_OK;
 }
 
-int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
-                   float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream)
+// A frame between its preparation (enqueued) and its render launch.  Split so
+// that a multi-device render can enqueue every device's preparation before it
+// waits for any (xrt_render_rows_multi).
+struct PendingFrame {
+    FrameSet* fs = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t prep_done = nullptr;    // host waits for it before the launch (prep stream)
+    int kernel = XRT_KERNEL_AUTO;
+    bool binned = false;
+    uint32_t rows = 0, rx = 0, ry = 0;
+    dim3 grid;
+    RenderParams p;
+    Outputs out;
+    BinBuffers bins = {};
+    BinState* bin_ctl = nullptr;
+    HostClock::time_point t_call;
+};
+
+int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
+                  float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream, PendingFrame& pf)
 {
     int rc = check_camera(ctx, cam, row_begin, row_end);
     if (rc) return rc;
@@ -557,9 +575,41 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
             }
         }
     }
+    pf.fs = &fs;
+    pf.stream = stream;
+    pf.prep_done = rows > 0 ? prep_done : nullptr;
+    pf.kernel = kernel;
+    pf.binned = binned;
+    pf.rows = rows;
+    pf.rx = rx;
+    pf.ry = ry;
+    pf.grid = grid;
+    pf.p = p;
+    pf.out = out;
+    pf.bins = bins;
+    pf.bin_ctl = bin_ctl;
+    pf.t_call = t_call;
+    return XRT_OK;
+}
+
+int launch_frame(xrt_context* ctx, PendingFrame& pf)
+{
+    FrameSet& fs = *pf.fs;
+    hipStream_t stream = pf.stream;
+    const int kernel = pf.kernel;
+    const bool binned = pf.binned;
+    const uint32_t rows = pf.rows, rx = pf.rx, ry = pf.ry;
+    const dim3 grid = pf.grid;
+    const RenderParams& p = pf.p;
+    const Outputs& out = pf.out;
+    const BinBuffers& bins = pf.bins;
+    BinState* bin_ctl = pf.bin_ctl;
+    const auto t_call = pf.t_call;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
     // The render is launched once the preparation is complete (host-side
     // order; the caller's queue never waits on the prep queue).
-    if (rows > 0 && prep_done) {
+    if (pf.prep_done) {
+        hipEvent_t prep_done = pf.prep_done;
         const auto t = HostClock::now();
         XRT_HIP(ctx, hipEventSynchronize(prep_done));
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
@@ -628,6 +678,14 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     ctx->pending = true;
     ctx->last_kernel = kernel;
     return XRT_OK;
+}
+
+int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
+                   float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream)
+{
+    PendingFrame pf;
+    int rc = prepare_frame(ctx, cam, row_begin, row_end, d_image, d_lbuffer, d_u8, stream, pf);
+    return rc ? rc : launch_frame(ctx, pf);
 }
 
 }  // namespace
