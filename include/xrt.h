@@ -173,6 +173,48 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
 int xrt_timing_begin(xrt_context* ctx);
 int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches);
 
+/* --- multi-GPU: row strips + RCCL root gather (one process) --------------- */
+
+/*
+ * The image split into contiguous row strips over several devices, as the
+ * reference's parallel drivers split the pixel index space: rows_per = H / n,
+ * the remainder going to the first strips (src/main-pthreads-rows.cxx:311-334).
+ * Strip g renders on devices[g]; the strips' planes are gathered into device
+ * 0's frame with grouped ncclSend / ncclRecv over xGMI -- the analogue of the
+ * MPI root gather of src/main-mpi.cxx:855-881 -- on one communicator per device
+ * (ncclCommInitAll).  A device listed more than once (rehearsing the strip
+ * logic on fewer GPUs) gathers with device copies instead.
+ */
+typedef struct xrt_multi xrt_multi;
+
+int xrt_multi_create(const int* devices, int num_devices, xrt_multi** out);
+void xrt_multi_destroy(xrt_multi* m);
+const char* xrt_multi_last_error(const xrt_multi* m);
+int xrt_multi_num_devices(const xrt_multi* m);
+/* The mesh, replicated on every device (xrt_upload_mesh). */
+int xrt_multi_upload_mesh(xrt_multi* m, const float* triangles, uint64_t num_triangles);
+int xrt_multi_set_kernel(xrt_multi* m, int kernel);
+
+/*
+ * Renders the whole camera->height x width frame as strips and gathers it into
+ * HOST buffers (any may be NULL).  Synchronous.  `stats` sums the devices'.
+ * renderLoop over n GPUs == xrt_render_rows_multi(m, cam, image, ...).
+ */
+int xrt_render_rows_multi(xrt_multi* m, const xrt_camera* camera, float* image, float* lbuffer,
+                          uint8_t* image_u8, xrt_stats* stats);
+
+/*
+ * The same into device-0 DEVICE buffers (full-frame planes; NULL planes are
+ * neither rendered nor gathered), ordered on device 0's HIP stream `stream`.
+ * Asynchronous: the next frame's strips render while this frame's gather is
+ * in flight (double-buffered strip planes).
+ */
+int xrt_render_rows_multi_device(xrt_multi* m, const xrt_camera* camera, float* d_image,
+                                 float* d_lbuffer, uint8_t* d_image_u8, void* stream);
+
+/* Waits for the last frame's gathers; the devices' statistics, summed. */
+int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
+
 /* --- diagnostics (device probes of the exact device code paths) ----------- */
 
 /*

@@ -22,7 +22,7 @@ from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F
                    XRT_KERNEL_BRUTE, XRT_KERNEL_TILED)
 
 __all__ = [
-    "Camera", "Stats", "Context", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
+    "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
     "XRT_KERNEL_BINNED",
 ]
@@ -198,3 +198,71 @@ class Context:
         self._check(self._lib.xrt_probe_math(self._ctx, int(op), _fptr(x), _fptr(out), x.size),
                     "xrt_probe_math")
         return out
+
+
+class MultiContext:
+    """xrt_multi: row strips over several devices, gathered into device 0's
+    frame with RCCL (include/xrt.h, "multi-GPU").  A device listed twice
+    rehearses the strip logic on one GPU (device-copy gather)."""
+
+    def __init__(self, devices):
+        self._lib = _abi.load()
+        self._m = _abi._MultiP()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        rc = self._lib.xrt_multi_create(arr, len(devices), ctypes.byref(self._m))
+        if rc != _abi.XRT_OK:
+            raise XrtError(rc, self._lib.xrt_multi_last_error(None).decode())
+        self.devices = list(devices)
+
+    def close(self):
+        if self._m:
+            self._lib.xrt_multi_destroy(self._m)
+            self._m = _abi._MultiP()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != _abi.XRT_OK:
+            raise XrtError(rc, f"{what}: {self._lib.xrt_multi_last_error(self._m).decode()}")
+
+    def upload_mesh(self, tris: np.ndarray):
+        tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        self._check(self._lib.xrt_multi_upload_mesh(self._m, _fptr(tris), len(tris)), "xrt_multi_upload_mesh")
+
+    def set_kernel(self, kernel: int):
+        self._check(self._lib.xrt_multi_set_kernel(self._m, int(kernel)), "xrt_multi_set_kernel")
+
+    def render(self, cam: Camera, image=True, lbuffer=True, u8=True):
+        """The whole frame, gathered to the host: (image, lbuffer, u8, stats)."""
+        n = cam.width * cam.height
+        img = np.empty(n, np.float32) if image else None
+        lb = np.empty(n, np.float32) if lbuffer else None
+        u = np.empty(n, np.uint8) if u8 else None
+        st = Stats()
+        rc = self._lib.xrt_render_rows_multi(self._m, ctypes.byref(cam),
+                                             _fptr(img) if img is not None else None,
+                                             _fptr(lb) if lb is not None else None,
+                                             _u8ptr(u) if u is not None else None, ctypes.byref(st))
+        self._check(rc, "xrt_render_rows_multi")
+        return img, lb, u, st
+
+    def render_device(self, cam: Camera, d_image: int, d_lbuffer: int, d_u8: int, stream: int = 0):
+        """Into device-0 planes (raw pointers), ordered on device 0's stream; asynchronous."""
+        rc = self._lib.xrt_render_rows_multi_device(self._m, ctypes.byref(cam), d_image or None,
+                                                    d_lbuffer or None, d_u8 or None, stream or None)
+        self._check(rc, "xrt_render_rows_multi_device")
+
+    def read_stats(self) -> Stats:
+        st = Stats()
+        self._check(self._lib.xrt_multi_read_stats(self._m, ctypes.byref(st)), "xrt_multi_read_stats")
+        return st

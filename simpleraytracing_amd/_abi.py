@@ -75,7 +75,12 @@ class _Context(ctypes.Structure):
     pass
 
 
+class _Multi(ctypes.Structure):
+    pass
+
+
 _CtxP = ctypes.POINTER(_Context)
+_MultiP = ctypes.POINTER(_Multi)
 
 # name -> (restype, argtypes); every symbol declared in include/xrt.h
 XRT_SYMBOLS = {
@@ -105,6 +110,16 @@ XRT_SYMBOLS = {
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
+    "xrt_multi_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_MultiP)]),
+    "xrt_multi_destroy": (None, [_MultiP]),
+    "xrt_multi_last_error": (ctypes.c_char_p, [_MultiP]),
+    "xrt_multi_num_devices": (ctypes.c_int, [_MultiP]),
+    "xrt_multi_upload_mesh": (ctypes.c_int, [_MultiP, _fp, _u64]),
+    "xrt_multi_set_kernel": (ctypes.c_int, [_MultiP, ctypes.c_int]),
+    "xrt_render_rows_multi": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _fp, _fp, _u8p,
+                                             ctypes.POINTER(Stats)]),
+    "xrt_render_rows_multi_device": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _vp, _vp, _vp, _vp]),
+    "xrt_multi_read_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(Stats)]),
 }
 
 # every C symbol declared in include/xrt_host.h

@@ -930,7 +930,9 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // Region counters touched by atomics are padded to one 128-B L2 line each:
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
-constexpr uint32_t kBinBatch = 4;            // cells per lane per binning round (their atomics in flight together)         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
+constexpr uint32_t kBinBatch = 4;            // queued pairs per lane per commit round (their atomics in flight together)
+constexpr uint32_t kBinSmall = 64;           // region rectangles up to this many cells are flattened over the wave
+constexpr uint32_t kBinQueue = 256;          // passing (region, triangle) pairs queued per wave before a commit         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -1016,7 +1018,7 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
 constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 
-__global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restrict__ tris, uint32_t T,
+__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
@@ -1068,14 +1070,20 @@ __global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restric
         if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
     }
 
-    // Binning.  Each wave flattens the region rectangles of its 64 triangles
-    // into one list of cells (inclusive scan of the cell counts) and deals
-    // them out kBinBatch per lane per round, so a wave's work does not hinge
-    // on its largest footprint: per round, every lane's region tests, launch
-    // slots, count atomics and entry stores are in flight together.
+    // Binning, per wave, in two phases.  (1) Test: every cell of the wave's
+    // 64 region rectangles against its triangle's relaxed edges -- VALU and
+    // LDS only; the cells of rectangles up to kBinSmall cells are flattened
+    // over the wave (inclusive scan of the counts, a binary search per cell),
+    // larger rectangles are walked by the whole wave one after the other --
+    // and the passing (region, triangle) pairs appended to a wave-local queue.
+    // (2) Commit: the queue dealt kBinBatch pairs per lane per round, each
+    // round's launch slots, count atomics and entry stores in flight together.
+    // A full queue is committed early.
     __shared__ float4 s_fp[kPrepWaves][4][64];     // footprint (e0.w = triangle id), per lane
     __shared__ uint2 s_rect[kPrepWaves][64];       // (x0 | x1 << 16, y0 | y1 << 16)
-    __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the cell counts
+    __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the small cell counts
+    __shared__ uint32_t s_qreg[kPrepWaves][kBinQueue];   // passing pairs: region
+    __shared__ uint8_t s_qown[kPrepWaves][kBinQueue];    //                owner lane
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
@@ -1087,7 +1095,9 @@ __global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restric
         e->e2 = fp.e2;
         e->bb = fp.bbox;
     }
-    uint32_t cum = has ? (x1 - x0 + 1u) * (y1 - y0 + 1u) : 0u;
+    const uint32_t cells = has ? (x1 - x0 + 1u) * (y1 - y0 + 1u) : 0u;
+    const bool big = cells > kBinSmall;
+    uint32_t cum = big ? 0u : cells;
 #pragma unroll
     for (uint32_t off = 1; off < 64u; off <<= 1) {
         const uint32_t o = (uint32_t)__shfl_up((int)cum, off);
@@ -1106,47 +1116,99 @@ __global__ __launch_bounds__(kPrepThreads, 8) void k_prep(const float* __restric
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
-    for (uint32_t base = 0; base < total; base += 64u * kBinBatch) {
-        uint32_t reg[kBinBatch], own[kBinBatch], slot[kBinBatch];
+    uint32_t queued = 0;                           // wave-uniform queue length
+    auto commit = [&]() {
+        for (uint32_t base = 0; base < queued; base += 64u * kBinBatch) {
+            uint32_t reg[kBinBatch], own[kBinBatch], slot[kBinBatch];
 #pragma unroll
-        for (uint32_t b = 0; b < kBinBatch; ++b) {
-            const uint32_t c = base + b * 64u + lane;
-            reg[b] = kEmpty;
-            own[b] = 0u;
-            if (c < total) {
-                uint32_t lo = 0, hi = 63u;          // the first lane whose prefix exceeds c
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_cum[wave][mid] > c) hi = mid; else lo = mid + 1u;
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
+                const uint32_t q = base + b * 64u + lane;
+                reg[b] = kEmpty;
+                own[b] = 0u;
+                if (q < queued) {
+                    reg[b] = slot_of(bins, s_qreg[wave][q]);
+                    own[b] = s_qown[wave][q];
                 }
-                const uint2 rc = s_rect[wave][lo];
-                const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
-                const uint32_t k = c - (lo ? s_cum[wave][lo - 1u] : 0u);
-                const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
-                const float xc = (float)(rx * kRegion) + 15.5f;
-                const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
-                if (edges_pass(s_fp[wave][0][lo], s_fp[wave][1][lo], s_fp[wave][2][lo], xc, yc, 15.5f, 15.5f)) {
-                    reg[b] = slot_of(bins, ry * bins.regions_x + rx);
-                    own[b] = lo;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b)
+                slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
+                if (reg[b] == kEmpty) continue;
+                my_max = max(my_max, slot[b] + 1u);
+                if (slot[b] < bins.cap) {
+                    RegionEntry* e = bins.list + (size_t)reg[b] * bins.cap + slot[b];
+                    e->e0 = s_fp[wave][0][own[b]];
+                    e->e1 = s_fp[wave][1][own[b]];
+                    e->e2 = s_fp[wave][2][own[b]];
+                    e->bb = s_fp[wave][3][own[b]];
                 }
             }
         }
-#pragma unroll
-        for (uint32_t b = 0; b < kBinBatch; ++b)
-            slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
-#pragma unroll
-        for (uint32_t b = 0; b < kBinBatch; ++b) {
-            if (reg[b] == kEmpty) continue;
-            my_max = max(my_max, slot[b] + 1u);
-            if (slot[b] < bins.cap) {
-                RegionEntry* e = bins.list + (size_t)reg[b] * bins.cap + slot[b];
-                e->e0 = s_fp[wave][0][own[b]];
-                e->e1 = s_fp[wave][1][own[b]];
-                e->e2 = s_fp[wave][2][own[b]];
-                e->bb = s_fp[wave][3][own[b]];
+        __builtin_amdgcn_wave_barrier();          // the queue is refilled after every lane read it
+        queued = 0;
+    };
+    // append the passing cells of one round (pass, region rx/ry, owner) to the queue
+    auto enqueue = [&](bool pass, uint32_t rx, uint32_t ry, uint32_t owner) {
+        const unsigned long long m = __ballot(pass);
+        if (!m) return;
+        if (queued + 64u > kBinQueue) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            commit();
+        }
+        if (pass) {
+            const uint32_t q = queued + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            s_qreg[wave][q] = ry * bins.regions_x + rx;
+            s_qown[wave][q] = (uint8_t)owner;
+        }
+        queued += (uint32_t)__popcll(m);
+    };
+    auto cell_pass = [&](uint32_t owner, uint32_t rx, uint32_t ry) {
+        const float xc = (float)(rx * kRegion) + 15.5f;
+        const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
+        return edges_pass(s_fp[wave][0][owner], s_fp[wave][1][owner], s_fp[wave][2][owner], xc, yc, 15.5f, 15.5f);
+    };
+    // (1a) small rectangles, flattened over the wave
+    for (uint32_t base = 0; base < total; base += 64u) {
+        const uint32_t c = base + lane;
+        bool pass = false;
+        uint32_t rx = 0, ry = 0, lo = 0;
+        if (c < total) {
+            uint32_t hi = 63u;                        // the first lane whose prefix exceeds c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_cum[wave][mid] > c) hi = mid; else lo = mid + 1u;
             }
+            const uint2 rc = s_rect[wave][lo];
+            const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+            const uint32_t k = c - (lo ? s_cum[wave][lo - 1u] : 0u);
+            rx = bx0 + k % bw;
+            ry = by0 + k / bw;
+            pass = cell_pass(lo, rx, ry);
+        }
+        enqueue(pass, rx, ry, lo);
+    }
+    // (1b) large rectangles, one at a time over the whole wave
+    unsigned long long mbig = __ballot(big);
+    while (mbig) {                                 // wave-uniform
+        const uint32_t owner = (uint32_t)__builtin_ctzll(mbig);
+        mbig &= mbig - 1ull;
+        const uint2 rc = s_rect[wave][owner];
+        const uint32_t bx0 = rc.x & 0xFFFFu, bw = (rc.x >> 16) - bx0 + 1u, by0 = rc.y & 0xFFFFu;
+        const uint32_t n = wave_uniform(bw * ((rc.y >> 16) - by0 + 1u));
+        for (uint32_t base = 0; base < n; base += 64u) {
+            const uint32_t k = base + lane;
+            const uint32_t rx = bx0 + k % bw, ry = by0 + k / bw;
+            enqueue(k < n && cell_pass(owner, rx, ry), rx, ry, owner);
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    commit();                                      // (2)
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
     // A region count past the list capacity: the render of that region falls
     // back to the whole mesh, and the host grows the lists for the next frame

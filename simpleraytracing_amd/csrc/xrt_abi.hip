@@ -1123,3 +1123,5 @@ void xrt_host_expf_batch(const float* in, float* outp, uint64_t n)
 }
 
 }  // extern "C"
+
+#include "xrt_multi.inc"
