@@ -8,7 +8,8 @@ mkdir -p $OUT
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-      -I../../include -DXRT_KERNEL_NS=xrt_$name $flags -shared -o $OUT/libxrt_$name.so xrt_abi.hip &
+      -I../../include -DXRT_KERNEL_NS=xrt_$name $flags -shared -o $OUT/libxrt_$name.so xrt_abi.hip \
+      -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
 done
 wait
 ls -la $OUT
