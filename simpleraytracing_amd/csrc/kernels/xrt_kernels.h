@@ -938,16 +938,19 @@ constexpr uint32_t kBinQueue = 256;          // passing (region, triangle) pairs
 // wave of slot s loads its count and list without first looking up which
 // region it renders (order[s], loaded alongside); k_prep maps region -> slot
 // through rank.
-// Region-list entry: the triangle's conservative footprint, copied into every
-// region list it joins, so a render wave reads its candidates with one
-// coalesced 64-B load per lane (no id -> footprint indirection).
+// Region-list entry: the triangle's conservative footprint and its record,
+// copied into every region list it joins, so a render wave reads a candidate
+// with no indirection: the footprint into registers (the tile test) and the
+// record straight into LDS by DMA (the survivors' exact tests), both issued
+// together.
 struct alignas(16) RegionEntry {
     float4 e0;   // relaxed edge 0 (a, b, c); w = triangle id (bits)
     float4 e1;   // relaxed edge 1
     float4 e2;   // relaxed edge 2
     float4 bb;   // footprint box (xmin, xmax, ymin, ymax)
+    TriRec rec;  // Ray::intersect's ray-independent terms (k_prep)
 };
-static_assert(sizeof(RegionEntry) == 64, "RegionEntry must be 64 bytes");
+static_assert(sizeof(RegionEntry) == 128, "RegionEntry must be 128 bytes");
 
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
@@ -1038,13 +1041,13 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
     Footprint fp;
+    TriRec r = {};
     if (valid) {
         const float* P = tris + 9ull * i;
         float p1x = P[0], p1y = P[1], p1z = P[2];
         float p2x = P[3], p2y = P[4], p2z = P[5];
         float p3x = P[6], p3y = P[7], p3z = P[8];
         // Exactly the reference's f32 operations (Ray.cxx:86-87, 102, 112, 122).
-        TriRec r;
         r.e1x = p2x - p1x; r.e1y = p2y - p1y; r.e1z = p2z - p1z;
         r.e2x = p3x - p1x; r.e2y = p3y - p1y; r.e2z = p3z - p1z;
         r.tvx = p.ox - p1x; r.tvy = p.oy - p1y; r.tvz = p.oz - p1z;
@@ -1079,7 +1082,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     // (2) Commit: the queue dealt kBinBatch pairs per lane per round, each
     // round's launch slots, count atomics and entry stores in flight together.
     // A full queue is committed early.
-    __shared__ float4 s_fp[kPrepWaves][4][64];     // footprint (e0.w = triangle id), per lane
+    __shared__ float4 s_fp[kPrepWaves][8][64];     // footprint (e0.w = triangle id) and record, per lane
     __shared__ uint2 s_rect[kPrepWaves][64];       // (x0 | x1 << 16, y0 | y1 << 16)
     __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the small cell counts
     __shared__ uint32_t s_qreg[kPrepWaves][kBinQueue];   // passing pairs: region
@@ -1094,6 +1097,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
         e->e1 = fp.e1;
         e->e2 = fp.e2;
         e->bb = fp.bbox;
+        e->rec = r;
     }
     const uint32_t cells = has ? (x1 - x0 + 1u) * (y1 - y0 + 1u) : 0u;
     const bool big = cells > kBinSmall;
@@ -1108,6 +1112,13 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     s_fp[wave][1][lane] = fp.e1;
     s_fp[wave][2][lane] = fp.e2;
     s_fp[wave][3][lane] = fp.bbox;
+    {
+        const float4* q = reinterpret_cast<const float4*>(&r);
+        s_fp[wave][4][lane] = q[0];
+        s_fp[wave][5][lane] = q[1];
+        s_fp[wave][6][lane] = q[2];
+        s_fp[wave][7][lane] = q[3];
+    }
     s_rect[wave][lane] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
     s_cum[wave][lane] = cum;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1138,11 +1149,9 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
                 if (reg[b] == kEmpty) continue;
                 my_max = max(my_max, slot[b] + 1u);
                 if (slot[b] < bins.cap) {
-                    RegionEntry* e = bins.list + (size_t)reg[b] * bins.cap + slot[b];
-                    e->e0 = s_fp[wave][0][own[b]];
-                    e->e1 = s_fp[wave][1][own[b]];
-                    e->e2 = s_fp[wave][2][own[b]];
-                    e->bb = s_fp[wave][3][own[b]];
+                    float4* e = reinterpret_cast<float4*>(bins.list + (size_t)reg[b] * bins.cap + slot[b]);
+#pragma unroll
+                    for (uint32_t w = 0; w < 8; ++w) e[w] = s_fp[wave][w][own[b]];
                 }
             }
         }
@@ -1239,6 +1248,23 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
 constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
 constexpr uint32_t kWavesPerRegion = 16u;               // one 8x8 tile per wave
 
+// The records of one chunk's candidates in the wave's LDS slice, DMA'd from
+// global memory (global_load_lds, 16 B per lane per instruction): r[q][k] =
+// quarter q of candidate k's TriRec.
+struct WaveStage {
+    float4 r[4][64];
+};
+
+// Candidate record -> LDS: lane k's 64 B land at r[0..3][k] (exec-masked).
+__device__ __forceinline__ void dma_record(WaveStage& st, const TriRec* rec)
+{
+    const float4* q = reinterpret_cast<const float4*>(rec);
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        __builtin_amdgcn_global_load_lds((const void*)(q + w),
+                                         (__attribute__((address_space(3))) void*)&st.r[w][0], 16, 0, 0);
+}
+
 // A chunk of 64 candidates as seen by one wave: this lane's candidate.
 struct Cand {
     uint32_t j;          // triangle id (always a valid index)
@@ -1251,7 +1277,7 @@ struct Cand {
 // Candidate k < n_local is the region's entry k, then the global list's.
 __device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t n_local,
                                              const RegionEntry* __restrict__ glob, uint32_t n_valid,
-                                             uint32_t base, uint32_t T)
+                                             uint32_t base, uint32_t T, WaveStage& st)
 {
     Cand c;
     const uint32_t k = base + (threadIdx.x & 63u);
@@ -1263,6 +1289,7 @@ __device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ lis
         c.e1 = e->e1;
         c.e2 = e->e2;
         c.bb = e->bb;
+        dma_record(st, &e->rec);
     }
     const uint32_t j = __float_as_uint(c.e0.w);
     c.j = c.valid && j < T ? j : 0u;
@@ -1271,8 +1298,8 @@ __device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ lis
 
 // Candidates by triangle id (global list, whole-mesh fallback): the SoA cull planes.
 template <typename Fetch>
-__device__ __forceinline__ Cand load_ids(const float4* __restrict__ culls, uint32_t T, uint32_t n,
-                                         uint32_t base, Fetch fetch)
+__device__ __forceinline__ Cand load_ids(const float4* __restrict__ culls, const TriRec* __restrict__ recs,
+                                         uint32_t T, uint32_t n, uint32_t base, Fetch fetch, WaveStage& st)
 {
     Cand c;
     const uint32_t k = base + (threadIdx.x & 63u);
@@ -1283,14 +1310,10 @@ __device__ __forceinline__ Cand load_ids(const float4* __restrict__ culls, uint3
     c.e0 = culls[(size_t)T + c.j];
     c.e1 = culls[2 * (size_t)T + c.j];
     c.e2 = culls[3 * (size_t)T + c.j];
+    if (c.valid) dma_record(st, recs + c.j);
     return c;
 }
 
-// The survivors of one chunk, staged in the wave's LDS slice (one TriRec each,
-// in ascending candidate order).
-struct WaveStage {
-    float4 r[4][64];     // r[q][s] = quarter q of survivor s's TriRec
-};
 
 __device__ __forceinline__ void test_staged_pair(const WaveStage& st, uint32_t s0, uint32_t s1,
                                                  bool two, float dx, float dy, float dz, HitList& hl)
@@ -1333,37 +1356,28 @@ __device__ __forceinline__ void test_staged_one(const WaveStage& st, uint32_t s,
     hl.push_if(h, t);
 }
 
-// One chunk's survivors (mask m, this lane's candidate j): gather their
-// records into LDS, then test them two at a time.
-__device__ __forceinline__ void test_survivors(WaveStage& st, const TriRec* __restrict__ recs,
-                                               unsigned long long m, bool pass, uint32_t j, float dx,
-                                               float dy, float dz, HitList& hl)
+// One chunk's survivors (candidate mask m): their records are in the wave's
+// LDS slice (the chunk's DMA); tested one at a time as broadcast reads.
+__device__ __forceinline__ void test_survivors(const WaveStage& st, unsigned long long m, float dx, float dy,
+                                               float dz, HitList& hl)
 {
-    const uint32_t idx =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (pass) {
-        const float4* q = reinterpret_cast<const float4*>(recs + j);
-        const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
-        st.r[0][idx] = r0;
-        st.r[1][idx] = r1;
-        st.r[2][idx] = r2;
-        st.r[3][idx] = r3;
-    }
-    // the wave reads what its own lanes wrote: LDS keeps one wave's order
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t ns = (uint32_t)__popcll(m);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the records' DMA has landed
 #if XRT_STAGED_PAIRS
-    for (uint32_t s = 0; s < ns; s += 2u) {
-        const bool two = s + 1u < ns;
-        test_staged_pair(st, s, two ? s + 1u : s, two, dx, dy, dz, hl);
+    while (m) {
+        const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+        const bool two = m != 0ull;
+        const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m) : k0;
+        m &= m - 1ull;
+        test_staged_pair(st, k0, k1, two, dx, dy, dz, hl);
     }
 #else
-    for (uint32_t s = 0; s < ns; ++s) test_staged_one(st, s, dx, dy, dz, hl);
+    while (m) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+        test_staged_one(st, k, dx, dy, dz, hl);
+    }
 #endif
-    // the next chunk overwrites the slice only after every lane's reads
-    __builtin_amdgcn_wave_barrier();
 }
 
 template <typename Fetch>
@@ -1390,7 +1404,7 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
     HitList hl;
     hl.init();
     uint32_t tests = 0;
-    const uint32_t n_cand = whole_mesh ? T : n_local + n_glob;
+    const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole_mesh ? T : n_local + n_glob;
     // One loop over the chunks (one copy of its body): the region's entries
     // followed by the global list's, or every triangle id.
     const uint32_t chunks = (n_cand + 63u) / 64u;
@@ -1405,12 +1419,12 @@ __device__ __forceinline__ void render_binned_tile(const RenderParams& p, const 
             have_ray = true;
         }
         if (ablation(p) & kAblateExact) return;
-        test_survivors(st, recs, m, pass, c.j, dx, dy, dz, hl);
+        test_survivors(st, m, dx, dy, dz, hl);
     };
     for (uint32_t ci = 0; ci < chunks; ++ci) {
         Cand c;
-        if (!whole_mesh) c = load_entries(local, n_local, glob, n_cand, ci * 64u, T);   // wave-uniform switch
-        else c = load_ids(culls, T, T, ci * 64u, [](uint32_t k) { return k; });
+        if (!whole_mesh) c = load_entries(local, n_local, glob, n_cand, ci * 64u, T, st);   // wave-uniform switch
+        else c = load_ids(culls, recs, T, T, ci * 64u, [](uint32_t k) { return k; }, st);
         body(c);
     }
     ws.tile_tests += tests;
