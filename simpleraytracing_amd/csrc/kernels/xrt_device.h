@@ -54,8 +54,8 @@
 #define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
                           // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
-#ifndef XRT_STAGED_PAIRS
-#define XRT_STAGED_PAIRS 0   // binned render: LDS-staged survivors tested two at a time (else one)
+#ifndef XRT_STAGE
+#define XRT_STAGE 128     // binned render: candidates staged in LDS per round (16 KB)
 #endif
 #ifndef XRT_PREP_THREADS
 #define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)

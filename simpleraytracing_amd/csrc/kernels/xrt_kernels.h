@@ -1231,121 +1231,85 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
 }
 
 // ---------------------------------------------------------------------------
-// k_render_binned: wave-per-tile render over the binned region lists.
+// k_render_binned: the render over the binned region lists.
 //
-// One wavefront owns one 8x8 ray tile of a 32x32 region.  Its candidates are
-// the region's list entries (64-B footprints, read directly: the first 64
-// speculatively, beside the count) followed by the global list (ids, read
-// through the SoA cull planes).  Per chunk of 64 candidates, one lane per
-// candidate tests the tile rectangle against the footprint box and the three
-// relaxed edges and a ballot keeps the survivors.  The survivors' triangle
-// records are gathered in ONE vector-load round trip into the wave's slice of
-// LDS, then read back as wave-uniform broadcasts and tested exactly for all
-// 64 rays, two at a time -- no dependent memory round trip per survivor.
-// Rays are generated when the first survivor appears (pixel offsets from the
-// frame's tables); a tile without survivors stores the miss constants.
+// A workgroup of kTileWaves (4) waves renders one 32x8 row of a region's 8x8
+// tiles, one tile per wave.  The region's candidates -- its list entries
+// followed by the global list's, each a 128-B footprint + triangle record --
+// are staged into LDS by DMA (global_load_lds, no registers), kBinStage at a
+// time and structure-of-arrays, by the workgroup's waves together; then each
+// wave tests its tile rectangle against the staged footprints (one candidate
+// per lane, conflict-free reads), a ballot keeps the survivors, and each
+// survivor's record is read back as a wave-uniform broadcast and tested
+// exactly for the tile's 64 rays.  One global round trip after the region's
+// count, and each region's entries are read once per workgroup.  Rays are
+// generated when the first survivor appears (pixel offsets from the frame's
+// tables); a tile without survivors stores the miss constants.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
 constexpr uint32_t kWavesPerRegion = 16u;               // one 8x8 tile per wave
+constexpr uint32_t kBinStage = XRT_STAGE;                  // candidates staged per round
+static_assert(kBinStage % 64u == 0u && 8u % kTileWaves == 0u, "staging layout");
 
-// The records of one chunk's candidates in the wave's LDS slice, DMA'd from
-// global memory (global_load_lds, 16 B per lane per instruction): r[q][k] =
-// quarter q of candidate k's TriRec.
-struct WaveStage {
-    float4 r[4][64];
+// The staged candidates: q[0..3][k] = footprint (e0 -- w = id --, e1, e2, box),
+// q[4..7][k] = the TriRec, of staged candidate k.
+struct RegionStage {
+    float4 q[8][kBinStage];
 };
 
-// Candidate record -> LDS: lane k's 64 B land at r[0..3][k] (exec-masked).
-__device__ __forceinline__ void dma_record(WaveStage& st, const TriRec* rec)
+// Candidates [base, base + cnt) into the stage.  Candidate k is the region's
+// entry k (k < n_local), then the global list's; wave w copies quarters
+// [w * 8 / kTileWaves, (w + 1) * 8 / kTileWaves) of every candidate.
+__device__ __forceinline__ void stage_entries(RegionStage& st, const RegionEntry* __restrict__ local,
+                                              uint32_t n_local, const RegionEntry* __restrict__ glob,
+                                              uint32_t base, uint32_t cnt)
 {
-    const float4* q = reinterpret_cast<const float4*>(rec);
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_in_block();
+    constexpr uint32_t kPer = 8u / kTileWaves;
+    for (uint32_t g = 0; g < cnt; g += 64u) {
+        if (g + lane < cnt) {
+            const uint32_t k = base + g + lane;
+            const float4* src = reinterpret_cast<const float4*>(k < n_local ? local + k : glob + (k - n_local));
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
-        __builtin_amdgcn_global_load_lds((const void*)(q + w),
-                                         (__attribute__((address_space(3))) void*)&st.r[w][0], 16, 0, 0);
-}
-
-// A chunk of 64 candidates as seen by one wave: this lane's candidate.
-struct Cand {
-    uint32_t j;          // triangle id (always a valid index)
-    bool valid;
-    float4 e0, e1, e2, bb;
-};
-
-// Region-list entries [base, base + 64): direct 64-B loads; `bound` (the
-// wave-uniform list length or capacity) keeps the reads inside the list.
-// Candidate k < n_local is the region's entry k, then the global list's.
-__device__ __forceinline__ Cand load_entries(const RegionEntry* __restrict__ list, uint32_t n_local,
-                                             const RegionEntry* __restrict__ glob, uint32_t n_valid,
-                                             uint32_t base, uint32_t T, WaveStage& st)
-{
-    Cand c;
-    const uint32_t k = base + (threadIdx.x & 63u);
-    c.valid = k < n_valid;
-    c.e0 = c.e1 = c.e2 = c.bb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (c.valid) {                                // lanes past the count load nothing
-        const RegionEntry* e = k < n_local ? list + k : glob + (k - n_local);
-        c.e0 = e->e0;
-        c.e1 = e->e1;
-        c.e2 = e->e2;
-        c.bb = e->bb;
-        dma_record(st, &e->rec);
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t q = wave * kPer + i;
+                __builtin_amdgcn_global_load_lds((const void*)(src + q),
+                                                 (__attribute__((address_space(3))) void*)&st.q[q][g], 16, 0, 0);
+            }
+        }
     }
-    const uint32_t j = __float_as_uint(c.e0.w);
-    c.j = c.valid && j < T ? j : 0u;
-    return c;
 }
 
-// Candidates by triangle id (global list, whole-mesh fallback): the SoA cull planes.
-template <typename Fetch>
-__device__ __forceinline__ Cand load_ids(const float4* __restrict__ culls, const TriRec* __restrict__ recs,
-                                         uint32_t T, uint32_t n, uint32_t base, Fetch fetch, WaveStage& st)
+// The same from the whole mesh (a region whose list overflowed): candidate k
+// is triangle k, its footprint from the SoA cull planes, its record from recs.
+__device__ __forceinline__ void stage_mesh(RegionStage& st, const float4* __restrict__ culls,
+                                           const TriRec* __restrict__ recs, uint32_t T, uint32_t base,
+                                           uint32_t cnt)
 {
-    Cand c;
-    const uint32_t k = base + (threadIdx.x & 63u);
-    c.valid = k < n;
-    const uint32_t j = c.valid ? fetch(k) : 0u;
-    c.j = j < T ? j : 0u;
-    c.bb = culls[c.j];
-    c.e0 = culls[(size_t)T + c.j];
-    c.e1 = culls[2 * (size_t)T + c.j];
-    c.e2 = culls[3 * (size_t)T + c.j];
-    if (c.valid) dma_record(st, recs + c.j);
-    return c;
-}
-
-
-__device__ __forceinline__ void test_staged_pair(const WaveStage& st, uint32_t s0, uint32_t s1,
-                                                 bool two, float dx, float dy, float dz, HitList& hl)
-{
-    const float4 a0 = st.r[0][s0], a1 = st.r[1][s0], a2 = st.r[2][s0], a3 = st.r[3][s0];
-    const float4 b0 = st.r[0][s1], b1 = st.r[1][s1], b2 = st.r[2][s1], b3 = st.r[3][s1];
-    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (a3.x)
-    float det0, u0, v0, det1, u1, v1;
-    mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
-                  det0, u0, v0);
-    mt_numerators(dx, dy, dz, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w,
-                  det1, u1, v1);
-    float i0, i1;
-    if (__builtin_expect(__ballot(!(rcp_newton_exact_for(det0) && rcp_newton_exact_for(det1))) == 0ull, 1)) {
-        i0 = rcp_newton(det0);
-        i1 = rcp_newton(det1);
-    } else {
-        i0 = inv_det_of(det0);
-        i1 = inv_det_of(det1);
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_in_block();
+    constexpr uint32_t kPer = 8u / kTileWaves;
+    for (uint32_t g = 0; g < cnt; g += 64u) {
+        if (g + lane < cnt) {
+            const uint32_t j = base + g + lane;
+            const float4* rec = reinterpret_cast<const float4*>(recs + j);
+            const float4* src[8] = {culls + (size_t)T + j, culls + 2 * (size_t)T + j, culls + 3 * (size_t)T + j,
+                                    culls + j, rec, rec + 1, rec + 2, rec + 3};
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t q = wave * kPer + i;
+                __builtin_amdgcn_global_load_lds((const void*)src[q],
+                                                 (__attribute__((address_space(3))) void*)&st.q[q][g], 16, 0, 0);
+            }
+        }
     }
-    bool h0, h1;
-    const float t0 = mt_finish_inv(det0, i0, u0, v0, a3.x, h0);
-    const float t1 = mt_finish_inv(det1, i1, u1, v1, b3.x, h1);
-    hl.push_if(h0, t0);
-    hl.push_if(two && h1, t1);
 }
 
-__device__ __forceinline__ void test_staged_one(const WaveStage& st, uint32_t s, float dx, float dy,
+__device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
                                                 float dz, HitList& hl)
 {
-    const float4 a0 = st.r[0][s], a1 = st.r[1][s], a2 = st.r[2][s];
-    const float tnum = st.r[3][s].x;
+    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[7].x)
+    const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k];
+    const float tnum = st.q[7][k].x;
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
@@ -1356,102 +1320,17 @@ __device__ __forceinline__ void test_staged_one(const WaveStage& st, uint32_t s,
     hl.push_if(h, t);
 }
 
-// One chunk's survivors (candidate mask m): their records are in the wave's
-// LDS slice (the chunk's DMA); tested one at a time as broadcast reads.
-__device__ __forceinline__ void test_survivors(const WaveStage& st, unsigned long long m, float dx, float dy,
-                                               float dz, HitList& hl)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the records' DMA has landed
-#if XRT_STAGED_PAIRS
-    while (m) {
-        const uint32_t k0 = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1ull;
-        const bool two = m != 0ull;
-        const uint32_t k1 = two ? (uint32_t)__builtin_ctzll(m) : k0;
-        m &= m - 1ull;
-        test_staged_pair(st, k0, k1, two, dx, dy, dz, hl);
-    }
-#else
-    while (m) {
-        const uint32_t k = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1ull;
-        test_staged_one(st, k, dx, dy, dz, hl);
-    }
-#endif
-}
-
-template <typename Fetch>
-__device__ __forceinline__ void render_binned_tile(const RenderParams& p, const Outputs& out,
-                                                   const TriRec* __restrict__ recs,
-                                                   const float4* __restrict__ culls,
-                                                   uint32_t tx0, uint32_t ty0,
-                                                   const RegionEntry* __restrict__ local,
-                                                   uint32_t n_local,
-                                                   const RegionEntry* __restrict__ glob, uint32_t n_glob,
-                                                   bool whole_mesh, Fetch fetch, WaveStage& st,
-                                                   WaveStats& ws)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t T = p.num_triangles;
-    const uint32_t col = tx0 + (lane & 7u);
-    const uint32_t row = ty0 + (lane >> 3);
-    const bool active = col < p.width && row < p.row_end;
-    const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
-    const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
-
-    float dx = 1.0f, dy = 0.0f, dz = 0.0f;
-    bool have_ray = false;                        // wave-uniform
-    HitList hl;
-    hl.init();
-    uint32_t tests = 0;
-    const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole_mesh ? T : n_local + n_glob;
-    // One loop over the chunks (one copy of its body): the region's entries
-    // followed by the global list's, or every triangle id.
-    const uint32_t chunks = (n_cand + 63u) / 64u;
-    auto body = [&](const Cand& c) {
-        const bool pass = c.valid & edges_pass(c.e0, c.e1, c.e2, xc, yc, 3.5f, 3.5f) &
-                          box_overlaps(c.bb, fx0, fx1, fy0, fy1);
-        const unsigned long long m = __ballot(pass);
-        if (!m) return;
-        tests += (uint32_t)__popcll(m);
-        if (!have_ray) {
-            if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
-            have_ray = true;
-        }
-        if (ablation(p) & kAblateExact) return;
-        test_survivors(st, m, dx, dy, dz, hl);
-    };
-    for (uint32_t ci = 0; ci < chunks; ++ci) {
-        Cand c;
-        if (!whole_mesh) c = load_entries(local, n_local, glob, n_cand, ci * 64u, T, st);   // wave-uniform switch
-        else c = load_ids(culls, recs, T, T, ci * 64u, [](uint32_t k) { return k; }, st);
-        body(c);
-    }
-    ws.tile_tests += tests;
-    if (have_ray) {
-        finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
-        return;
-    }
-    // No survivor: every ray of the tile misses (main.cxx:700-718 with no hit).
-    ws.rays += (uint32_t)__popcll(__ballot(active));
-    if (!active || (ablation(p) & kAblateStores)) return;
-    const size_t o = (size_t)(row - p.row_begin) * p.width + col;
-    if (out.image) out.image[o] = 80.0f;
-    if (out.lbuffer) out.lbuffer[o] = __builtin_inff();
-    if (out.image_u8) out.image_u8[o] = 255u;
-}
-
-// Binned render: kTileWaves waves per workgroup, one 8x8 tile each, regions
-// in the launch order of bins.order; each wave stores its own statistics
-// record, so no wave waits for another.  8 waves per SIMD: the tile waves are
-// latency-bound, and occupancy is what hides it.
+// Binned render: kTileWaves waves per workgroup (one 32x8 row of a region's
+// tiles), regions in the launch order of bins.order; each wave stores its own
+// statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
+// occupancy is what hides it.
 __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins, const BinState* __restrict__ bs)
 {
     static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
                   "a workgroup's waves render tiles of one region");
-    __shared__ WaveStage s_stage[kTileWaves];
+    __shared__ RegionStage st;
     const uint64_t t_start = block_start_stamp();
 #if XRT_XCD_REMAP
     // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
@@ -1470,11 +1349,9 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 #else
     const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
 #endif
-    const uint32_t slot = g / kWavesPerRegion;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
-    WaveStage& st = s_stage[wave_in_block()];
-    // the count and the region are independent loads (lists are by slot)
-    const RegionEntry* __restrict__ local = bins.list + (size_t)slot * bins.cap;
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
     const uint32_t n_glob = wave_uniform(bs->global_count);
     uint32_t reg_x, reg_y;
@@ -1486,23 +1363,73 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         reg_x = slot % bins.regions_x;
         reg_y = slot / bins.regions_x;
     }
+    const RegionEntry* __restrict__ local = bins.list + (size_t)slot * bins.cap;
+    const RegionEntry* __restrict__ glob = bins.global_list;
+    const uint32_t T = p.num_triangles;
+    const bool whole = n_local > bins.cap;         // the region's list overflowed: whole mesh (exact, slower)
+    const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole ? T : n_local + n_glob;
+
     const uint32_t tx0 = reg_x * kRegion + (tile & 3u) * 8u;
     const uint32_t ty0 = p.row_begin + reg_y * kRegion + (tile >> 2) * 8u;
+    const bool tile_live = tx0 < p.width && ty0 < p.row_end;       // wave-uniform
+    const uint32_t col = tx0 + (lane & 7u);
+    const uint32_t row = ty0 + (lane >> 3);
+    const bool active = col < p.width && row < p.row_end;
+    const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
+    const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
+
+    float dx = 1.0f, dy = 0.0f, dz = 0.0f;
+    bool have_ray = false;                         // wave-uniform
+    HitList hl;
+    hl.init();
+    uint32_t tests = 0;
+    // every wave of the workgroup takes part in every round's staging and barriers
+    for (uint32_t base = 0; base < n_cand; base += kBinStage) {
+        const uint32_t cnt = min(kBinStage, n_cand - base);
+        if (base) __syncthreads();                 // the previous round's reads are done
+        if (whole) stage_mesh(st, culls, recs, T, base, cnt);
+        else stage_entries(st, local, n_local, glob, base, cnt);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
+        __syncthreads();                           // and every wave's
+        if (!tile_live) continue;
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64u) {
+            const uint32_t k = k0 + lane;
+            bool pass = false;
+            if (k < cnt)
+                pass = edges_pass(st.q[0][k], st.q[1][k], st.q[2][k], xc, yc, 3.5f, 3.5f) &
+                       box_overlaps(st.q[3][k], fx0, fx1, fy0, fy1);
+            unsigned long long m = __ballot(pass);
+            if (!m) continue;
+            tests += (uint32_t)__popcll(m);
+            if (!have_ray) {
+                if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
+                have_ray = true;
+            }
+            if (ablation(p) & kAblateExact) continue;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                test_staged_one(st, k0 + b, dx, dy, dz, hl);
+            }
+        }
+    }
     WaveStats ws = {};
-    uint32_t n_cand = 0;
-    if (tx0 < p.width && ty0 < p.row_end) {           // wave-uniform
-        const bool whole = n_local > bins.cap;        // the region's list overflowed: whole mesh (exact, slower)
-        const RegionEntry* __restrict__ glob = bins.global_list;
-        n_cand = whole ? p.num_triangles : n_local + n_glob;
-        // candidate k's triangle (the overflow fix-up re-reads the candidates)
-        const RegionEntry* __restrict__ lst = local;
-        const uint32_t nl = whole ? 0u : n_local;
-        const bool all = whole;
-        render_binned_tile(p, out, recs, culls, tx0, ty0, local, n_local, glob, n_glob, whole,
-                           [=](uint32_t k) {
-                               return all ? k : __float_as_uint((k < nl ? lst[k] : glob[k - nl]).e0.w);
-                           },
-                           st, ws);
+    ws.tile_tests = tests;
+    if (tile_live) {
+        if (have_ray) {
+            const uint32_t nl = whole ? 0u : n_local;
+            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, [=](uint32_t k) {
+                return whole ? k : __float_as_uint((k < nl ? local[k] : glob[k - nl]).e0.w);
+            });
+        } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
+            ws.rays += (uint32_t)__popcll(__ballot(active));
+            if (active && !(ablation(p) & kAblateStores)) {
+                const size_t o = (size_t)(row - p.row_begin) * p.width + col;
+                if (out.image) out.image[o] = 80.0f;
+                if (out.lbuffer) out.lbuffer[o] = __builtin_inff();
+                if (out.image_u8) out.image_u8[o] = 255u;
+            }
+        }
     }
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
