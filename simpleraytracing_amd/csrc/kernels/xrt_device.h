@@ -54,6 +54,9 @@
 #define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
                           // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
+#ifndef XRT_STAGED_PAIRS
+#define XRT_STAGED_PAIRS 1   // binned render: survivors tested two at a time (independent chains)
+#endif
 #ifndef XRT_STAGE
 #define XRT_STAGE 128     // binned render: candidates staged in LDS per round (16 KB)
 #endif
