@@ -55,7 +55,10 @@
                           // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
 #ifndef XRT_STAGED_PAIRS
-#define XRT_STAGED_PAIRS 1   // binned render: survivors tested two at a time (independent chains)
+#define XRT_STAGED_PAIRS 0   // binned render: survivors tested two at a time (A/B: spills at 8 waves/SIMD, slower)
+#endif
+#ifndef XRT_RENDER_WAVES
+#define XRT_RENDER_WAVES 8   // binned render: minimum waves per SIMD (8 = 64 VGPRs)
 #endif
 #ifndef XRT_STAGE
 #define XRT_STAGE 128     // binned render: candidates staged in LDS per round (16 KB)

@@ -1352,7 +1352,7 @@ __device__ __forceinline__ void test_staged_pair(const RegionStage& st, uint32_t
 // tiles), regions in the launch order of bins.order; each wave stores its own
 // statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
 // occupancy is what hides it.
-__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_render_binned(
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(XRT_RENDER_WAVES, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins, const BinState* __restrict__ bs)
 {
