@@ -1,25 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- Mrays/s of the X-ray render path (BASELINE.json metric).
 
-A step renders frames of the configured size (default dragon.ply, 2048x2048,
-every ray tested against the mesh, outputs f32 image + f32 L-buffer + u8
-image).  The mesh is resident in HBM before the timed region; the per-frame
-triangle preparation (binning) and the render kernel are inside it.
+A step renders one frame (default dragon.ply; outputs f32 image + f32
+L-buffer + u8 image, every ray against the mesh through the exact
+Moller-Trumbore test of its culled candidates).  The mesh is resident in HBM
+before the timed region; the per-frame triangle preparation (binning) and the
+render are inside it.
 
-  --mode frames  (default) weak scaling: every rank renders one whole frame per
-                 step on its own GPU; no collective in the timed loop (the path
-                 shards by frame and by row, with no exchange step).  With
-                 N > 1 an untimed frame is also rendered as row strips and
-                 gathered to rank 0 with RCCL; it must equal rank 0's frame
-                 bit for bit ("gather_check").
-  --mode strips  strong scaling: one frame per step split into row strips
+  one GPU (default): dragon.ply 2048x2048 frames (BASELINE configs[2]).
+  --gpus N > 1 (default --mode strips, 4096x4096: BASELINE configs[3]):
+                 strong scaling -- one frame per step split into row strips
                  (rows_per = H/N, remainder to the first, as
-                 main-pthreads-rows.cxx:311-334) and gathered to rank 0 with
-                 one RCCL gather over xGMI inside the timed loop.
+                 main-pthreads-rows.cxx:311-334); every rank but 0 sends its
+                 strip's L-buffer (misses coded XRT_MISS_TRANSIT, 4 B per
+                 pixel) to rank 0 over RCCL, which receives it into its frame
+                 and expands the image and u8 planes from it; frame k's gather
+                 overlaps frame k+1's render.  The gathered frame is checked bit
+                 for bit against rank 0's own single-device render after timing.
+  --mode frames  weak scaling: every rank renders whole frames, no exchange.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size W H]
                     [--kernel auto|binned|tiled|brute] [--mode frames|strips]
-                    [--tile-mesh n] [--no-cpu-baseline]
+                    [--tile-mesh n] [--no-cpu-baseline] [--dist-backend nccl|gloo]
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -45,9 +47,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--size", type=int, nargs=2, default=[2048, 2048], metavar=("W", "H"))
+    ap.add_argument("--size", type=int, nargs=2, default=None, metavar=("W", "H"),
+                    help="default 2048 2048; 4096 4096 for strips over N > 1 GPUs (BASELINE configs[3])")
     ap.add_argument("--kernel", choices=["auto", "binned", "tiled", "brute"], default="auto")
-    ap.add_argument("--mode", choices=["frames", "strips"], default="frames")
+    ap.add_argument("--mode", choices=["frames", "strips"], default=None,
+                    help="default: frames on one GPU, strips over N > 1")
     ap.add_argument("--mesh", default=os.path.join(ROOT, "data", "dragon.ply"))
     ap.add_argument("--tile-mesh", type=int, default=1,
                     help="n x n tiled copies of the mesh (7 = the 1M-triangle config)")
@@ -175,58 +179,96 @@ def main():
 
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.scenes import tiled_mesh
-    from simpleraytracing_amd.strips import max_strip_pixels, strip_bounds, views
+    from simpleraytracing_amd.strips import strip_bounds
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # N > 1: BASELINE configs[3] -- one frame split into row strips, gathered to rank 0
+    mode = args.mode or ("strips" if world > 1 else "frames")
+    W, H = args.size or ((4096, 4096) if mode == "strips" and world > 1 else (2048, 2048))
     device_index = 0 if args.same_device else local_rank
     torch.cuda.set_device(device_index)
     dev = torch.device("cuda", device_index)
+    nccl = args.dist_backend == "nccl"
     if world > 1:
-        if args.dist_backend == "nccl":
+        if nccl:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
-    def gather_to_root(t, out_list):
-        """dist.gather of a device tensor (RCCL), or staged through the host for gloo."""
-        if args.dist_backend == "nccl":
-            dist.gather(t, out_list, dst=0)
-            return out_list
-        host = t.cpu()
-        lst = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
-        dist.gather(host, lst, dst=0)
-        return lst
-
-    W, H = args.size
     tris = xrt.load_ply(args.mesh)
     if args.tile_mesh > 1:
         tris = tiled_mesh(tris, args.tile_mesh)
     T = len(tris)
     cam = xrt.camera_for_mesh(tris, W, H)
-    strips = args.mode == "strips"
+    strips = mode == "strips"
+    gathering = strips and world > 1
     r0, r1 = strip_bounds(H, world, rank) if strips else (0, H)
-    n_max = max_strip_pixels(W, H, world) if strips else W * H
+    bounds = [strip_bounds(H, world, g) for g in range(world)]
 
     ctx = xrt.Context(device_index)
     ctx.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
                     "tiled": xrt.XRT_KERNEL_TILED, "binned": xrt.XRT_KERNEL_BINNED}[args.kernel])
     ctx.upload_mesh(tris)
-
-    # one packed buffer: [image f32 | L-buffer f32 | u8]
-    strip = torch.zeros(9 * n_max, dtype=torch.uint8, device=dev)
-    img, lb, u8 = views(strip, n_max)
-    gathered = [torch.empty_like(strip) for _ in range(world)] if (strips and world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
 
+    # Rank 0 (and every rank in frames mode) holds a whole frame's planes.  In
+    # strips mode the other ranks render L-buffer strips with misses coded
+    # XRT_MISS_TRANSIT (4 B per pixel: image and u8 are functions of L) into
+    # two alternating buffers and send them to rank 0, which receives them into
+    # its frame's L plane and expands the image and u8 planes from them
+    # (xrt_expand_rows_device) -- frame k's gather overlaps frame k+1's render.
+    root = rank == 0 or not strips
+    if root:
+        img = torch.zeros(W * H, dtype=torch.float32, device=dev)
+        lb = torch.zeros(W * H, dtype=torch.float32, device=dev)
+        u8 = torch.zeros(W * H, dtype=torch.uint8, device=dev)
+    else:
+        ctx.set_miss_code(xrt.XRT_MISS_TRANSIT)
+        tbufs = [torch.zeros((r1 - r0) * W, dtype=torch.float32, device=dev) for _ in range(2)]
+        pending = [None, None]
+    rest = (H - bounds[0][1]) * W            # rows of strips 1 .. n-1 on rank 0
+    o0 = bounds[0][1] * W
+    frame_no = [0]
+
+    def send_strip(t):
+        if nccl:
+            return dist.isend(t, dst=0)
+        dist.send(t.cpu(), dst=0)             # gloo rehearsal: staged through the host
+        return None
+
+    def recv_strips():
+        if nccl:
+            ops = [dist.P2POp(dist.irecv, lb[b * W:e * W], g) for g, (b, e) in enumerate(bounds) if g]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()                      # the current stream waits for the receives
+        else:
+            for g, (b, e) in enumerate(bounds):
+                if g:
+                    host = torch.empty((e - b) * W, dtype=torch.float32)
+                    dist.recv(host, src=g)
+                    lb[b * W:e * W].copy_(host, non_blocking=False)
+
     def step():
-        ctx.render_rows_device(cam, r0, r1, img.data_ptr(), lb.data_ptr(), u8.data_ptr(),
-                               stream.cuda_stream)
-        if strips and world > 1:
-            gather_to_root(strip, gathered)
+        k = frame_no[0]
+        frame_no[0] += 1
+        if root:
+            o = r0 * W
+            ctx.render_rows_device(cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
+                                   u8.data_ptr() + o, stream.cuda_stream)
+            if gathering:
+                recv_strips()
+                ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0,
+                                       u8.data_ptr() + o0, stream.cuda_stream)
+        else:
+            b = k % 2
+            if pending[b] is not None:
+                pending[b].wait()             # the send of frame k-2 has read this buffer
+            ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
+            pending[b] = send_strip(tbufs[b])
 
     for _ in range(args.warmup):
         step()
@@ -238,6 +280,10 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if not root:
+        for p_ in pending:
+            if p_ is not None:
+                p_.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -246,33 +292,20 @@ def main():
     kernel_ms, launches = ctx.timing_end()
     stats = ctx.read_stats()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if nccl else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    # untimed: the row-strip + RCCL gather path must reproduce rank 0's frame
+    # untimed: the gathered frame against rank 0's own render of the whole frame
     gather = None
-    if world > 1 and not strips:
-        from simpleraytracing_amd.strips import assemble
-        g0, g1 = strip_bounds(H, world, rank)
-        gn = max_strip_pixels(W, H, world)
-        gbuf = torch.zeros(9 * gn, dtype=torch.uint8, device=dev)
-        gi, gl, gu = views(gbuf, gn)
-        glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        ctx.render_rows_device(cam, g0, g1, gi.data_ptr(), gl.data_ptr(), gu.data_ptr(), stream.cuda_stream)
-        glist = gather_to_root(gbuf, glist)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0:
-            full = assemble([x.cpu().numpy() for x in glist], W, H)
-            mine = (img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy())
-            ok = all(np.array_equal(a.view(np.uint8), b.view(np.uint8)) for a, b in zip(full, mine))
-            gather = {"bit_exact_vs_rank0_frame": bool(ok), "striped_frame_plus_gather_ms": gather_ms,
-                      "bytes_gathered": 9 * W * H}
+    if gathering and rank == 0:
+        full = ctx.render_rows(cam)
+        ok = (np.array_equal(img.cpu().numpy().view(np.uint32), full[0].view(np.uint32))
+              and np.array_equal(lb.cpu().numpy().view(np.uint32), full[1].view(np.uint32))
+              and np.array_equal(u8.cpu().numpy(), full[2]))
+        gather = {"bit_exact_vs_single_device_frame": bool(ok),
+                  "bytes_gathered_per_step": 4 * rest, "transit": "L-buffer strips, misses as XRT_MISS_TRANSIT"}
 
     result = None
     if rank == 0:
@@ -302,12 +335,14 @@ def main():
             "config": {
                 "workload": workload,
                 "kernel": {0: "auto", 1: "brute", 2: "tiled", 3: "binned"}[stats.kernel],
-                "mode": args.mode,
+                "mode": mode,
                 "triangles": T,
                 "image": [W, H],
                 "rays_per_step": W * H * (1 if strips else world),
-                "parallelism": (f"row strips x{world}, RCCL gather to rank 0" if strips
-                                else f"one frame per rank x{world} (weak)"),
+                "parallelism": (f"row strips x{world}, L-buffer strips gathered to rank 0 over "
+                                f"{'RCCL (xGMI)' if nccl else 'gloo (host-staged rehearsal)'}, overlapped with "
+                                f"the next frame's render" if gathering
+                                else f"one frame per rank x{world} (weak)" if world > 1 else "one GPU"),
             },
             "roofline": roofline,
             "render_stats": {

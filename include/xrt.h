@@ -173,6 +173,29 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
 int xrt_timing_begin(xrt_context* ctx);
 int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches);
 
+/* --- strips in transit ---------------------------------------------------- */
+
+/*
+ * The L-buffer alone determines a pixel's image and 8-bit values (image =
+ * shade(L) for a hit, 80 for a miss), except that a miss and a ray with a t =
+ * +inf "hit" both have L = +inf.  Strips gathered to another device travel as
+ * L-buffers with misses written as XRT_MISS_TRANSIT (a signalling NaN no render
+ * produces): 4 bytes per pixel instead of 9.
+ */
+#define XRT_MISS_TRANSIT 0x7F800001u
+
+/* L-buffer bits of a miss for later renders: 0 (+inf, the default) or XRT_MISS_TRANSIT. */
+int xrt_set_miss_code(xrt_context* ctx, uint32_t bits);
+
+/*
+ * Expands num_pixels of a received L-buffer (misses as XRT_MISS_TRANSIT) in
+ * place: d_image / d_u8 (either may be NULL) get the pixels' image and 8-bit
+ * values and the miss codes become +inf -- bit-identical to a direct render.
+ * Asynchronous on `stream` (device buffers).
+ */
+int xrt_expand_rows_device(xrt_context* ctx, uint64_t num_pixels, float* d_lbuffer, float* d_image,
+                           uint8_t* d_image_u8, void* stream);
+
 /* --- multi-GPU: row strips + RCCL root gather (one process) --------------- */
 
 /*

@@ -163,6 +163,16 @@ class Context:
         self._check(self._lib.xrt_read_stats(self._ctx, ctypes.byref(st)), "xrt_read_stats")
         return st
 
+    def set_miss_code(self, bits: int):
+        """L-buffer bits of a miss in later renders: 0 (+inf) or XRT_MISS_TRANSIT."""
+        self._check(self._lib.xrt_set_miss_code(self._ctx, int(bits)), "xrt_set_miss_code")
+
+    def expand_rows_device(self, num_pixels: int, d_lbuffer: int, d_image: int, d_u8: int, stream: int = 0):
+        """A received transit L-buffer into image / u8 planes, in place (device pointers)."""
+        rc = self._lib.xrt_expand_rows_device(self._ctx, int(num_pixels), d_lbuffer or None, d_image or None,
+                                              d_u8 or None, stream or None)
+        self._check(rc, "xrt_expand_rows_device")
+
     def timing_begin(self):
         self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
 

@@ -24,6 +24,8 @@ XRT_KERNEL_BRUTE = 1
 XRT_KERNEL_TILED = 2
 XRT_KERNEL_BINNED = 3
 
+XRT_MISS_TRANSIT = 0x7F800001
+
 XRT_PROBE_EXPF = 0
 XRT_PROBE_SQRTF = 1
 XRT_PROBE_RCP = 2
@@ -110,6 +112,8 @@ XRT_SYMBOLS = {
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
+    "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
+    "xrt_expand_rows_device": (ctypes.c_int, [_CtxP, _u64, _vp, _vp, _vp, _vp]),
     "xrt_multi_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_MultiP)]),
     "xrt_multi_destroy": (None, [_MultiP]),
     "xrt_multi_last_error": (ctypes.c_char_p, [_MultiP]),

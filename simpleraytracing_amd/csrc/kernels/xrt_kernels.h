@@ -79,7 +79,17 @@ struct Outputs {
     // SGPRs for the whole kernel.
     const __attribute__((address_space(4))) RenderParams* frame;
     PixelOffsets off;          // the frame's pixel-offset tables (k_prep)
+    // L-buffer value of a ray that hits nothing: +inf (the reference's
+    // z_buffer), or a transit code for strips gathered as L-buffers only
+    // (kMissTransit, expanded on the receiving device by k_expand).
+    float miss_l;
 };
+
+// A signalling NaN no render produces (path lengths are >= 0, +inf, or x86's
+// default NaN): marks "no hit" in L-buffer strips in transit, where +inf
+// would be ambiguous (a ray with t = +inf hits also has L = +inf, but its
+// image value is 0, not 80).
+constexpr uint32_t kMissTransit = 0x7F800001u;
 
 // A pixel inside the image for the offset tables (lanes of a partial tile
 // outside it compute a ray nobody stores).
@@ -418,7 +428,7 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
     wave_stats(ws, active, hl.n, odd, overflow);
     // main.cxx:700-718
     float distance = 0.0f;
-    float lval = __builtin_inff();
+    float lval = out.miss_l;
     if (hl.n > 0) {
         if (!odd) distance = hl.path_length();
         lval = distance;
@@ -1465,13 +1475,63 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
             if (active && !(ablation(p) & kAblateStores)) {
                 const size_t o = (size_t)(row - p.row_begin) * p.width + col;
                 if (out.image) out.image[o] = 80.0f;
-                if (out.lbuffer) out.lbuffer[o] = __builtin_inff();
+                if (out.lbuffer) out.lbuffer[o] = out.miss_l;
                 if (out.image_u8) out.image_u8[o] = 255u;
             }
         }
     }
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
+}
+
+// ---------------------------------------------------------------------------
+// k_expand: a gathered strip's L-buffer (misses as kMissTransit) into the
+// frame's three planes -- image = 80 and u8 = 255 for misses, else the shade
+// of the path length and its LUT, exactly as finish_ray computes them (for a
+// hit the image is shade(L): L is the path length, 0 for an odd count) -- and
+// the miss code back to +inf.  Four pixels per thread.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_expand(float* __restrict__ lbuffer, float* __restrict__ image,
+                                                uint8_t* __restrict__ image_u8, uint64_t n)
+{
+    const uint64_t i0 = 4ull * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (i0 >= n) return;
+    float l[4], img[4];
+    uint8_t u8[4];
+    bool miss[4];
+    const bool full = i0 + 4u <= n && (reinterpret_cast<uintptr_t>(lbuffer + i0) & 15u) == 0u;
+    if (full) {
+        const float4 v = *reinterpret_cast<const float4*>(lbuffer + i0);
+        l[0] = v.x; l[1] = v.y; l[2] = v.z; l[3] = v.w;
+    } else {
+        for (int k = 0; k < 4; ++k) l[k] = i0 + k < n ? lbuffer[i0 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        miss[k] = __float_as_uint(l[k]) == kMissTransit;
+        img[k] = miss[k] ? 80.0f : shade(l[k]);
+        u8[k] = miss[k] ? (uint8_t)255u : lut_u8(img[k]);
+    }
+    if (full) {
+        if (image) *reinterpret_cast<float4*>(image + i0) = make_float4(img[0], img[1], img[2], img[3]);
+        if (image_u8 && (reinterpret_cast<uintptr_t>(image_u8 + i0) & 3u) == 0u)
+            *reinterpret_cast<uint32_t*>(image_u8 + i0) =
+                (uint32_t)u8[0] | ((uint32_t)u8[1] << 8) | ((uint32_t)u8[2] << 16) | ((uint32_t)u8[3] << 24);
+        else if (image_u8)
+            for (int k = 0; k < 4; ++k) image_u8[i0 + k] = u8[k];
+        if (miss[0] | miss[1] | miss[2] | miss[3]) {
+            const float inf = __builtin_inff();
+            *reinterpret_cast<float4*>(lbuffer + i0) = make_float4(miss[0] ? inf : l[0], miss[1] ? inf : l[1],
+                                                                   miss[2] ? inf : l[2], miss[3] ? inf : l[3]);
+        }
+    } else {
+        for (int k = 0; k < 4; ++k) {
+            if (i0 + k >= n) break;
+            if (image) image[i0 + k] = img[k];
+            if (image_u8) image_u8[i0 + k] = u8[k];
+            if (miss[k]) lbuffer[i0 + k] = __builtin_inff();
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------

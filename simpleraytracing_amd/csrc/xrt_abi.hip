@@ -141,6 +141,7 @@ struct xrt_context {
     } bin_key = {};
     static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
+    uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     xrt_camera cull_cam = {};          // camera of the cached cull parameters
     CullParams cull = {};
     bool cull_valid = false;
@@ -526,6 +527,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     out.frame = (const __attribute__((address_space(4))) RenderParams*)fs.frame;
     out.off.v = fs.offsets;
     out.off.u = fs.offsets + cam->height;
+    const uint32_t miss_bits = ctx->miss_code ? ctx->miss_code : 0x7F800000u;   // +inf
+    std::memcpy(&out.miss_l, &miss_bits, sizeof miss_bits);
     const uint32_t n_regions = rows ? rx * ry : 0u;
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
@@ -852,6 +855,28 @@ int xrt_set_kernel(xrt_context* ctx, int kernel)
     if (kernel < XRT_KERNEL_AUTO || kernel > XRT_KERNEL_BINNED)
         return fail(ctx, XRT_ERR_ARGUMENT, "unknown kernel");
     ctx->kernel = kernel;
+    return XRT_OK;
+}
+
+int xrt_set_miss_code(xrt_context* ctx, uint32_t bits)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (bits && bits != kMissTransit) return fail(ctx, XRT_ERR_ARGUMENT, "miss code must be 0 or XRT_MISS_TRANSIT");
+    ctx->miss_code = bits;
+    return XRT_OK;
+}
+
+int xrt_expand_rows_device(xrt_context* ctx, uint64_t num_pixels, float* d_lbuffer, float* d_image,
+                           uint8_t* d_u8, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (num_pixels && !d_lbuffer) return fail(ctx, XRT_ERR_ARGUMENT, "lbuffer is NULL");
+    if (!num_pixels) return XRT_OK;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t threads = (num_pixels + 3) / 4;
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_lbuffer, d_image, d_u8, num_pixels);
+    XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
 

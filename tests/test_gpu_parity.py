@@ -615,3 +615,55 @@ def test_multi_device_pipelined(dragon):
     for k, planes in enumerate(outs):
         for x, y in zip(planes, refs[k % 2][:3]):
             assert np.array_equal(bits(x.cpu().numpy()), bits(y)), k
+
+
+@pytest.mark.parametrize("soup", ["dragon", "corner"])
+def test_transit_expand_equals_direct_render(ctx, dragon, soup):
+    """An L-buffer strip rendered with misses coded XRT_MISS_TRANSIT, expanded by
+    xrt_expand_rows_device, equals the direct render's three planes -- also for
+    the t = +inf hits of the corner soup, whose L is +inf like a miss's but whose
+    image is 0, not 80."""
+    import torch
+    tris = dragon if soup == "dragon" else corner_soup()
+    W, H = (192, 160) if soup == "dragon" else (33, 31)
+    cam = xrt.camera_for_mesh(tris, W, H)
+    ctx.upload_mesh(tris)
+    ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+    ref = ctx.render_rows(cam)
+    dev = torch.device("cuda", ctx.device)
+    lb = torch.full((W * H,), -1.0, device=dev)
+    img = torch.zeros(W * H, device=dev)
+    u8 = torch.zeros(W * H, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_miss_code(xrt._abi.XRT_MISS_TRANSIT)
+    try:
+        ctx.render_rows_device(cam, 0, H, 0, lb.data_ptr(), 0, stream.cuda_stream)
+        coded = lb.cpu().numpy().copy()
+        ctx.expand_rows_device(W * H, lb.data_ptr(), img.data_ptr(), u8.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+    finally:
+        ctx.set_miss_code(0)
+    n_coded = int(np.count_nonzero(coded.view(np.uint32) == xrt._abi.XRT_MISS_TRANSIT))
+    assert n_coded == W * H - ref[3].hit_rays                       # every miss, and only misses
+    assert np.array_equal(bits(img.cpu().numpy()), bits(ref[0]))
+    assert np.array_equal(bits(lb.cpu().numpy()), bits(ref[1]))
+    assert np.array_equal(u8.cpu().numpy(), ref[2])
+
+
+def test_bench_strips_two_ranks_one_gpu(tmp_path):
+    """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0,
+    expanded there) with 2 ranks on the one GPU (gloo, host-staged): the
+    gathered frame is bit-equal to rank 0's single-device render."""
+    import json
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    port = 29500 + (os.getpid() % 1000)
+    cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
+           "--steps", "4", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["config"]["mode"] == "strips" and d["n_gpus"] == 2
+    assert d["gather_check"]["bit_exact_vs_single_device_frame"] is True
