@@ -19,12 +19,12 @@ import numpy as np
 
 from . import _abi
 from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
-                   XRT_KERNEL_BRUTE, XRT_KERNEL_TILED)
+                   XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT)
 
 __all__ = [
     "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
-    "XRT_KERNEL_BINNED",
+    "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT",
 ]
 
 

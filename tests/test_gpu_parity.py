@@ -662,7 +662,9 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path):
            "--gpus", "2", "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
            "--steps", "4", "--warmup", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0:
+        print(r.stderr[-6000:])
+    assert r.returncode == 0
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
     assert d["config"]["mode"] == "strips" and d["n_gpus"] == 2
