@@ -194,44 +194,48 @@ unsigned long long renderLoop(Image& image, const std::vector<TriangleMesh>& mes
     return stats.odd_rays;
 }
 
+// Row strips over num_gpus devices gathered into device 0 with RCCL
+// (xrt_render_rows_multi).  $XRT_MULTI_DEVICES ("0,0" ...) overrides the
+// device list -- a device listed twice rehearses the strip path on one GPU.
 unsigned long long renderLoopMultiGPU(Image& image, const std::vector<TriangleMesh>& meshes,
                                       RayTracerInfo& info, int num_gpus)
 {
-    int available = xrt_device_count();
-    if (num_gpus < 1 || num_gpus > available)
-        throw std::runtime_error("renderLoopMultiGPU: " + std::to_string(num_gpus) + " GPUs requested, " +
-                                 std::to_string(available) + " available");
+    std::vector<int> devices;
+    if (const char* env = std::getenv("XRT_MULTI_DEVICES")) {
+        std::string list(env);
+        for (size_t pos = 0; pos < list.size();) {
+            size_t next = list.find(',', pos);
+            if (next == std::string::npos) next = list.size();
+            devices.push_back(std::atoi(list.substr(pos, next - pos).c_str()));
+            pos = next + 1;
+        }
+    } else {
+        int available = xrt_device_count();
+        if (num_gpus < 1 || num_gpus > available)
+            throw std::runtime_error("renderLoopMultiGPU: " + std::to_string(num_gpus) + " GPUs requested, " +
+                                     std::to_string(available) + " available");
+        for (int g = 0; g < num_gpus; ++g) devices.push_back(g);
+    }
     xrt_camera cam = camera_for(image, meshes, info);
     std::vector<float> soup = mesh0_soup(meshes);
-    const unsigned H = image.getHeight();
-    std::vector<unsigned> begin(num_gpus), end(num_gpus);
-    unsigned rows_per = H / num_gpus, rem = H % num_gpus, next = 0;
-    for (int g = 0; g < num_gpus; ++g) {
-        begin[g] = next;
-        next += rows_per + (g < (int)rem ? 1u : 0u);
-        end[g] = next;
+    // one multi-device context per device list for the process lifetime
+    static std::mutex lock;
+    static std::map<std::vector<int>, xrt_multi*> contexts;
+    std::lock_guard<std::mutex> g(lock);
+    xrt_multi*& m = contexts[devices];
+    if (!m && xrt_multi_create(devices.data(), (int)devices.size(), &m) != XRT_OK) {
+        m = nullptr;
+        throw std::runtime_error(std::string("xrt_multi_create: ") + xrt_multi_last_error(nullptr));
     }
-    std::vector<xrt_stats> stats(num_gpus);
-    std::vector<std::exception_ptr> errors(num_gpus);
-    std::vector<std::thread> threads;
-    for (int g = 0; g < num_gpus; ++g) {
-        threads.emplace_back([&, g]() {
-            try {
-                render_strip(g, cam, soup, begin[g], end[g],
-                             image.getData() + (size_t)begin[g] * image.getWidth(), nullptr, nullptr,
-                             &stats[g]);
-            } catch (...) {
-                errors[g] = std::current_exception();
-            }
-        });
-    }
-    for (auto& t : threads) t.join();
-    for (auto& e : errors)
-        if (e) std::rethrow_exception(e);
-    unsigned long long odd = 0;
-    for (const auto& s : stats) odd += s.odd_rays;
-    report_odd(odd);
-    return odd;
+    auto mcheck = [&](int rc, const char* what) {
+        if (rc != XRT_OK) throw std::runtime_error(std::string(what) + ": " + xrt_multi_last_error(m));
+    };
+    mcheck(xrt_multi_set_kernel(m, kernel_choice()), "xrt_multi_set_kernel");
+    mcheck(xrt_multi_upload_mesh(m, soup.data(), soup.size() / 9), "xrt_multi_upload_mesh");
+    xrt_stats stats;
+    mcheck(xrt_render_rows_multi(m, &cam, image.getData(), nullptr, nullptr, &stats), "xrt_render_rows_multi");
+    report_odd(stats.odd_rays);
+    return stats.odd_rays;
 }
 
 // --- extern "C" helpers (include/xrt_host.h) --------------------------------

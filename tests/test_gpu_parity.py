@@ -669,3 +669,16 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path):
     d = json.loads(line)
     assert d["config"]["mode"] == "strips" and d["n_gpus"] == 2
     assert d["gather_check"]["bit_exact_vs_single_device_frame"] is True
+
+
+def test_cli_multi_gpu_golden_text(tmp_path):
+    """xrt_main -g 2 (renderLoopMultiGPU over xrt_render_rows_multi): strips on a
+    device listed twice (one GPU here), the golden text byte for byte."""
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    (tmp_path / "out").mkdir()
+    env = dict(os.environ, XRT_MULTI_DEVICES="0,0")
+    r = subprocess.run([exe, "-s", "128", "128", "-i", DRAGON, "-f", "d.txt", "-g", "2"], capture_output=True,
+                       text=True, cwd=tmp_path, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    got = (tmp_path / "out" / "d.txt").read_bytes()
+    assert got == open(os.path.join(GOLDEN, "dragon-128x128-serial.txt"), "rb").read()
