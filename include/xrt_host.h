@@ -22,6 +22,14 @@ extern "C" {
 int xrt_host_load_ply(const char* path, float** triangles, uint64_t* num_triangles);
 void xrt_host_free(void* p);
 
+/*
+ * Ray::intersect (src/Ray.cxx:72-124) of the drop-in host class for n pairs:
+ * rays[6*i] = origin, direction (normalised by the Ray constructor as
+ * include/Ray.inl:74-85); triangles[9*i] = p1, p2, p3.  hit[i] = 0/1, t[i] =
+ * distance (0 when no hit).
+ */
+void xrt_host_intersect_batch(const float* rays, const float* triangles, uint64_t n, uint8_t* hit, float* t);
+
 #ifdef __cplusplus
 }
 

@@ -130,6 +130,7 @@ XRT_SYMBOLS = {
 XRT_HOST_SYMBOLS = {
     "xrt_host_load_ply": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_u64)]),
     "xrt_host_free": (None, [_vp]),
+    "xrt_host_intersect_batch": (None, [_fp, _fp, _u64, _u8p, _fp]),
 }
 
 _lib = None

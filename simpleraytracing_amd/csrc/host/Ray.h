@@ -1,11 +1,9 @@
 // Ray.h -- ray of the drop-in host API (include/Ray.h:84-107).
 //
 // The constructor normalises the direction unless its length is zero, as
-// include/Ray.inl:74-85 does.  Ray::intersect runs the render kernel's own
-// device Moller-Trumbore test (xrt_probe_intersect on a lazily created
-// context of device 0 or $XRT_DEVICE); there is no host implementation of the
-// intersection, so single calls pay a device round trip -- renderLoop is the
-// bulk path.  intersect() throws std::runtime_error when no GPU is available.
+// include/Ray.inl:74-85 does.  Ray::intersect is src/Ray.cxx:72-124 on the
+// host (the drop-in class's single-pair utility); renderLoop's kernel is the
+// bulk path.
 #pragma once
 
 #include <vector>
@@ -27,7 +25,7 @@ public:
     void setDirection(const Vec3& d) { m_direction = d / d.getLength(); }
     Vec3 getPointAt(float t) const { return m_origin + m_direction * t; }
 
-    // src/Ray.cxx:72-124 on the device.
+    // src/Ray.cxx:72-124.
     bool intersect(const Triangle& triangle, float& t) const;
 
 private:

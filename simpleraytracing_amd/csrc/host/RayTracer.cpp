@@ -53,6 +53,8 @@ void check(xrt_context* ctx, int rc, const char* what)
 struct DeviceSlot {
     std::mutex lock;
     xrt_context* ctx = nullptr;
+    std::vector<float> mesh;   // the soup last uploaded (renders of the same mesh skip the upload)
+    bool uploaded = false;
 };
 
 static DeviceSlot& device_slot(int device)
@@ -155,7 +157,11 @@ void render_strip(int device, const xrt_camera& cam, const std::vector<float>& s
     std::lock_guard<std::mutex> g(slot.lock);
     xrt_context* ctx = slot.ctx;
     check(ctx, xrt_set_kernel(ctx, kernel_choice()), "xrt_set_kernel");
-    check(ctx, xrt_upload_mesh(ctx, soup.data(), soup.size() / 9), "xrt_upload_mesh");
+    if (!slot.uploaded || slot.mesh != soup) {   // the mesh lives on the device between renders
+        check(ctx, xrt_upload_mesh(ctx, soup.data(), soup.size() / 9), "xrt_upload_mesh");
+        slot.mesh = soup;
+        slot.uploaded = true;
+    }
     check(ctx, xrt_render_rows(ctx, &cam, row_begin, row_end, image_strip, lbuffer_strip, u8_strip, stats),
           "xrt_render_rows");
 }

@@ -9,7 +9,8 @@
 //   -i, --input FILE           mesh (default ./dragon.ply)
 // additions:
 //   -g, --gpus N               row strips over N GPUs (default 1)
-//   -k, --kernel brute|tiled|binned  render kernel (default binned)
+//   -k, --kernel brute|tiled|binned  render kernel (default: automatic -- tiled
+//                              for small frames, binned past 2e7 footprint tests)
 //   -t, --threads N            accepted for main-pthreads*.cxx compatibility (ignored)
 //       --lbuffer FILE         also write the L-buffer as raw little-endian f32
 //       --u8 FILE              also write the 8-bit image (LUT 0..80) as PGM
@@ -38,7 +39,7 @@ void showUsage(const std::string& prog)
               << "\t-f,--filename FILENAME\t\tName of the output text file, written to ./out/ (default: test.jpg)\n"
               << "\t-i,--input FILENAME\t\tInput mesh (default: ./dragon.ply)\n"
               << "\t-g,--gpus N\t\t\tRender row strips on N GPUs (default: 1)\n"
-              << "\t-k,--kernel brute|tiled|binned\tRender kernel (default: binned)\n"
+              << "\t-k,--kernel brute|tiled|binned\tRender kernel (default: automatic)\n"
               << "\t--lbuffer FILE\t\t\tWrite the L-buffer as raw float32\n"
               << "\t--u8 FILE\t\t\tWrite the 8-bit image (0..80 keV LUT) as PGM\n"
               << "\t--time\t\t\t\tPrint render time and Mrays/s\n"
@@ -142,8 +143,17 @@ int main(int argc, char** argv)
         RayTracerInfo info = initialiseRayTracing(meshes, upper, lower, opt.height, opt.width, image, lut);
 
         auto r0 = std::chrono::high_resolution_clock::now();
-        if (opt.gpus > 1) renderLoopMultiGPU(image, meshes, info, opt.gpus);
-        else renderLoop(image, meshes, info);
+        std::vector<float> lb;
+        if (opt.gpus > 1) {
+            renderLoopMultiGPU(image, meshes, info, opt.gpus);
+        } else if (!opt.lbuffer.empty()) {       // the image and the L-buffer in one render
+            lb.resize((size_t)opt.width * opt.height);
+            xrt_stats st;
+            renderLoopRows(image, meshes, info, 0, opt.height, lb.data(), nullptr, &st);
+            for (unsigned long long k = 0; k < st.odd_rays; ++k) std::cout << "Only one intersect on this ray" << std::endl;
+        } else {
+            renderLoop(image, meshes, info);
+        }
         auto r1 = std::chrono::high_resolution_clock::now();
         if (opt.time) {
             double s = std::chrono::duration<double>(r1 - r0).count();
@@ -155,9 +165,11 @@ int main(int argc, char** argv)
         image.saveTextFile(opt.output);
         if (!opt.u8.empty()) image.savePGMFile(opt.u8, 0.0f, 80.0f);
         if (!opt.lbuffer.empty()) {
-            std::vector<float> lb((size_t)opt.width * opt.height);
-            xrt_stats st;
-            renderLoopRows(image, meshes, info, 0, opt.height, lb.data(), nullptr, &st);
+            if (lb.empty()) {                   // multi-GPU: the L-buffer of the same frame
+                lb.resize((size_t)opt.width * opt.height);
+                xrt_stats st;
+                renderLoopRows(image, meshes, info, 0, opt.height, lb.data(), nullptr, &st);
+            }
             std::FILE* f = std::fopen(opt.lbuffer.c_str(), "wb");
             if (!f) throw std::runtime_error("Cannot create the file " + opt.lbuffer);
             std::fwrite(lb.data(), sizeof(float), lb.size(), f);

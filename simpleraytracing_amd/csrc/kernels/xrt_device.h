@@ -445,7 +445,8 @@ struct HitList {
 // (e_expf-fma.c: the compiler fuses InvLn2N*x into both uses and the
 // polynomial).  This is the function std::exp(float) binds to in
 // src/main.cxx:739.  Bit-identical to the system libm on all 2^32 inputs
-// (tools/gen_expf_table.py, tests/test_expf.py).
+// (tools/gen_expf_table.py; tests/test_abi.py::test_host_expf_restatement_matches_libm on
+// the host build, tests/test_gpu_parity.py::test_probe_expf_matches_libm on the device).
 // ---------------------------------------------------------------------------
 __host__ __device__ __forceinline__ double xrt_u64_as_double(uint64_t u)
 {

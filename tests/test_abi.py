@@ -185,3 +185,20 @@ def test_fp_identities_exhaustive(tmp_path):
     subprocess.run(["gcc", "-O2", "-o", exe, src, "-lm"], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_host_ray_intersect_kat_matches_oracle():
+    """The drop-in Ray::intersect (host C++, src/Ray.cxx:72-124 over host/Vec3.h)
+    on the KAT pairs: bit-equal to the oracle (itself pinned to the reference's
+    compiled Ray.cxx in test_oracle.py)."""
+    from kat import kat_vectors
+    rays, tris = kat_vectors()
+    host = _abi.load_host()
+    n = len(rays)
+    hit = np.zeros(n, np.uint8)
+    t = np.zeros(n, np.float32)
+    host.xrt_host_intersect_batch(rays.ctypes.data_as(_abi._fp), tris.ctypes.data_as(_abi._fp), n,
+                                  hit.ctypes.data_as(_abi._u8p), t.ctypes.data_as(_abi._fp))
+    h2, t2 = oracle.intersect_batch(rays, tris)
+    assert np.array_equal(hit, h2)
+    assert np.array_equal(bits(t), bits(t2))
