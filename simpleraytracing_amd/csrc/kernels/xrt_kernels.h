@@ -972,7 +972,20 @@ struct BinBuffers {
     uint32_t regions_x, regions_y;
     uint32_t* clear;         // the other half's counters (its BinState line precedes them), cleared by k_prep
     uint32_t clear_regions;  // counters to clear there
+    // Compact lists: slot s's list is list[offsets[s] .. offsets[s+1]) -- sized
+    // from the counts of the first frame of the geometry (identical for every
+    // frame of it).  Null: fixed capacity `cap` per slot (that first frame).
+    const uint32_t* offsets;
 };
+
+__device__ __forceinline__ uint32_t list_base(const BinBuffers& b, uint32_t slot)
+{
+    return b.offsets ? b.offsets[slot] : slot * b.cap;
+}
+__device__ __forceinline__ uint32_t list_cap(const BinBuffers& b, uint32_t slot)
+{
+    return b.offsets ? b.offsets[slot + 1u] - b.offsets[slot] : b.cap;
+}
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
@@ -1137,6 +1150,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
+    bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
     auto commit = [&]() {
         for (uint32_t base = 0; base < queued; base += 64u * kBinBatch) {
@@ -1151,15 +1165,20 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
                     own[b] = s_qown[wave][q];
                 }
             }
+            uint32_t lbase[kBinBatch], lcap[kBinBatch];
 #pragma unroll
-            for (uint32_t b = 0; b < kBinBatch; ++b)
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
                 slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
+                lbase[b] = reg[b] != kEmpty ? list_base(bins, reg[b]) : 0u;
+                lcap[b] = reg[b] != kEmpty ? list_cap(bins, reg[b]) : 0u;
+            }
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 if (reg[b] == kEmpty) continue;
                 my_max = max(my_max, slot[b] + 1u);
-                if (slot[b] < bins.cap) {
-                    float4* e = reinterpret_cast<float4*>(bins.list + (size_t)reg[b] * bins.cap + slot[b]);
+                if (slot[b] >= lcap[b]) over = true;
+                else {
+                    float4* e = reinterpret_cast<float4*>(bins.list + (size_t)lbase[b] + slot[b]);
 #pragma unroll
                     for (uint32_t w = 0; w < 8; ++w) e[w] = s_fp[wave][w][own[b]];
                 }
@@ -1233,7 +1252,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     // back to the whole mesh, and the host grows the lists for the next frame
     // (xrt_read_stats / the sizing read).  No global atomic otherwise.
     my_max = wave_reduce_u32<true>(my_max);
-    if (lane == 0 && my_max > bins.cap) {
+    if (__ballot(over) && lane == 0) {
         atomicMax(&bs->max_count, my_max);
         atomicOr(&bs->overflow, 1u);
     }
@@ -1401,10 +1420,10 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         reg_x = slot % bins.regions_x;
         reg_y = slot / bins.regions_x;
     }
-    const RegionEntry* __restrict__ local = bins.list + (size_t)slot * bins.cap;
+    const RegionEntry* __restrict__ local = bins.list + list_base(bins, slot);
     const RegionEntry* __restrict__ glob = bins.global_list;
     const uint32_t T = p.num_triangles;
-    const bool whole = n_local > bins.cap;         // the region's list overflowed: whole mesh (exact, slower)
+    const bool whole = n_local > list_cap(bins, slot);   // the list overflowed: whole mesh (exact, slower)
     const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole ? T : n_local + n_glob;
 
     const uint32_t tx0 = reg_x * kRegion + (tile & 3u) * 8u;

@@ -19,25 +19,18 @@
 
 using namespace XRT_KERNEL_NS;
 
-// Region list capacity: the first frame of a geometry starts here; the sizing
-// read (xrt_context::BinKey) raises it to a power of two above 1.25x the
-// largest region count, up to kMaxRegionCap (past it a region renders from
-// the whole mesh).
+// Region lists: the first frame of a geometry (xrt_context::BinKey) bins into
+// lists of kInitialRegionCap entries per region, reads every region's count
+// back once, and re-bins into compact lists sized from them (the counts of
+// every later frame of the geometry are the same): the sum of the counts plus
+// 1/8 + 4 per region, instead of the largest count times the regions.
 constexpr uint32_t kInitialRegionCap = 256;
-constexpr uint32_t kMaxRegionCap = 1u << 16;
 // Timed regions put render timing events on every kTimingStride-th frame.
 constexpr uint64_t kTimingStride = 4;
 // Buffer sets in rotation: frame N's preparation reuses the set of frame
 // N - kFrameSets, whose render the host has seen complete by then.
 constexpr int kFrameSets = 4;
 
-inline uint32_t region_cap_for(uint32_t max_count)
-{
-    uint64_t want = (uint64_t)max_count + max_count / 4u + 1u;
-    uint32_t cap = 64;
-    while (cap < want && cap < kMaxRegionCap) cap <<= 1;
-    return cap;
-}
 
 // Everything one frame's preparation writes and its render reads or writes.
 // kFrameSets sets rotate, so frame N+1's preparation (k_prep, binning) runs on
@@ -102,7 +95,11 @@ struct xrt_context {
     FrameSet* last_set = nullptr;      // set of the last enqueued frame
     hipStream_t prep_stream = nullptr;
 
-    uint32_t bin_region_cap = kInitialRegionCap;   // list capacity per region (grown by sizing)
+    // compact region lists of the current geometry (bin_key): slot offsets
+    uint32_t* d_slot_off = nullptr;
+    size_t slot_off_cap = 0;
+    uint64_t slot_pool = 0;            // entries of the compact lists
+    bool compact = false;              // d_slot_off is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     uint32_t* d_order = nullptr;       // render launch order of the regions (launch_order)
     size_t order_cap = 0;
@@ -374,8 +371,11 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
         fs.bin_half_words = half_words;
         fs.dirty[0] = fs.dirty[1] = kDirtyAll;
     }
-    const uint32_t cap = ctx->bin_region_cap;
-    if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, (size_t)n_regions * cap))) return rc;
+    const bool compact = ctx->compact && !ctx->bin_force_cap;
+    const uint32_t cap = ctx->bin_force_cap ? (uint32_t)std::min<size_t>(kInitialRegionCap, ctx->bin_force_cap)
+                                            : kInitialRegionCap;
+    if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, compact ? ctx->slot_pool : (size_t)n_regions * cap)))
+        return rc;
     if ((rc = ensure(ctx, fs.global_list, fs.global_list_cap, T))) return rc;
     const uint32_t q = rerun ? fs.half : fs.half ^ 1u;     // a re-run recounts into the same half
     uint32_t* mine = fs.bin_counts + (size_t)q * fs.bin_half_words;
@@ -397,7 +397,7 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
     bins.list = fs.bin_list;
     bins.global_list = fs.global_list;
     bins.cap = cap;
-    if (ctx->bin_force_cap) bins.cap = (uint32_t)std::min<size_t>(bins.cap, ctx->bin_force_cap);
+    bins.offsets = compact ? ctx->d_slot_off : nullptr;
     return XRT_OK;
 }
 
@@ -543,6 +543,14 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
 
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
+    xrt_context::BinKey key = {};                  // the frame geometry of the region lists
+    key.cam = *cam;
+    key.row_begin = row_begin;
+    key.row_end = row_end;
+    key.T = T;
+    key.gen = ctx->mesh_gen;
+    const bool new_geometry = binned && rows > 0 && (!ctx->bin_key_valid || !key.same(ctx->bin_key));
+    if (new_geometry) ctx->compact = false;
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
@@ -554,29 +562,33 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
     if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, prep_flags))) return rc;
-    if (binned && !ctx->bin_force_cap) {
-        // Size the region lists once per frame geometry (mesh, camera,
-        // strip): a synchronous read of the largest region count, and a
-        // re-run of k_prep with larger lists if this frame's did not fit.
-        xrt_context::BinKey key = {};
-        key.cam = *cam;
-        key.row_begin = row_begin;
-        key.row_end = row_end;
-        key.T = T;
-        key.gen = ctx->mesh_gen;
-        if (!ctx->bin_key_valid || !key.same(ctx->bin_key)) {
-            BinState h = {};
-            XRT_HIP(ctx, hipMemcpyAsync(&h, bin_ctl, sizeof h, hipMemcpyDeviceToHost, ps));
-            XRT_HIP(ctx, hipStreamSynchronize(ps));
-            ctx->bin_key = key;
-            ctx->bin_key_valid = true;
-            if (h.max_count > bins.cap && ctx->bin_region_cap < kMaxRegionCap) {
-                ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(h.max_count));
-                bool cleared = false;
-                if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
-                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
-            }
+    if (new_geometry && !ctx->bin_force_cap) {
+        // Size the compact region lists once per frame geometry (mesh, camera,
+        // strip): a synchronous read of every region's count, slot offsets
+        // from them, and a re-run of k_prep into the compact lists.
+        std::vector<uint32_t> counts((size_t)n_regions * kCounterStride);
+        XRT_HIP(ctx, hipMemcpyAsync(counts.data(), bins.counts, counts.size() * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, ps));
+        XRT_HIP(ctx, hipStreamSynchronize(ps));
+        std::vector<uint32_t> off(n_regions + 1u);
+        uint64_t run = 0;
+        for (uint32_t r = 0; r < n_regions; ++r) {
+            off[r] = (uint32_t)run;
+            const uint64_t c = counts[(size_t)r * kCounterStride];
+            run += c + c / 8u + 4u;
         }
+        if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
+        off[n_regions] = (uint32_t)run;
+        XRT_HIP(ctx, hipDeviceSynchronize());      // frames in flight may read the previous offsets
+        if ((rc = ensure(ctx, ctx->d_slot_off, ctx->slot_off_cap, off.size()))) return rc;
+        XRT_HIP(ctx, hipMemcpy(ctx->d_slot_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ctx->slot_pool = run;
+        ctx->compact = true;
+        ctx->bin_key = key;
+        ctx->bin_key_valid = true;
+        bool cleared = false;
+        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
+        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
     }
     pf.fs = &fs;
     pf.stream = stream;
@@ -767,6 +779,7 @@ void xrt_destroy(xrt_context* ctx)
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
     (void)hipFree(ctx->d_order);
+    (void)hipFree(ctx->d_slot_off);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
@@ -969,8 +982,8 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
         BinState bs = {};
         XRT_HIP(ctx, hipMemcpy(&bs, fs->last_state, sizeof bs, hipMemcpyDeviceToHost));
         stats->global_triangles = bs.global_count;
-        if (bs.overflow && !ctx->bin_force_cap)   // next frame gets lists large enough for this one
-            ctx->bin_region_cap = std::max(ctx->bin_region_cap, region_cap_for(bs.max_count));
+        if (bs.overflow && !ctx->bin_force_cap)   // the next frame re-sizes its lists
+            ctx->bin_key_valid = false;
     }
     return XRT_OK;
 }
