@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 2
+#define XRT_ABI_VERSION 3
 
 typedef enum xrt_status {
     XRT_OK = 0,
@@ -129,6 +129,16 @@ int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_trian
 int xrt_mesh_bbox(const float* triangles, uint64_t num_triangles, float lower[3], float upper[3]);
 
 /*
+ * Bounding box of a scene of several meshes: getBBox over each mesh's
+ * computeBoundingBox (src/main.cxx:538-563).  tris holds the meshes' soups one
+ * after another; mesh_triangles[m] is mesh m's triangle count.  The camera
+ * comes from the box of every mesh (main.cxx:634), while only mesh 0 is
+ * uploaded -- the only mesh whose hits count (main.cxx:687).
+ */
+int xrt_scene_bbox(const float* tris, const uint64_t* mesh_triangles, uint32_t num_meshes, float lower[3],
+                   float upper[3]);
+
+/*
  * Camera from the scene bounding box: initialiseRayTracing (main.cxx:566-622)
  * and renderLoop's pixel spacing (main.cxx:634-641), f32/f64 rounding as written.
  */
@@ -196,6 +206,51 @@ int xrt_set_miss_code(xrt_context* ctx, uint32_t bits);
 int xrt_expand_rows_device(xrt_context* ctx, uint64_t num_pixels, float* d_lbuffer, float* d_image,
                            uint8_t* d_image_u8, void* stream);
 
+/* --- the signed multi-material L-buffer (the L-buffer fork) --------------- */
+
+/*
+ * What renders compute per ray:
+ *   XRT_MODEL_ATTENUATION  renderLoop, src/main.cxx:626-743 (the default):
+ *                          image, L-buffer and 8-bit planes as above.
+ *   XRT_MODEL_SIGNED       renderLoopCallBack of src/main-pthreads-lbuffer.cxx
+ *                          (:733-813): per ray, distance = the sum of
+ *                          sign(direction . normal) * t over the mesh-0 hits
+ *                          in triangle order (f32), L = 80 * exp(-(mu *
+ *                          (distance * 0.1))) in f64 (glibc exp), or -1 when
+ *                          the signs do not cancel (:805-806).  Renders write
+ *                          the L-buffer plane only (image and u8 must be NULL);
+ *                          xrt_hole_fill makes the image.  Kernels: BRUTE or
+ *                          BINNED (AUTO picks BINNED).
+ * mu: mesh 0's attenuation coefficient, 0.1037f in the fork (soft tissue,
+ * :800).  Other meshes add no hits (the mesh-0 filter, :788), so their
+ * coefficient (0.3971f, :802) multiplies L by exp(-0.0) = 1.
+ */
+#define XRT_MODEL_ATTENUATION 0
+#define XRT_MODEL_SIGNED 1
+int xrt_set_model(xrt_context* ctx, int model, float mu);
+
+/*
+ * The fork's hole fill (main-pthreads-lbuffer.cxx:327-404) over a whole
+ * width x height L-buffer: pixels flagged -1 become the mean of the first
+ * unflagged non-zero value within 4 steps in each of four directions; others
+ * keep their value.  Writes image (f32) and/or image_u8 (the LUT of
+ * image_u8's plane above).  Host buffers, synchronous; _device: device
+ * buffers, asynchronous on `stream`.
+ */
+int xrt_hole_fill(xrt_context* ctx, uint32_t width, uint32_t height, const float* lbuffer, float* image,
+                  uint8_t* image_u8);
+int xrt_hole_fill_device(xrt_context* ctx, uint32_t width, uint32_t height, const float* d_lbuffer,
+                         float* d_image, uint8_t* d_image_u8, void* stream);
+
+/*
+ * The fork end to end on the whole frame (XRT_MODEL_SIGNED): render, hole
+ * fill; host buffers (any may be NULL): image = the fork's output image,
+ * lbuffer = its L_buffer (-1 flags), image_u8 = the image's LUT.  stats.odd_rays
+ * counts the flagged rays.
+ */
+int xrt_render_signed(xrt_context* ctx, const xrt_camera* camera, float* image, float* lbuffer,
+                      uint8_t* image_u8, xrt_stats* stats);
+
 /* --- multi-GPU: row strips + RCCL root gather (one process) --------------- */
 
 /*
@@ -253,7 +308,9 @@ typedef enum xrt_probe_op {
     XRT_PROBE_SQRTF = 1,    /* std::sqrt(float), correctly rounded               */
     XRT_PROBE_RCP = 2,      /* (float)(1.0 / (double)x), src/Ray.cxx:99           */
     XRT_PROBE_LUT_U8 = 3,   /* 8-bit LUT of a photon value (out[i] = (float)u8)  */
-    XRT_PROBE_RCP_FAST = 4  /* the culled tests' 1/det (rcp + Newton where exact) */
+    XRT_PROBE_RCP_FAST = 4, /* the culled tests' 1/det (rcp + Newton where exact) */
+    XRT_PROBE_SIGNED_L = 5  /* (float)(80.0 * exp(-(0.1037f * (d * 0.1)))): the signed
+                               model's L for distance d (glibc exp in f64)          */
 } xrt_probe_op;
 
 /* Evaluates one scalar device function elementwise.  Host buffers. */
@@ -274,6 +331,15 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
  * compiled for the host): lets CPU-only tests check it against libm.
  */
 void xrt_host_expf_batch(const float* in, float* out, uint64_t n);
+
+/*
+ * The same for the signed model: the device glibc exp restatement, and its L
+ * update (float)(80.0 * exp(-(mu * (distance * 0.1)))) (-1 for a non-zero
+ * sign sum; sign_sum may be NULL for all zero).
+ */
+void xrt_host_exp_batch(const double* in, double* out, uint64_t n);
+void xrt_host_signed_lbuffer_batch(const float* distance, const int32_t* sign_sum, float mu, float* out,
+                                   uint64_t n);
 
 /*
  * Test hook: caps the per-ray register hit list at `capacity` (1..12) so the

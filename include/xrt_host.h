@@ -20,6 +20,14 @@ extern "C" {
 
 /* Loads a PLY file; *triangles is malloc'd (free with xrt_host_free). */
 int xrt_host_load_ply(const char* path, float** triangles, uint64_t* num_triangles);
+
+/*
+ * Every mesh of a PLY (one mesh) or OBJ (one per object) file, as loadMeshes
+ * builds them (main.cxx:455-508): *triangles holds the meshes' soups one
+ * after another, (*mesh_triangles)[m] the triangle count of mesh m.  Both
+ * malloc'd (free with xrt_host_free).
+ */
+int xrt_host_load_meshes(const char* path, float** triangles, uint64_t** mesh_triangles, uint32_t* num_meshes);
 void xrt_host_free(void* p);
 
 /*

@@ -18,6 +18,8 @@ _F = ctypes.POINTER(ctypes.c_float)
 _U8 = ctypes.POINTER(ctypes.c_uint8)
 _I32 = ctypes.POINTER(ctypes.c_int32)
 _U32 = ctypes.POINTER(ctypes.c_uint32)
+_U64 = ctypes.POINTER(ctypes.c_uint64)
+_D = ctypes.POINTER(ctypes.c_double)
 
 _orc = None
 _ref = None
@@ -58,6 +60,16 @@ def lib():
         L.orc_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
         L.orc_save_text.argtypes = [_F, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
         L.orc_expf_batch.argtypes = [_F, _F, ctypes.c_uint64]
+        L.orc_render_scene_rows.restype = ctypes.c_int64
+        L.orc_render_scene_rows.argtypes = [_F, _U64, ctypes.c_uint32, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, _F, _F, _U8, _I32, ctypes.c_int]
+        L.orc_render_signed_rows.restype = ctypes.c_int64
+        L.orc_render_signed_rows.argtypes = [_F, _U64, ctypes.c_uint32, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint32, _F, _I32, ctypes.c_int]
+        L.orc_hole_fill.argtypes = [_F, ctypes.c_uint32, ctypes.c_uint32, _F]
+        L.orc_scene_bbox.argtypes = [_F, _U64, ctypes.c_uint32, _F, _F]
+        L.orc_exp_batch.argtypes = [_D, _D, ctypes.c_uint64]
+        L.orc_triangle_normals.argtypes = [_F, ctypes.c_uint64, _F]
         L.orc_lut_u8.restype = ctypes.c_uint8
         L.orc_lut_u8.argtypes = [ctypes.c_float]
         _orc = L
@@ -78,6 +90,10 @@ def ref_lib():
         R.ref_intersect_batch.argtypes = [_F, _F, ctypes.c_uint64, _U8, _F]
         R.ref_mesh_bbox.argtypes = [_F, ctypes.c_uint64, _F, _F]
         R.ref_camera.argtypes = [_F, _F, ctypes.c_uint32, ctypes.c_uint32, _F]
+        R.ref_triangle_normals.argtypes = [_F, ctypes.c_uint64, _F]
+        R.ref_render_signed_rows.restype = ctypes.c_int64
+        R.ref_render_signed_rows.argtypes = [_F, _U64, ctypes.c_uint32, _F, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint32, _F]
         R.ref_render_rows.restype = ctypes.c_int64
         R.ref_render_rows.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, _F, _F]
@@ -253,3 +269,104 @@ def text_bytes(img, width, height):
 
 def lut_u8(v):
     return lib().orc_lut_u8(float(v))
+
+
+# --- scenes of several meshes, the signed L-buffer fork -----------------------
+
+def scene_arrays(meshes):
+    """(concatenated soup f32 (T, 9), triangles per mesh u64) of a list of soups."""
+    meshes = [np.ascontiguousarray(m, np.float32).reshape(-1, 9) for m in meshes]
+    counts = np.array([len(m) for m in meshes], np.uint64)
+    tris = np.concatenate(meshes) if meshes else np.zeros((0, 9), np.float32)
+    return np.ascontiguousarray(tris, np.float32), counts
+
+
+def scene_bbox(meshes):
+    tris, counts = scene_arrays(meshes)
+    lo = np.zeros(3, np.float32)
+    hi = np.zeros(3, np.float32)
+    lib().orc_scene_bbox(_fp(tris), counts.ctypes.data_as(_U64), len(counts), _fp(lo), _fp(hi))
+    return lo, hi
+
+
+def camera_for_scene(meshes, width, height):
+    lo, hi = scene_bbox(meshes)
+    return camera(lo, hi, width, height)
+
+
+def render_scene_rows(meshes, cam13, width, height, row_begin=0, row_end=None, threads=None):
+    """renderLoop over a scene (hits on mesh 0 only): (image, lbuffer, u8, nhits, odd)."""
+    if row_end is None:
+        row_end = height
+    tris, counts = scene_arrays(meshes)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    n = (row_end - row_begin) * width
+    img = np.empty(n, np.float32)
+    lb = np.empty(n, np.float32)
+    u8 = np.empty(n, np.uint8)
+    nh = np.empty(n, np.int32)
+    odd = lib().orc_render_scene_rows(_fp(tris), counts.ctypes.data_as(_U64), len(counts), _fp(cam13), width,
+                                      height, row_begin, row_end, _fp(img), _fp(lb), u8.ctypes.data_as(_U8),
+                                      nh.ctypes.data_as(_I32), threads or os.cpu_count() or 1)
+    if odd < 0:
+        raise ValueError("bad row range")
+    return img, lb, u8, nh, odd
+
+
+def render_signed_rows(meshes, cam13, width, height, row_begin=0, row_end=None, threads=None):
+    """The L-buffer fork's signed L-buffer: (lbuffer f32 with -1 flags, nhits i32, flagged)."""
+    if row_end is None:
+        row_end = height
+    tris, counts = scene_arrays(meshes)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    n = (row_end - row_begin) * width
+    lb = np.empty(n, np.float32)
+    nh = np.empty(n, np.int32)
+    flagged = lib().orc_render_signed_rows(_fp(tris), counts.ctypes.data_as(_U64), len(counts), _fp(cam13),
+                                           width, height, row_begin, row_end, _fp(lb),
+                                           nh.ctypes.data_as(_I32), threads or os.cpu_count() or 1)
+    if flagged < 0:
+        raise ValueError("bad row range")
+    return lb, nh, flagged
+
+
+def hole_fill(lbuffer, width, height):
+    """The fork's -1 hole fill: the final image (f32) from a full-frame L-buffer."""
+    lb = np.ascontiguousarray(lbuffer, np.float32).reshape(-1)
+    assert lb.size == width * height
+    out = np.empty_like(lb)
+    lib().orc_hole_fill(_fp(lb), width, height, _fp(out))
+    return out
+
+
+def exp(x):
+    """glibc exp (double)."""
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.empty_like(x)
+    lib().orc_exp_batch(x.ctypes.data_as(_D), out.ctypes.data_as(_D), x.size)
+    return out
+
+
+def triangle_normals(tris):
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    out = np.empty((len(tris), 3), np.float32)
+    lib().orc_triangle_normals(_fp(tris), len(tris), _fp(out))
+    return out
+
+
+def ref_triangle_normals(tris):
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    out = np.empty((len(tris), 3), np.float32)
+    ref_lib().ref_triangle_normals(_fp(tris), len(tris), _fp(out))
+    return out
+
+
+def ref_render_signed_rows(meshes, cam13, width, height, row_begin=0, row_end=None):
+    if row_end is None:
+        row_end = height
+    tris, counts = scene_arrays(meshes)
+    cam13 = np.ascontiguousarray(cam13, np.float32)
+    lb = np.empty((row_end - row_begin) * width, np.float32)
+    flagged = ref_lib().ref_render_signed_rows(_fp(tris), counts.ctypes.data_as(_U64), len(counts), _fp(cam13),
+                                               width, height, row_begin, row_end, _fp(lb))
+    return lb, flagged

@@ -142,4 +142,72 @@ int64_t ref_render_rows(const float* tris, uint64_t ntris, const float cam[13],
     return odd;
 }
 
+// Triangle::getNormal of the reference's Triangle (include/Triangle.inl:170-178).
+void ref_triangle_normals(const float* tris, uint64_t n, float* normals)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        const float* p = tris + 9 * i;
+        Triangle tri(Vec3(p[0], p[1], p[2]), Vec3(p[3], p[4], p[5]), Vec3(p[6], p[7], p[8]));
+        for (int k = 0; k < 3; ++k) normals[3 * i + k] = tri.getNormal()[k];
+    }
+}
+
+// The signed L-buffer of src/main-pthreads-lbuffer.cxx:750-811 restated over
+// the reference's classes (the fork itself needs glm and Assimp): a scene of
+// meshes (soups one after another, mesh_ntris[m] triangles each), rows
+// [row_begin, row_end); lbuffer = the fork's L_buffer values.  Returns the
+// number of pixels flagged -1.
+int64_t ref_render_signed_rows(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes,
+                               const float cam[13], uint32_t width, uint32_t height, uint32_t row_begin,
+                               uint32_t row_end, float* lbuffer)
+{
+    std::vector<TriangleMesh> meshes(nmeshes);    // built in place (no TriangleMesh copies)
+    uint64_t first = 0;
+    for (uint32_t m = 0; m < nmeshes; ++m) {
+        std::vector<float> v(tris + 9 * first, tris + 9 * (first + mesh_ntris[m]));
+        std::vector<unsigned int> idx(3 * mesh_ntris[m]);
+        for (uint64_t i = 0; i < idx.size(); ++i) idx[i] = (unsigned int)i;
+        meshes[m].setGeometry(v, idx);
+        first += mesh_ntris[m];
+    }
+    const Vec3 origin(cam[0], cam[1], cam[2]);
+    const Vec3 detector(cam[3], cam[4], cam[5]);
+    const Vec3 up(cam[6], cam[7], cam[8]);
+    const Vec3 right(cam[9], cam[10], cam[11]);
+    const float spacing = cam[12];
+    int64_t flagged = 0;
+    for (uint32_t row = row_begin; row < row_end; ++row) {
+        for (uint32_t col = 0; col < width; ++col) {
+            float v_off = spacing * (0.5 + row - height / 2.0);
+            float u_off = spacing * (0.5 + col - width / 2.0);
+            Vec3 direction = detector + up * v_off + right * u_off - origin;
+            direction.normalise();
+            Ray ray(origin, direction);
+            float L = 80.000f;
+            for (size_t m = 0; m < meshes.size(); ++m) {
+                if (L == -1) break;
+                float distance = 0.0f;
+                int sign_sum = 0;
+                for (unsigned int k = 0; k < meshes[m].getNumberOfTriangles(); ++k) {
+                    const Triangle& triangle = meshes[m].getTriangle(k);
+                    float t;
+                    bool intersect = ray.intersect(triangle, t);
+                    if (intersect && m == 0 && t > 0.0000001) {
+                        float dp = direction.dotProduct(triangle.getNormal());
+                        int sign = (0.0f < dp) - (dp < 0.0f);
+                        distance += (sign * t);
+                        sign_sum += sign;
+                    }
+                }
+                float mu = m == 0 ? 0.1037f : 0.3971f;
+                if (sign_sum != 0) L = -1;
+                else L = L * std::exp(-(mu * (distance * 0.1)));
+            }
+            if (L == -1) ++flagged;
+            lbuffer[(size_t)(row - row_begin) * width + col] = L;
+        }
+    }
+    return flagged;
+}
+
 }  // extern "C"

@@ -427,8 +427,11 @@ static inline uint8_t lut_u8(float v)
 }
 
 struct render_job {
-    const float* tris;
-    uint64_t ntris;
+    const float* tris;       /* the scene's meshes, soups one after another */
+    uint64_t ntris;          /* triangles of mesh 0 (the first ntris of tris) */
+    const uint64_t* mesh_ntris;  /* triangles per mesh */
+    uint32_t nmeshes;
+    int signed_model;        /* 1: main-pthreads-lbuffer.cxx's signed L-buffer */
     const float* cam;
     uint32_t width, height;
     const uint32_t* rows;  /* image rows to render, output row i = rows[i] */
@@ -474,17 +477,23 @@ static void render_pixel(const struct render_job* job, uint32_t row, uint32_t co
         d[2] = direction[2] / len;
     }
 
-    /* :670-696 -- every triangle of mesh 0; keep t > 1e-7 (double compare) */
+    /* :670-696 -- every mesh (intersectBBox is `return true`, TriangleMesh.inl:
+     * 232-236) and every triangle; only hits on mesh 0 with t > 1e-7 (double
+     * compare) are kept (:687).  Ray::intersect has no side effects, so the
+     * other meshes' tests -- whose results :687 discards -- are skipped. */
     size_t count = 0;
-    for (uint64_t i = 0; i < job->ntris; ++i) {
-        const float* tr = job->tris + 9 * i;
-        float t;
-        if (orc_intersect(origin, d, tr, tr + 3, tr + 6, &t) && (double)t > 0.0000001) {
-            if (count == *hits_cap) {
-                *hits_cap *= 2;
-                *hits = (float*)realloc(*hits, sizeof(float) * *hits_cap);
+    for (uint32_t m = 0; m < job->nmeshes; ++m) {
+        if (m != 0) continue;
+        for (uint64_t i = 0; i < job->mesh_ntris[0]; ++i) {
+            const float* tr = job->tris + 9 * i;
+            float t;
+            if (orc_intersect(origin, d, tr, tr + 3, tr + 6, &t) && (double)t > 0.0000001) {
+                if (count == *hits_cap) {
+                    *hits_cap *= 2;
+                    *hits = (float*)realloc(*hits, sizeof(float) * *hits_cap);
+                }
+                (*hits)[count++] = t;
             }
-            (*hits)[count++] = t;
         }
     }
 
@@ -512,6 +521,73 @@ static void render_pixel(const struct render_job* job, uint32_t row, uint32_t co
     if (nh) *nh = (int32_t)count;
 }
 
+/*
+ * The signed multi-material L-buffer, src/main-pthreads-lbuffer.cxx:750-811
+ * (renderLoopCallBack of the L-buffer fork): per mesh, the sum of
+ * sign(direction . normal) * t over mesh-0 hits in triangle order; a non-zero
+ * sum of the signs flags the pixel -1 (:805-806), otherwise the L-buffer value
+ * (initially 80, :314) is attenuated with the mesh's coefficient (:798-808).
+ * Camera and ray as main.cxx (the fork's :739-762 restate :639-661).
+ */
+static void render_pixel_signed(const struct render_job* job, uint32_t row, uint32_t col, float* lb,
+                                int32_t* nh, uint64_t* flagged)
+{
+    const float* cam = job->cam;
+    const float* origin = cam + 0;
+    const float* detector = cam + 3;
+    const float* up = cam + 6;
+    const float* right = cam + 9;
+    float ps = cam[12];
+    float v_offset = (float)((double)ps * (0.5 + (double)row - (double)job->height / 2.0));  /* :756 */
+    float u_offset = (float)((double)ps * (0.5 + (double)col - (double)job->width / 2.0));   /* :757 */
+    float direction[3];
+    for (int k = 0; k < 3; ++k)                                        /* :760 */
+        direction[k] = ((detector[k] + up[k] * v_offset) + right[k] * u_offset) - origin[k];
+    normalise3(direction);                                             /* :761 */
+    float d[3] = {0.0f, 0.0f, 0.0f};                                   /* :762, Ray ctor */
+    float len = length3(direction);
+    if (fpclassify(len) != FP_ZERO) {
+        d[0] = direction[0] / len;
+        d[1] = direction[1] / len;
+        d[2] = direction[2] / len;
+    }
+    float L = 80.000f;                                                 /* :314 */
+    int32_t count = 0;
+    uint64_t first = 0;
+    for (uint32_t m = 0; m < job->nmeshes; ++m) {                      /* :768 */
+        const uint64_t n = job->mesh_ntris[m];
+        if (L == -1) break;                                            /* :772 */
+        float distance = 0.0f;                                         /* :778 */
+        int sign_sum = 0;
+        for (uint64_t i = 0; m == 0 && i < n; ++i) {                   /* :780; :788 keeps mesh 0 only */
+            const float* tr = job->tris + 9 * (first + i);
+            float t;
+            if (orc_intersect(origin, d, tr, tr + 3, tr + 6, &t) && (double)t > 0.0000001) {
+                /* Triangle::computeNormal, include/Triangle.inl:170-178 */
+                float e1[3] = {tr[3] - tr[0], tr[4] - tr[1], tr[5] - tr[2]};
+                float e2[3] = {tr[6] - tr[0], tr[7] - tr[1], tr[8] - tr[2]};
+                float nrm[3];
+                cross3(e1, e2, nrm);
+                normalise3(nrm);
+                float dp = dot3(direction, nrm);                       /* :791 */
+                int sign = (0.0f < dp) - (dp < 0.0f);                  /* signum, :729-731 */
+                distance += (float)sign * t;                           /* :792 */
+                sign_sum += sign;                                      /* :793 */
+                ++count;
+            }
+        }
+        float mu = m == 0 ? 0.1037f : 0.3971f;                         /* :798-803 */
+        if (sign_sum != 0)
+            L = -1;                                                    /* :806 */
+        else                                                           /* :808, std::exp(double) */
+            L = (float)((double)L * exp(-((double)mu * ((double)distance * 0.1))));
+        first += n;
+    }
+    if (L == -1) ++*flagged;
+    if (lb) *lb = L;
+    if (nh) *nh = count;
+}
+
 static void* render_worker(void* arg)
 {
     struct render_job* job = (struct render_job*)arg;
@@ -531,6 +607,11 @@ static void* render_worker(void* arg)
         size_t base = (size_t)i * span - job->col_begin;
         for (uint32_t col = c0; col < c1; ++col) {
             size_t o = base + col;
+            if (job->signed_model) {
+                render_pixel_signed(job, job->rows[i], col, job->lbuffer ? job->lbuffer + o : NULL,
+                                    job->nhits ? job->nhits + o : NULL, &odd);
+                continue;
+            }
             render_pixel(job, job->rows[i], col, &hits, &cap,
                          job->image ? job->image + o : NULL,
                          job->lbuffer ? job->lbuffer + o : NULL,
@@ -545,18 +626,37 @@ static void* render_worker(void* arg)
     return NULL;
 }
 
+static int64_t render_scene(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes, int signed_model,
+                            const float cam[13], uint32_t width, uint32_t height, const uint32_t* rows,
+                            uint32_t nrows, uint32_t col_begin, uint32_t col_end, float* image,
+                            float* lbuffer, uint8_t* image_u8, int32_t* nhits, int nthreads);
+
 static int64_t render_list(const float* tris, uint64_t ntris, const float cam[13], uint32_t width,
                            uint32_t height, const uint32_t* rows, uint32_t nrows,
                            uint32_t col_begin, uint32_t col_end, float* image,
                            float* lbuffer, uint8_t* image_u8, int32_t* nhits, int nthreads)
 {
+    return render_scene(tris, &ntris, 1, 0, cam, width, height, rows, nrows, col_begin, col_end, image,
+                        lbuffer, image_u8, nhits, nthreads);
+}
+
+static int64_t render_scene(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes, int signed_model,
+                            const float cam[13], uint32_t width, uint32_t height, const uint32_t* rows,
+                            uint32_t nrows, uint32_t col_begin, uint32_t col_end, float* image,
+                            float* lbuffer, uint8_t* image_u8, int32_t* nhits, int nthreads)
+{
+    const uint64_t no_mesh = 0;
+    if (nmeshes == 0) mesh_ntris = &no_mesh;   /* no meshes: nothing is hit */
     for (uint32_t i = 0; i < nrows; ++i)
         if (rows[i] >= height) return -1;
     if (col_begin > col_end || col_end > width) return -1;
     struct render_job job;
     memset(&job, 0, sizeof job);
     job.tris = tris;
-    job.ntris = ntris;
+    job.ntris = mesh_ntris[0];
+    job.mesh_ntris = mesh_ntris;
+    job.nmeshes = nmeshes ? nmeshes : 1;
+    job.signed_model = signed_model;
     job.cam = cam;
     job.width = width;
     job.height = height;
@@ -630,6 +730,132 @@ int64_t orc_render_span(const float* tris, uint64_t ntris, const float cam[13], 
 {
     return render_list(tris, ntris, cam, width, height, &row, 1, col_begin, col_end, image,
                        lbuffer, image_u8, nhits, nthreads);
+}
+
+/*
+ * A scene of several meshes (tris = their soups one after another,
+ * mesh_ntris[m] = triangles of mesh m): renderLoop's mesh loop with the
+ * mesh-0 filter (main.cxx:670-696), rows [row_begin, row_end).
+ */
+int64_t orc_render_scene_rows(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes,
+                              const float cam[13], uint32_t width, uint32_t height, uint32_t row_begin,
+                              uint32_t row_end, float* image, float* lbuffer, uint8_t* image_u8,
+                              int32_t* nhits, int nthreads)
+{
+    if (row_end > height || row_begin > row_end) return -1;
+    uint32_t n = row_end - row_begin;
+    uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; ++i) rows[i] = row_begin + i;
+    int64_t odd = render_scene(tris, mesh_ntris, nmeshes, 0, cam, width, height, rows, n, 0, width, image,
+                               lbuffer, image_u8, nhits, nthreads);
+    free(rows);
+    return odd;
+}
+
+/*
+ * The signed L-buffer of src/main-pthreads-lbuffer.cxx:733-813 over rows
+ * [row_begin, row_end): lbuffer = the fork's L_buffer values (80-based photon
+ * counts, or -1 for a flagged pixel), nhits = mesh-0 hits per ray.  Returns
+ * the number of flagged pixels, or -1.
+ */
+int64_t orc_render_signed_rows(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes,
+                               const float cam[13], uint32_t width, uint32_t height, uint32_t row_begin,
+                               uint32_t row_end, float* lbuffer, int32_t* nhits, int nthreads)
+{
+    if (row_end > height || row_begin > row_end) return -1;
+    uint32_t n = row_end - row_begin;
+    uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; ++i) rows[i] = row_begin + i;
+    int64_t flagged = render_scene(tris, mesh_ntris, nmeshes, 1, cam, width, height, rows, n, 0, width, NULL,
+                                   lbuffer, NULL, nhits, nthreads);
+    free(rows);
+    return flagged;
+}
+
+/*
+ * The fork's "error correction" pass, src/main-pthreads-lbuffer.cxx:327-404:
+ * each pixel flagged -1 becomes the mean of the first unflagged value within
+ * 4 steps in each of four directions (+1 and -1 along the row-major index --
+ * which runs on into the next / previous row -- and +-1 row), skipping zero
+ * values; a pixel with no such value becomes 0.0f / 0 (NaN).  Index
+ * arithmetic is the fork's unsigned int arithmetic; an index past the buffer
+ * ends the walk.  The fork also reads the element one past the end (its test
+ * is `> size`, not `>= size`) -- undefined behaviour, taken here as the end
+ * of the walk.  Reads L only (the fill does not cascade), writes image.
+ */
+void orc_hole_fill(const float* L, uint32_t width, uint32_t height, float* image)
+{
+    const uint64_t size = (uint64_t)width * height;
+    const int max_depth = 4;                                           /* :339 */
+    for (uint64_t pixel = 0; pixel < size; ++pixel) {
+        uint32_t row = (uint32_t)(pixel / width);
+        uint32_t col = (uint32_t)(pixel % width);
+        float photon = L[(uint32_t)(row * width + col)];               /* :334 */
+        if (photon == -1) {                                            /* :338 */
+            float values[4];
+            size_t count = 0;
+            for (int dir = 0; dir < 4; ++dir) {
+                float value = 0;
+                for (int i = 1; i <= max_depth; ++i) {
+                    uint32_t idx;
+                    switch (dir) {
+                    case 0: idx = row * width + (col + (uint32_t)i); break;    /* :343-352 */
+                    case 1: idx = (row - (uint32_t)i) * width + col; break;    /* :356-365 */
+                    case 2: idx = row * width + (col - (uint32_t)i); break;    /* :369-378 */
+                    default: idx = (row + (uint32_t)i) * width + col; break;   /* :382-391 */
+                    }
+                    if ((uint64_t)idx >= size) break;                   /* `> size` + the UB read */
+                    if (L[idx] != -1) {
+                        value = L[idx];
+                        break;
+                    }
+                }
+                if (value != 0) values[count++] = value;
+            }
+            float sum = 0;                                             /* :394-397 */
+            for (size_t k = 0; k < count; ++k) sum += values[k];
+            photon = sum / (float)count;                               /* :399 */
+        }
+        image[pixel] = photon;                                         /* :403 */
+    }
+}
+
+/* getBBox (main.cxx:538-563) over the meshes' computeBoundingBox boxes. */
+void orc_scene_bbox(const float* tris, const uint64_t* mesh_ntris, uint32_t nmeshes, float lower[3],
+                    float upper[3])
+{
+    for (int k = 0; k < 3; ++k) {
+        lower[k] = INFINITY;
+        upper[k] = -INFINITY;
+    }
+    uint64_t first = 0;
+    for (uint32_t m = 0; m < nmeshes; ++m) {
+        float lo[3], hi[3];
+        orc_bbox(tris + 9 * first, mesh_ntris[m], lo, hi);
+        for (int k = 0; k < 3; ++k) {
+            lower[k] = stdmin(lower[k], lo[k]);
+            upper[k] = stdmax(upper[k], hi[k]);
+        }
+        first += mesh_ntris[m];
+    }
+}
+
+/* Triangle::computeNormal (include/Triangle.inl:170-178) of each triangle. */
+void orc_triangle_normals(const float* tris, uint64_t n, float* normals)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        const float* tr = tris + 9 * i;
+        float e1[3] = {tr[3] - tr[0], tr[4] - tr[1], tr[5] - tr[2]};
+        float e2[3] = {tr[6] - tr[0], tr[7] - tr[1], tr[8] - tr[2]};
+        cross3(e1, e2, normals + 3 * i);
+        normalise3(normals + 3 * i);
+    }
+}
+
+/* glibc exp (the fork's std::exp(double), :808), for checking the restatement. */
+void orc_exp_batch(const double* in, double* out, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) out[i] = exp(in[i]);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -19,12 +19,14 @@ import numpy as np
 
 from . import _abi
 from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
-                   XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT)
+                   XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT, XRT_MODEL_ATTENUATION,
+                   XRT_MODEL_SIGNED)
 
 __all__ = [
     "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
-    "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT",
+    "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT", "load_meshes", "scene_bbox", "camera_for_scene",
+    "XRT_MODEL_ATTENUATION", "XRT_MODEL_SIGNED",
 ]
 
 
@@ -60,6 +62,49 @@ def load_ply(path: str) -> np.ndarray:
     finally:
         host.xrt_host_free(ctypes.cast(p, ctypes.c_void_p))
     return out.reshape(count, 9)
+
+
+def load_meshes(path: str) -> list:
+    """Every mesh of a PLY (one) or OBJ (one per object) file, as (T, 9) float32 soups."""
+    host = _abi.load_host()
+    p = ctypes.POINTER(ctypes.c_float)()
+    c = ctypes.POINTER(ctypes.c_uint64)()
+    m = ctypes.c_uint32()
+    rc = host.xrt_host_load_meshes(str(path).encode(), ctypes.byref(p), ctypes.byref(c), ctypes.byref(m))
+    if rc != _abi.XRT_OK:
+        raise XrtError(rc, f"cannot load {path}")
+    try:
+        counts = [int(c[i]) for i in range(m.value)]
+        total = sum(counts)
+        flat = np.ctypeslib.as_array(p, shape=(max(total, 1) * 9,))[: total * 9].copy().reshape(total, 9)
+    finally:
+        host.xrt_host_free(ctypes.cast(p, ctypes.c_void_p))
+        host.xrt_host_free(ctypes.cast(c, ctypes.c_void_p))
+    out, first = [], 0
+    for n in counts:
+        out.append(flat[first:first + n])
+        first += n
+    return out
+
+
+def scene_bbox(meshes):
+    """getBBox over several meshes (src/main.cxx:538-563)."""
+    meshes = [np.ascontiguousarray(m, dtype=np.float32).reshape(-1, 9) for m in meshes]
+    counts = np.array([len(m) for m in meshes], np.uint64)
+    tris = np.ascontiguousarray(np.concatenate(meshes) if meshes else np.zeros((0, 9), np.float32))
+    lo = np.zeros(3, np.float32)
+    hi = np.zeros(3, np.float32)
+    rc = _abi.load().xrt_scene_bbox(_fptr(tris), counts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                    len(counts), _fptr(lo), _fptr(hi))
+    if rc != _abi.XRT_OK:
+        raise XrtError(rc, "xrt_scene_bbox")
+    return lo, hi
+
+
+def camera_for_scene(meshes, width: int, height: int) -> Camera:
+    """The camera of a scene: from the box of every mesh (main.cxx:634)."""
+    lo, hi = scene_bbox(meshes)
+    return camera_from_bbox(lo, hi, width, height)
 
 
 def mesh_bbox(tris: np.ndarray):
@@ -125,6 +170,36 @@ class Context:
 
     def set_kernel(self, kernel: int):
         self._check(self._lib.xrt_set_kernel(self._ctx, int(kernel)), "xrt_set_kernel")
+
+    def set_model(self, model: int, mu: float = 0.1037):
+        """XRT_MODEL_ATTENUATION (main.cxx) or XRT_MODEL_SIGNED (the L-buffer fork, mesh-0 mu)."""
+        self._check(self._lib.xrt_set_model(self._ctx, int(model), float(np.float32(mu))), "xrt_set_model")
+
+    def render_signed(self, cam: Camera):
+        """The L-buffer fork end to end: (image f32, lbuffer f32 with -1 flags, u8, Stats)."""
+        n = cam.width * cam.height
+        img = np.empty(n, np.float32)
+        lb = np.empty(n, np.float32)
+        u8 = np.empty(n, np.uint8)
+        st = Stats()
+        self._check(self._lib.xrt_render_signed(self._ctx, ctypes.byref(cam), _fptr(img), _fptr(lb), _u8ptr(u8),
+                                                ctypes.byref(st)), "xrt_render_signed")
+        return img, lb, u8, st
+
+    def hole_fill(self, lbuffer: np.ndarray, width: int, height: int):
+        """The fork's hole fill of a whole-frame L-buffer: (image f32, u8)."""
+        lb = np.ascontiguousarray(lbuffer, dtype=np.float32).reshape(-1)
+        if lb.size != width * height:
+            raise ValueError("L-buffer size does not match width x height")
+        img = np.empty_like(lb)
+        u8 = np.empty(lb.size, np.uint8)
+        self._check(self._lib.xrt_hole_fill(self._ctx, width, height, _fptr(lb), _fptr(img), _u8ptr(u8)),
+                    "xrt_hole_fill")
+        return img, u8
+
+    def hole_fill_device(self, width: int, height: int, d_lbuffer: int, d_image: int, d_u8: int, stream: int = 0):
+        self._check(self._lib.xrt_hole_fill_device(self._ctx, width, height, d_lbuffer, d_image, d_u8, stream),
+                    "xrt_hole_fill_device")
 
     def set_hit_capacity(self, capacity: int):
         self._check(self._lib.xrt_set_hit_capacity(self._ctx, int(capacity)), "xrt_set_hit_capacity")

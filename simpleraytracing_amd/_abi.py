@@ -31,6 +31,10 @@ XRT_PROBE_SQRTF = 1
 XRT_PROBE_RCP = 2
 XRT_PROBE_LUT_U8 = 3
 XRT_PROBE_RCP_FAST = 4
+XRT_PROBE_SIGNED_L = 5
+
+XRT_MODEL_ATTENUATION = 0
+XRT_MODEL_SIGNED = 1
 
 _f = ctypes.c_float
 _fp = ctypes.POINTER(ctypes.c_float)
@@ -38,6 +42,9 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32 = ctypes.c_uint32
 _u64 = ctypes.c_uint64
 _vp = ctypes.c_void_p
+_dp = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
 class Camera(ctypes.Structure):
@@ -93,6 +100,7 @@ XRT_SYMBOLS = {
     "xrt_device_count": (ctypes.c_int, []),
     "xrt_upload_mesh": (ctypes.c_int, [_CtxP, _fp, _u64]),
     "xrt_mesh_bbox": (ctypes.c_int, [_fp, _u64, _fp, _fp]),
+    "xrt_scene_bbox": (ctypes.c_int, [_fp, _u64p, _u32, _fp, _fp]),
     "xrt_camera_from_bbox": (ctypes.c_int, [_fp, _fp, _u32, _u32, ctypes.POINTER(Camera)]),
     "xrt_set_kernel": (ctypes.c_int, [_CtxP, ctypes.c_int]),
     "xrt_render_rows": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _fp, _fp, _u8p,
@@ -106,6 +114,12 @@ XRT_SYMBOLS = {
     "xrt_probe_math": (ctypes.c_int, [_CtxP, ctypes.c_int, _fp, _fp, _u64]),
     "xrt_probe_prep": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp]),
     "xrt_host_expf_batch": (None, [_fp, _fp, _u64]),
+    "xrt_host_exp_batch": (None, [_dp, _dp, _u64]),
+    "xrt_host_signed_lbuffer_batch": (None, [_fp, _i32p, _f, _fp, _u64]),
+    "xrt_set_model": (ctypes.c_int, [_CtxP, ctypes.c_int, _f]),
+    "xrt_hole_fill": (ctypes.c_int, [_CtxP, _u32, _u32, _fp, _fp, _u8p]),
+    "xrt_hole_fill_device": (ctypes.c_int, [_CtxP, _u32, _u32, _vp, _vp, _vp, _vp]),
+    "xrt_render_signed": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp, _u8p, ctypes.POINTER(Stats)]),
     "xrt_host_mt_check": (None, [_fp, _fp, _fp, _fp, _u64, ctypes.POINTER(ctypes.c_uint8),
                                  ctypes.POINTER(ctypes.c_uint8), _fp]),
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
@@ -129,6 +143,8 @@ XRT_SYMBOLS = {
 # every C symbol declared in include/xrt_host.h
 XRT_HOST_SYMBOLS = {
     "xrt_host_load_ply": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_u64)]),
+    "xrt_host_load_meshes": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_fp), ctypes.POINTER(_u64p),
+                                            ctypes.POINTER(_u32)]),
     "xrt_host_free": (None, [_vp]),
     "xrt_host_intersect_batch": (None, [_fp, _fp, _u64, _u8p, _fp]),
 }

@@ -19,3 +19,6 @@ struct PlyMesh {
 
 // Throws std::runtime_error on I/O or format errors.
 PlyMesh loadPly(const std::string& file_name);
+
+// Wavefront OBJ: one mesh per object / group with faces (ObjLoader.cpp).
+std::vector<PlyMesh> loadObj(const std::string& file_name);

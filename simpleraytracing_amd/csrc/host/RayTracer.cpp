@@ -78,14 +78,26 @@ xrt_context* xrt_host_device_context(int device) { return device_slot(device).ct
 void setRenderKernel(int kernel) { g_kernel = kernel; }
 void setRenderDevice(int device) { g_device = device; }
 
-// Assimp-free loadMeshes: one triangle mesh per file (main.cxx:455-508).
+// Assimp-free loadMeshes (main.cxx:455-508): each mesh of the file through
+// TriangleMesh::setGeometry(vertices, indices), in file order.
+void appendMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes)
+{
+    const std::string ext = file_name.size() >= 4 ? file_name.substr(file_name.size() - 4) : "";
+    std::vector<PlyMesh> parts;
+    if (ext == ".obj" || ext == ".OBJ") parts = loadObj(file_name);
+    else parts.push_back(loadPly(file_name));
+    for (const PlyMesh& part : parts) {
+        TriangleMesh mesh;
+        mesh.setGeometry(part.vertices, part.indices);
+        meshes.push_back(mesh);
+    }
+}
+
 void loadMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes)
 {
-    PlyMesh ply = loadPly(file_name);
-    meshes.clear();
-    TriangleMesh mesh;
-    mesh.setGeometry(ply.vertices, ply.indices);
-    meshes.push_back(mesh);
+    std::vector<TriangleMesh> loaded;
+    appendMeshes(file_name, loaded);
+    meshes.swap(loaded);
 }
 
 // main.cxx:538-563
@@ -200,6 +212,30 @@ unsigned long long renderLoop(Image& image, const std::vector<TriangleMesh>& mes
     return stats.odd_rays;
 }
 
+unsigned long long renderLoopLBuffer(Image& image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info,
+                                     std::vector<float>* lbuffer)
+{
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    DeviceSlot& slot = device_slot(device_choice());
+    std::lock_guard<std::mutex> g(slot.lock);
+    xrt_context* ctx = slot.ctx;
+    int k = kernel_choice();
+    check(ctx, xrt_set_kernel(ctx, k == XRT_KERNEL_TILED ? XRT_KERNEL_BINNED : k), "xrt_set_kernel");
+    if (!slot.uploaded || slot.mesh != soup) {
+        check(ctx, xrt_upload_mesh(ctx, soup.data(), soup.size() / 9), "xrt_upload_mesh");
+        slot.mesh = soup;
+        slot.uploaded = true;
+    }
+    check(ctx, xrt_set_model(ctx, XRT_MODEL_SIGNED, 0.1037f), "xrt_set_model");   // :800
+    if (lbuffer) lbuffer->resize((size_t)image.getWidth() * image.getHeight());
+    xrt_stats stats;
+    const int rc = xrt_render_signed(ctx, &cam, image.getData(), lbuffer ? lbuffer->data() : nullptr, nullptr, &stats);
+    xrt_set_model(ctx, XRT_MODEL_ATTENUATION, 0.0f);
+    check(ctx, rc, "xrt_render_signed");
+    return stats.odd_rays;
+}
+
 // Row strips over num_gpus devices gathered into device 0 with RCCL
 // (xrt_render_rows_multi).  $XRT_MULTI_DEVICES ("0,0" ...) overrides the
 // device list -- a device listed twice rehearses the strip path on one GPU.
@@ -259,6 +295,41 @@ extern "C" int xrt_host_load_ply(const char* path, float** triangles, uint64_t* 
         std::memcpy(out, soup.data(), sizeof(float) * soup.size());
         *triangles = out;
         *num_triangles = soup.size() / 9;
+        return XRT_OK;
+    } catch (const std::exception& e) {
+        return std::string(e.what()).find("Cannot open") != std::string::npos ? XRT_ERR_IO : XRT_ERR_FORMAT;
+    }
+}
+
+extern "C" int xrt_host_load_meshes(const char* path, float** triangles, uint64_t** mesh_triangles,
+                                    uint32_t* num_meshes)
+{
+    if (!path || !triangles || !mesh_triangles || !num_meshes) return XRT_ERR_ARGUMENT;
+    *triangles = nullptr;
+    *mesh_triangles = nullptr;
+    *num_meshes = 0;
+    try {
+        std::vector<TriangleMesh> meshes;
+        loadMeshes(path, meshes);
+        std::vector<float> all;
+        std::vector<uint64_t> counts;
+        for (const TriangleMesh& m : meshes) {
+            std::vector<float> soup = m.flatten();
+            all.insert(all.end(), soup.begin(), soup.end());
+            counts.push_back(soup.size() / 9);
+        }
+        float* t = static_cast<float*>(std::malloc(sizeof(float) * (all.size() ? all.size() : 1)));
+        uint64_t* c = static_cast<uint64_t*>(std::malloc(sizeof(uint64_t) * (counts.size() ? counts.size() : 1)));
+        if (!t || !c) {
+            std::free(t);
+            std::free(c);
+            return XRT_ERR_ARGUMENT;
+        }
+        std::memcpy(t, all.data(), sizeof(float) * all.size());
+        std::memcpy(c, counts.data(), sizeof(uint64_t) * counts.size());
+        *triangles = t;
+        *mesh_triangles = c;
+        *num_meshes = (uint32_t)counts.size();
         return XRT_OK;
     } catch (const std::exception& e) {
         return std::string(e.what()).find("Cannot open") != std::string::npos ? XRT_ERR_IO : XRT_ERR_FORMAT;

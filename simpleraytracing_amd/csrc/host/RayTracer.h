@@ -36,7 +36,11 @@ struct RayTracerInfo {
 void setRenderKernel(int kernel);
 void setRenderDevice(int device);
 
+// Every mesh of a file, replacing `meshes` (main.cxx:455-508): a PLY file is
+// one mesh, an OBJ file one mesh per object.  appendMeshes keeps the meshes
+// already loaded (several input files make one scene; mesh 0 stays first).
 void loadMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes);
+void appendMeshes(const std::string& file_name, std::vector<TriangleMesh>& meshes);
 
 void getBBox(const std::vector<TriangleMesh>& meshes, Vec3& upper, Vec3& lower);
 
@@ -54,6 +58,14 @@ unsigned long long renderLoop(Image& output_image, const std::vector<TriangleMes
 void renderLoopRows(Image& output_image, const std::vector<TriangleMesh>& meshes,
                     const RayTracerInfo& info, unsigned int row_begin, unsigned int row_end,
                     float* lbuffer_strip, unsigned char* u8_strip, xrt_stats* stats);
+
+// The L-buffer fork, src/main-pthreads-lbuffer.cxx: renderLoopCallBack over
+// the whole image (:733-813, the signed multi-material L-buffer, mesh 0's
+// coefficient 0.1037) and main's hole fill (:327-404) into output_image.
+// `lbuffer` (optional) receives the fork's L_buffer (-1 flags).  Returns the
+// number of flagged pixels.
+unsigned long long renderLoopLBuffer(Image& output_image, const std::vector<TriangleMesh>& meshes,
+                                     RayTracerInfo& info, std::vector<float>* lbuffer = nullptr);
 
 // Row strips over `num_gpus` devices (rows_per = H / n, remainder to the first
 // strips), one host thread per device; returns the number of odd rays.

@@ -6,12 +6,15 @@
 //   -b, --background R G B     parsed and unused, as in the reference
 //   -f, --filename NAME        output text file "./out/NAME" (default test.jpg,
 //                              which, as in the reference, receives text)
-//   -i, --input FILE           mesh (default ./dragon.ply)
+//   -i, --input FILE           mesh file (default ./dragon.ply); repeatable: the
+//                              files' meshes make one scene, in order
 // additions:
 //   -g, --gpus N               row strips over N GPUs (default 1)
 //   -k, --kernel brute|tiled|binned  render kernel (default: automatic -- tiled
 //                              for small frames, binned past 2e7 footprint tests)
 //   -t, --threads N            accepted for main-pthreads*.cxx compatibility (ignored)
+//       --signed               the L-buffer fork (main-pthreads-lbuffer.cxx): signed
+//                              multi-material L-buffer + hole fill
 //       --lbuffer FILE         also write the L-buffer as raw little-endian f32
 //       --u8 FILE              also write the 8-bit image (LUT 0..80) as PGM
 //       --time                 print render wall-clock and Mrays/s
@@ -37,9 +40,10 @@ void showUsage(const std::string& prog)
               << "\t-s,--size IMG_WIDTH IMG_HEIGHT\tSpecify the image size in number of pixels (default values: 2048 2048)\n"
               << "\t-b,--background R G B\t\tSpecify the background colour in RGB (accepted, unused)\n"
               << "\t-f,--filename FILENAME\t\tName of the output text file, written to ./out/ (default: test.jpg)\n"
-              << "\t-i,--input FILENAME\t\tInput mesh (default: ./dragon.ply)\n"
+              << "\t-i,--input FILENAME\t\tInput mesh, PLY or OBJ (default: ./dragon.ply); repeat for a scene of several files\n"
               << "\t-g,--gpus N\t\t\tRender row strips on N GPUs (default: 1)\n"
               << "\t-k,--kernel brute|tiled|binned\tRender kernel (default: automatic)\n"
+              << "\t--signed\t\t\tSigned multi-material L-buffer and hole fill (main-pthreads-lbuffer.cxx)\n"
               << "\t--lbuffer FILE\t\t\tWrite the L-buffer as raw float32\n"
               << "\t--u8 FILE\t\t\tWrite the 8-bit image (0..80 keV LUT) as PGM\n"
               << "\t--time\t\t\t\tPrint render time and Mrays/s\n"
@@ -48,12 +52,13 @@ void showUsage(const std::string& prog)
 
 struct Options {
     std::string output = "test.jpg";
-    std::string input = "./dragon.ply";
+    std::vector<std::string> inputs;
     unsigned width = 2048, height = 2048;
     int gpus = 1;
     int kernel = XRT_KERNEL_AUTO;
     std::string lbuffer, u8;
     bool time = false;
+    bool signed_model = false;
 };
 
 unsigned parse_uint(const char* prog, int argc, char** argv, int& i)
@@ -90,7 +95,7 @@ Options processCmd(int argc, char** argv)
         } else if (a == "-f" || a == "--filename") {
             o.output = "./out/" + parse_str(argv[0], argc, argv, i);
         } else if (a == "-i" || a == "--input") {
-            o.input = parse_str(argv[0], argc, argv, i);
+            o.inputs.push_back(parse_str(argv[0], argc, argv, i));
         } else if (a == "-g" || a == "--gpus") {
             o.gpus = (int)parse_uint(argv[0], argc, argv, i);
         } else if (a == "-t" || a == "--threads") {
@@ -108,6 +113,8 @@ Options processCmd(int argc, char** argv)
             o.lbuffer = parse_str(argv[0], argc, argv, i);
         } else if (a == "--u8") {
             o.u8 = parse_str(argv[0], argc, argv, i);
+        } else if (a == "--signed") {
+            o.signed_model = true;
         } else if (a == "--time") {
             o.time = true;
         } else {
@@ -115,6 +122,7 @@ Options processCmd(int argc, char** argv)
             std::exit(EXIT_FAILURE);
         }
     }
+    if (o.inputs.empty()) o.inputs.push_back("./dragon.ply");
     return o;
 }
 
@@ -129,7 +137,8 @@ int main(int argc, char** argv)
         std::cout << "Loading polygon meshes... " << std::endl;
         auto t0 = std::chrono::high_resolution_clock::now();
         std::vector<TriangleMesh> meshes;
-        loadMeshes(opt.input, meshes);
+        loadMeshes(opt.inputs[0], meshes);
+        for (size_t f = 1; f < opt.inputs.size(); ++f) appendMeshes(opt.inputs[f], meshes);
         auto t1 = std::chrono::high_resolution_clock::now();
         std::cout << "Loading meshes took: " << std::chrono::duration<double>(t1 - t0).count()
                   << " seconds" << std::endl
@@ -144,7 +153,9 @@ int main(int argc, char** argv)
 
         auto r0 = std::chrono::high_resolution_clock::now();
         std::vector<float> lb;
-        if (opt.gpus > 1) {
+        if (opt.signed_model) {
+            renderLoopLBuffer(image, meshes, info, opt.lbuffer.empty() ? nullptr : &lb);
+        } else if (opt.gpus > 1) {
             renderLoopMultiGPU(image, meshes, info, opt.gpus);
         } else if (!opt.lbuffer.empty()) {       // the image and the L-buffer in one render
             lb.resize((size_t)opt.width * opt.height);

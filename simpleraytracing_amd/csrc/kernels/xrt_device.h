@@ -113,7 +113,12 @@ struct RenderParams {
     uint32_t num_triangles;
     uint32_t hit_capacity;  // <= XRT_MAX_HITS
     uint32_t ablate;        // diagnostics only ($XRT_ABLATE bits, kAblate*); 0 in production
+    uint32_t model;         // kModelAttenuation (main.cxx) or kModelSigned (the L-buffer fork)
 };
+
+// What a render computes per ray.
+constexpr uint32_t kModelAttenuation = 0;   // renderLoop, src/main.cxx:626-743
+constexpr uint32_t kModelSigned = 1;        // renderLoopCallBack, src/main-pthreads-lbuffer.cxx:733-813
 
 // Ablation bits (timing studies; outputs are wrong when any is set).  Only
 // XRT_ABLATION builds (tools/gpu_ablate.sh) read them: the production kernels
@@ -172,7 +177,15 @@ __device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
 
 template <typename P>
 __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_off, float& dx,
-                                              float& dy, float& dz);
+                                              float& dy, float& dz, float& sx, float& sy, float& sz);
+
+template <typename P>
+__device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_off, float& dx,
+                                              float& dy, float& dz)
+{
+    float sx, sy, sz;
+    make_ray_from(p, v_off, u_off, dx, dy, dz, sx, sy, sz);
+}
 
 template <typename P>
 __device__ __forceinline__ void make_ray(const P& p, uint32_t row, uint32_t col,
@@ -190,9 +203,12 @@ __device__ __forceinline__ void make_ray(const P& p, const PixelOffsets& off, ui
     make_ray_from(p, off.v[row], off.u[col], dx, dy, dz);
 }
 
+// Also returns the direction after the first normalisation (sx, sy, sz): the
+// L-buffer fork takes sign(direction . normal) with it, not with the Ray's
+// twice-normalised copy (main-pthreads-lbuffer.cxx:761-762, :791).
 template <typename P>
 __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_off, float& dx,
-                                              float& dy, float& dz)
+                                              float& dy, float& dz, float& sx, float& sy, float& sz)
 {
     // :659  detector + up*v + right*u - origin  (Vec3 ops left to right, f32)
     float X = ((p.cx + p.ux * v_off) + p.rx * u_off) - p.ox;
@@ -203,6 +219,9 @@ __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_o
     X = X / len;
     Y = Y / len;
     Z = Z / len;
+    sx = X;
+    sy = Y;
+    sz = Z;
     // Ray ctor normalises again; a zero length keeps the default (0,0,0).
     float len2 = sqrtf((X * X + Y * Y) + Z * Z);
     if (len2 != 0.0f) {
@@ -440,6 +459,69 @@ struct HitList {
 };
 
 // ---------------------------------------------------------------------------
+// Signed hit list of the L-buffer fork (main-pthreads-lbuffer.cxx:778-795):
+// the per-hit terms sign(direction . normal) * t kept in triangle order --
+// the f32 sum runs in that order -- and the sum of the signs.  Slots hold
+// (triangle id, term) ascending by id, 0xFFFFFFFF past the end; n and
+// sign_sum count every hit, so a ray with more hits than slots knows it and
+// its flag is exact (finish_ray_signed recomputes the sum).
+// ---------------------------------------------------------------------------
+struct SignedHits {
+    uint32_t id[kMaxHits];
+    float v[kMaxHits];
+    uint32_t n;
+    int sign_sum;
+
+    __device__ __forceinline__ void init()
+    {
+#pragma unroll
+        for (int k = 0; k < kMaxHits; ++k) {
+            id[k] = 0xFFFFFFFFu;
+            v[k] = 0.0f;
+        }
+        n = 0;
+        sign_sum = 0;
+    }
+
+    // :791-793  sign = signum(direction . normal), distance += sign * t
+    __device__ __forceinline__ void push_if(bool hit, float t, uint32_t tid, int sign)
+    {
+        if (!hit) return;
+        ++n;
+        sign_sum += sign;
+        uint32_t cid = tid;
+        float cv = (float)sign * t;
+#pragma unroll
+        for (int k = 0; k < kMaxHits; ++k) {   // sorted insert by id (ids are distinct)
+            const bool lt = cid < id[k];
+            const uint32_t oid = id[k];
+            const float ov = v[k];
+            id[k] = lt ? cid : oid;
+            v[k] = lt ? cv : ov;
+            cid = lt ? oid : cid;
+            cv = lt ? ov : cv;
+        }
+    }
+
+    // :778, :792: 0.0f plus the terms in triangle order, sequential f32
+    __device__ __forceinline__ float distance() const
+    {
+        float d = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kMaxHits; ++k)
+            if ((uint32_t)k < n) d += v[k];
+        return d;
+    }
+};
+
+// signum(direction . normal) of the fork (:729-731, :791), Vec3::dotProduct's order.
+__host__ __device__ __forceinline__ int hit_sign(float sx, float sy, float sz, float nx, float ny, float nz)
+{
+    const float dp = (sx * nx + sy * ny) + sz * nz;
+    return (int)(0.0f < dp) - (int)(dp < 0.0f);
+}
+
+// ---------------------------------------------------------------------------
 // glibc 2.35 expf (sysdeps/ieee754/flt-32/e_expf.c with e_exp2f_data.c,
 // EXP2F_TABLE_BITS = 5), as x86-64 glibc dispatches it on FMA hardware
 // (e_expf-fma.c: the compiler fuses InvLn2N*x into both uses and the
@@ -510,6 +592,146 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     return (float)y;
 }
 
+// ---------------------------------------------------------------------------
+// glibc 2.35 exp (sysdeps/ieee754/dbl-64/e_exp.c with exp_data.c,
+// EXP_TABLE_BITS = 7, EXP_POLY_ORDER = 5) as x86-64 glibc dispatches it on FMA
+// hardware (e_exp-fma.c: the compiler fuses kd = InvLn2N*x + Shift, the two
+// steps of r, the polynomial's multiply-adds and scale + scale*tmp, except in
+// the special case's k < 0 branch -- found by the exhaustive check).  The
+// function std::exp(double) binds to in src/main-pthreads-lbuffer.cxx:808.
+// Table: tools/gen_exp_table.py (equal to the one inside the system libm);
+// the function: tests/test_abi.py::test_host_exp_restatement_matches_libm
+// (every exponent the signed L-buffer can produce) and the device probe.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t xrt_exp_tab(uint32_t i)
+{
+    constexpr uint64_t tab[256] = {
+        0x0000000000000000ULL, 0x3ff0000000000000ULL, 0x3c9b3b4f1a88bf6eULL, 0x3feff63da9fb3335ULL,
+        0xbc7160139cd8dc5dULL, 0x3fefec9a3e778061ULL, 0xbc905e7a108766d1ULL, 0x3fefe315e86e7f85ULL,
+        0x3c8cd2523567f613ULL, 0x3fefd9b0d3158574ULL, 0xbc8bce8023f98efaULL, 0x3fefd06b29ddf6deULL,
+        0x3c60f74e61e6c861ULL, 0x3fefc74518759bc8ULL, 0x3c90a3e45b33d399ULL, 0x3fefbe3ecac6f383ULL,
+        0x3c979aa65d837b6dULL, 0x3fefb5586cf9890fULL, 0x3c8eb51a92fdeffcULL, 0x3fefac922b7247f7ULL,
+        0x3c3ebe3d702f9cd1ULL, 0x3fefa3ec32d3d1a2ULL, 0xbc6a033489906e0bULL, 0x3fef9b66affed31bULL,
+        0xbc9556522a2fbd0eULL, 0x3fef9301d0125b51ULL, 0xbc5080ef8c4eea55ULL, 0x3fef8abdc06c31ccULL,
+        0xbc91c923b9d5f416ULL, 0x3fef829aaea92de0ULL, 0x3c80d3e3e95c55afULL, 0x3fef7a98c8a58e51ULL,
+        0xbc801b15eaa59348ULL, 0x3fef72b83c7d517bULL, 0xbc8f1ff055de323dULL, 0x3fef6af9388c8deaULL,
+        0x3c8b898c3f1353bfULL, 0x3fef635beb6fcb75ULL, 0xbc96d99c7611eb26ULL, 0x3fef5be084045cd4ULL,
+        0x3c9aecf73e3a2f60ULL, 0x3fef54873168b9aaULL, 0xbc8fe782cb86389dULL, 0x3fef4d5022fcd91dULL,
+        0x3c8a6f4144a6c38dULL, 0x3fef463b88628cd6ULL, 0x3c807a05b0e4047dULL, 0x3fef3f49917ddc96ULL,
+        0x3c968efde3a8a894ULL, 0x3fef387a6e756238ULL, 0x3c875e18f274487dULL, 0x3fef31ce4fb2a63fULL,
+        0x3c80472b981fe7f2ULL, 0x3fef2b4565e27cddULL, 0xbc96b87b3f71085eULL, 0x3fef24dfe1f56381ULL,
+        0x3c82f7e16d09ab31ULL, 0x3fef1e9df51fdee1ULL, 0xbc3d219b1a6fbffaULL, 0x3fef187fd0dad990ULL,
+        0x3c8b3782720c0ab4ULL, 0x3fef1285a6e4030bULL, 0x3c6e149289cecb8fULL, 0x3fef0cafa93e2f56ULL,
+        0x3c834d754db0abb6ULL, 0x3fef06fe0a31b715ULL, 0x3c864201e2ac744cULL, 0x3fef0170fc4cd831ULL,
+        0x3c8fdd395dd3f84aULL, 0x3feefc08b26416ffULL, 0xbc86a3803b8e5b04ULL, 0x3feef6c55f929ff1ULL,
+        0xbc924aedcc4b5068ULL, 0x3feef1a7373aa9cbULL, 0xbc9907f81b512d8eULL, 0x3feeecae6d05d866ULL,
+        0xbc71d1e83e9436d2ULL, 0x3feee7db34e59ff7ULL, 0xbc991919b3ce1b15ULL, 0x3feee32dc313a8e5ULL,
+        0x3c859f48a72a4c6dULL, 0x3feedea64c123422ULL, 0xbc9312607a28698aULL, 0x3feeda4504ac801cULL,
+        0xbc58a78f4817895bULL, 0x3feed60a21f72e2aULL, 0xbc7c2c9b67499a1bULL, 0x3feed1f5d950a897ULL,
+        0x3c4363ed60c2ac11ULL, 0x3feece086061892dULL, 0x3c9666093b0664efULL, 0x3feeca41ed1d0057ULL,
+        0x3c6ecce1daa10379ULL, 0x3feec6a2b5c13cd0ULL, 0x3c93ff8e3f0f1230ULL, 0x3feec32af0d7d3deULL,
+        0x3c7690cebb7aafb0ULL, 0x3feebfdad5362a27ULL, 0x3c931dbdeb54e077ULL, 0x3feebcb299fddd0dULL,
+        0xbc8f94340071a38eULL, 0x3feeb9b2769d2ca7ULL, 0xbc87deccdc93a349ULL, 0x3feeb6daa2cf6642ULL,
+        0xbc78dec6bd0f385fULL, 0x3feeb42b569d4f82ULL, 0xbc861246ec7b5cf6ULL, 0x3feeb1a4ca5d920fULL,
+        0x3c93350518fdd78eULL, 0x3feeaf4736b527daULL, 0x3c7b98b72f8a9b05ULL, 0x3feead12d497c7fdULL,
+        0x3c9063e1e21c5409ULL, 0x3feeab07dd485429ULL, 0x3c34c7855019c6eaULL, 0x3feea9268a5946b7ULL,
+        0x3c9432e62b64c035ULL, 0x3feea76f15ad2148ULL, 0xbc8ce44a6199769fULL, 0x3feea5e1b976dc09ULL,
+        0xbc8c33c53bef4da8ULL, 0x3feea47eb03a5585ULL, 0xbc845378892be9aeULL, 0x3feea34634ccc320ULL,
+        0xbc93cedd78565858ULL, 0x3feea23882552225ULL, 0x3c5710aa807e1964ULL, 0x3feea155d44ca973ULL,
+        0xbc93b3efbf5e2228ULL, 0x3feea09e667f3bcdULL, 0xbc6a12ad8734b982ULL, 0x3feea012750bdabfULL,
+        0xbc6367efb86da9eeULL, 0x3fee9fb23c651a2fULL, 0xbc80dc3d54e08851ULL, 0x3fee9f7df9519484ULL,
+        0xbc781f647e5a3ecfULL, 0x3fee9f75e8ec5f74ULL, 0xbc86ee4ac08b7db0ULL, 0x3fee9f9a48a58174ULL,
+        0xbc8619321e55e68aULL, 0x3fee9feb564267c9ULL, 0x3c909ccb5e09d4d3ULL, 0x3feea0694fde5d3fULL,
+        0xbc7b32dcb94da51dULL, 0x3feea11473eb0187ULL, 0x3c94ecfd5467c06bULL, 0x3feea1ed0130c132ULL,
+        0x3c65ebe1abd66c55ULL, 0x3feea2f336cf4e62ULL, 0xbc88a1c52fb3cf42ULL, 0x3feea427543e1a12ULL,
+        0xbc9369b6f13b3734ULL, 0x3feea589994cce13ULL, 0xbc805e843a19ff1eULL, 0x3feea71a4623c7adULL,
+        0xbc94d450d872576eULL, 0x3feea8d99b4492edULL, 0x3c90ad675b0e8a00ULL, 0x3feeaac7d98a6699ULL,
+        0x3c8db72fc1f0eab4ULL, 0x3feeace5422aa0dbULL, 0xbc65b6609cc5e7ffULL, 0x3feeaf3216b5448cULL,
+        0x3c7bf68359f35f44ULL, 0x3feeb1ae99157736ULL, 0xbc93091fa71e3d83ULL, 0x3feeb45b0b91ffc6ULL,
+        0xbc5da9b88b6c1e29ULL, 0x3feeb737b0cdc5e5ULL, 0xbc6c23f97c90b959ULL, 0x3feeba44cbc8520fULL,
+        0xbc92434322f4f9aaULL, 0x3feebd829fde4e50ULL, 0xbc85ca6cd7668e4bULL, 0x3feec0f170ca07baULL,
+        0x3c71affc2b91ce27ULL, 0x3feec49182a3f090ULL, 0x3c6dd235e10a73bbULL, 0x3feec86319e32323ULL,
+        0xbc87c50422622263ULL, 0x3feecc667b5de565ULL, 0x3c8b1c86e3e231d5ULL, 0x3feed09bec4a2d33ULL,
+        0xbc91bbd1d3bcbb15ULL, 0x3feed503b23e255dULL, 0x3c90cc319cee31d2ULL, 0x3feed99e1330b358ULL,
+        0x3c8469846e735ab3ULL, 0x3feede6b5579fdbfULL, 0xbc82dfcd978e9db4ULL, 0x3feee36bbfd3f37aULL,
+        0x3c8c1a7792cb3387ULL, 0x3feee89f995ad3adULL, 0xbc907b8f4ad1d9faULL, 0x3feeee07298db666ULL,
+        0xbc55c3d956dcaebaULL, 0x3feef3a2b84f15fbULL, 0xbc90a40e3da6f640ULL, 0x3feef9728de5593aULL,
+        0xbc68d6f438ad9334ULL, 0x3feeff76f2fb5e47ULL, 0xbc91eee26b588a35ULL, 0x3fef05b030a1064aULL,
+        0x3c74ffd70a5fddcdULL, 0x3fef0c1e904bc1d2ULL, 0xbc91bdfbfa9298acULL, 0x3fef12c25bd71e09ULL,
+        0x3c736eae30af0cb3ULL, 0x3fef199bdd85529cULL, 0x3c8ee3325c9ffd94ULL, 0x3fef20ab5fffd07aULL,
+        0x3c84e08fd10959acULL, 0x3fef27f12e57d14bULL, 0x3c63cdaf384e1a67ULL, 0x3fef2f6d9406e7b5ULL,
+        0x3c676b2c6c921968ULL, 0x3fef3720dcef9069ULL, 0xbc808a1883ccb5d2ULL, 0x3fef3f0b555dc3faULL,
+        0xbc8fad5d3ffffa6fULL, 0x3fef472d4a07897cULL, 0xbc900dae3875a949ULL, 0x3fef4f87080d89f2ULL,
+        0x3c74a385a63d07a7ULL, 0x3fef5818dcfba487ULL, 0xbc82919e2040220fULL, 0x3fef60e316c98398ULL,
+        0x3c8e5a50d5c192acULL, 0x3fef69e603db3285ULL, 0x3c843a59ac016b4bULL, 0x3fef7321f301b460ULL,
+        0xbc82d52107b43e1fULL, 0x3fef7c97337b9b5fULL, 0xbc892ab93b470dc9ULL, 0x3fef864614f5a129ULL,
+        0x3c74b604603a88d3ULL, 0x3fef902ee78b3ff6ULL, 0x3c83c5ec519d7271ULL, 0x3fef9a51fbc74c83ULL,
+        0xbc8ff7128fd391f0ULL, 0x3fefa4afa2a490daULL, 0xbc8dae98e223747dULL, 0x3fefaf482d8e67f1ULL,
+        0x3c8ec3bc41aa2008ULL, 0x3fefba1bee615a27ULL, 0x3c842b94c3a9eb32ULL, 0x3fefc52b376bba97ULL,
+        0x3c8a64a931d185eeULL, 0x3fefd0765b6e4540ULL, 0xbc8e37bae43be3edULL, 0x3fefdbfdad9cbe14ULL,
+        0x3c77893b4d91cd9dULL, 0x3fefe7c1819e90d8ULL, 0x3c5305c14160cc89ULL, 0x3feff3c22b8f71f1ULL,
+    };
+    return tab[i & 255u];
+}
+
+__host__ __device__ __forceinline__ double xrt_exp_special(double tmp, uint64_t sbits, uint64_t ki)
+{
+    if ((ki & 0x80000000u) == 0) {              // k > 0: the scale's exponent may have overflowed
+        sbits -= 1009ull << 52;
+        const double scale = xrt_u64_as_double(sbits);
+        return 0x1p1009 * __builtin_fma(scale, tmp, scale);
+    }
+    sbits += 1022ull << 52;                     // k < 0: subnormal range
+    const double scale = xrt_u64_as_double(sbits);
+    double y = scale + scale * tmp;
+    if (y < 1.0) {
+        double lo = scale - y + scale * tmp;
+        const double hi = 1.0 + y;
+        lo = 1.0 - hi + y + lo;
+        y = (hi + lo) - 1.0;
+        if (y == 0.0) y = 0.0;                  // no -0.0
+    }
+    return 0x1p-1022 * y;
+}
+
+__host__ __device__ __forceinline__ double xrt_exp(double x)
+{
+    constexpr double kInvLn2N = 0x1.71547652b82fep0 * 128;
+    constexpr double kNegLn2hiN = -0x1.62e42fefa0000p-8;
+    constexpr double kNegLn2loN = -0x1.cf79abc9e3b3ap-47;
+    constexpr double kShift = 0x1.8p52;
+    constexpr double kC2 = 0x1.ffffffffffdbdp-2;
+    constexpr double kC3 = 0x1.555555555543cp-3;
+    constexpr double kC4 = 0x1.55555cf172b91p-5;
+    constexpr double kC5 = 0x1.1111167a4d017p-7;
+
+    const uint64_t ix = xrt_double_as_u64(x);
+    uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ffu;
+    if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {   // |x| < 2^-54, |x| >= 512, inf or NaN
+        if (abstop - 0x3c9u >= 0x80000000u) return 1.0 + x;
+        if (abstop >= 0x409u) {                 // |x| >= 1024
+            if (ix == 0xfff0000000000000ull) return 0.0;
+            if (abstop >= 0x7ffu) return 1.0 + x;
+            return (ix >> 63) ? 0.0 : __builtin_inf();
+        }
+        abstop = 0;                             // large |x|: the special case below
+    }
+    double kd = __builtin_fma(kInvLn2N, x, kShift);
+    const uint64_t ki = xrt_double_as_u64(kd);
+    kd -= kShift;
+    const double r = __builtin_fma(kd, kNegLn2loN, __builtin_fma(kd, kNegLn2hiN, x));
+    const uint32_t idx = 2u * (uint32_t)(ki & 127u);
+    const uint64_t top = ki << 45;
+    const double tail = xrt_u64_as_double(xrt_exp_tab(idx));
+    const uint64_t sbits = xrt_exp_tab(idx + 1u) + top;
+    const double r2 = r * r;
+    const double tmp = __builtin_fma(r2 * r2, __builtin_fma(r, kC5, kC4),
+                                     __builtin_fma(r2, __builtin_fma(r, kC3, kC2), tail + r));
+    if (abstop == 0) return xrt_exp_special(tmp, sbits, ki);
+    const double scale = xrt_u64_as_double(sbits);
+    return __builtin_fma(scale, tmp, scale);
+}
+
 __host__ __device__ __forceinline__ float xrt_f32_from_bits(uint32_t u)
 {
     float f;
@@ -533,6 +755,19 @@ __host__ __device__ __forceinline__ float shade(float distance)
     if (distance != distance) return xrt_f32_from_bits(kX86ShadeNaN);
     float cm = (float)((double)distance * 0.1);
     return 80.000f * xrt_expf(-(0.3971f * cm));
+}
+
+// The fork's L-buffer update for mesh 0 (main-pthreads-lbuffer.cxx:805-808):
+// L = 80 (its initial value, :314) times exp(-(mu * (distance * 0.1))) in f64,
+// rounded to f32; -1 when the signs do not cancel.  A NaN distance (x86's
+// default NaN from inf - inf or 0 * inf) gives 0x7FC00000 there: the f64
+// negation flips its sign before exp returns it.
+constexpr uint32_t kX86SignedNaN = 0x7FC00000u;
+__host__ __device__ __forceinline__ float signed_lbuffer(float distance, int sign_sum, float mu)
+{
+    if (sign_sum != 0) return -1.0f;
+    if (distance != distance) return xrt_f32_from_bits(kX86SignedNaN);
+    return (float)((double)80.000f * xrt_exp(-((double)mu * ((double)distance * 0.1))));
 }
 
 // 8-bit image: Image::applyLUT's per-pixel formula (include/Image.inl:195-211)

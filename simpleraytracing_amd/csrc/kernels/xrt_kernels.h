@@ -83,6 +83,7 @@ struct Outputs {
     // z_buffer), or a transit code for strips gathered as L-buffers only
     // (kMissTransit, expanded on the receiving device by k_expand).
     float miss_l;
+    float mu;                  // kModelSigned: mesh 0's attenuation coefficient (fork :800)
 };
 
 // A signalling NaN no render produces (path lengths are >= 0, +inf, or x86's
@@ -97,6 +98,15 @@ __device__ __forceinline__ void make_tile_ray(const RenderParams& p, const Outpu
                                               uint32_t col, float& dx, float& dy, float& dz)
 {
     make_ray(*out.frame, out.off, min(row, p.height - 1u), min(col, p.width - 1u), dx, dy, dz);
+}
+
+// With the once-normalised direction too (the signed model's sign test).
+__device__ __forceinline__ void make_tile_ray(const RenderParams& p, const Outputs& out, uint32_t row,
+                                              uint32_t col, float& dx, float& dy, float& dz, float& sx,
+                                              float& sy, float& sz)
+{
+    const uint32_t r = min(row, p.height - 1u), c = min(col, p.width - 1u);
+    make_ray_from(*out.frame, out.off.v[r], out.off.u[c], dx, dy, dz, sx, sy, sz);
 }
 
 // Running counters of one wave: ballot counts (wave-uniform), per-lane hit sum
@@ -472,6 +482,74 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
     if (out.image_u8) out.image_u8[o] = u8;
 }
 
+// The signed model's exact sum for a ray with more hits than its list holds,
+// by the whole wave: the hits in triangle order by repeated scans for the
+// next larger triangle id (ids are distinct), each term added in turn.  Ray
+// (both directions) and result are wave-uniform; rare path.
+template <typename Fetch>
+__device__ float wave_signed_overflow_distance(const TriRec* __restrict__ recs, uint32_t n_cand, Fetch fetch,
+                                               float dx, float dy, float dz, float sx, float sy, float sz)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    float distance = 0.0f;
+    uint32_t prev = 0;
+    bool first = true;
+    for (;;) {
+        uint32_t best = 0xFFFFFFFFu;
+        for (uint32_t base = 0; base < n_cand; base += 64u) {
+            const uint32_t k = base + lane;
+            if (k >= n_cand) continue;
+            const uint32_t j = fetch(k);
+            float t;
+            if ((first || j > prev) && j < best && fixup_hit(recs, j, dx, dy, dz, t)) best = j;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)best, off);
+            best = o < best ? o : best;
+        }
+        best = wave_uniform(best);
+        if (best == 0xFFFFFFFFu) break;
+        float t = 0.0f;
+        fixup_hit(recs, best, dx, dy, dz, t);
+        const TriRec& r = recs[best];
+        distance += (float)hit_sign(sx, sy, sz, r.pad0, r.pad1, r.pad2) * t;
+        prev = best;
+        first = false;
+    }
+    return distance;
+}
+
+// finish_ray of the signed model: the fork's L-buffer value (-1 flags) into
+// out.lbuffer (image and u8 come from the hole fill, k_hole_fill).  The odd
+// counter counts flagged rays.
+template <typename Fetch>
+__device__ __forceinline__ void finish_ray_signed(const RenderParams& p, const Outputs& out, bool active,
+                                                  uint32_t row, uint32_t col, const SignedHits& hl,
+                                                  WaveStats& ws, const TriRec* __restrict__ recs, float dx,
+                                                  float dy, float dz, float sx, float sy, float sz,
+                                                  uint32_t n_cand, Fetch fetch)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool overflow = hl.n > p.hit_capacity;
+    const bool flagged = hl.sign_sum != 0;
+    wave_stats(ws, active, hl.n, flagged, overflow);
+    float distance = hl.distance();
+    unsigned long long om = __ballot(active && overflow && !flagged);
+    while (om) {                                      // wave-uniform
+        const uint32_t L = (uint32_t)__builtin_ctzll(om);
+        om &= om - 1ull;
+        auto at = [L](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)L)); };
+        const float d = wave_signed_overflow_distance(recs, n_cand, fetch, at(dx), at(dy), at(dz), at(sx),
+                                                      at(sy), at(sz));
+        if (lane == L) distance = d;
+    }
+    if (!active || !out.lbuffer) return;
+    float lval = 80.0f;                               // no term: 80 * exp(-0.0)
+    if (__ballot(distance != 0.0f || flagged)) lval = signed_lbuffer(distance, hl.sign_sum, out.mu);
+    out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = lval;
+}
+
 // Loads one triangle record with a wave-uniform index (scalar loads).
 __device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
                                             float dy, float dz, HitList& hl)
@@ -488,6 +566,20 @@ __device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uin
 // ---------------------------------------------------------------------------
 // k_render_brute: block = 256 lanes = 2x2 waves, each wave one 8x8 ray tile.
 // ---------------------------------------------------------------------------
+// The signed model's test: the term's sign from the record's unit normal.
+__device__ __forceinline__ void test_record(const TriRec* __restrict__ recs, uint32_t j, float dx,
+                                            float dy, float dz, float sx, float sy, float sz, SignedHits& hl)
+{
+    const float4* q = reinterpret_cast<const float4*>(recs + j);
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    float t;
+    const bool hit =
+        mt_intersect(dx, dy, dz, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, t) &&
+        accept_t(t);
+    if (__ballot(hit)) hl.push_if(hit, t, j, hit_sign(sx, sy, sz, d.y, d.z, d.w));
+}
+
+template <bool kSigned>
 __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__ recs,
                                                       RenderParams p, Outputs out)
 {
@@ -497,15 +589,22 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     const uint32_t row = p.row_begin + (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
     const bool active = col < p.width && row < p.row_end;
 
-    float dx, dy, dz;
-    make_tile_ray(p, out, row, col, dx, dy, dz);
-    HitList hl;
+    float dx, dy, dz, sx, sy, sz;
+    make_tile_ray(p, out, row, col, dx, dy, dz, sx, sy, sz);
+    typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     const uint32_t T = p.num_triangles;
-    for (uint32_t j = 0; j < T; ++j) test_record(recs, j, dx, dy, dz, hl);
+    for (uint32_t j = 0; j < T; ++j) {
+        if constexpr (kSigned) test_record(recs, j, dx, dy, dz, sx, sy, sz, hl);
+        else test_record(recs, j, dx, dy, dz, hl);
+    }
     WaveStats ws = {};
     ws.tile_tests = T;
-    finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, T, [](uint32_t k) { return k; });
+    auto fetch = [](uint32_t k) { return k; };
+    if constexpr (kSigned)
+        finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, T, fetch);
+    else
+        finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, T, fetch);
     store_block_stats(ws, 0u, out.block_stats);
 }
 
@@ -1079,6 +1178,15 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
         r.qvz = r.tvx * r.e1y - r.tvy * r.e1x;
         r.tnum = (r.e2x * r.qvx + r.e2y * r.qvy) + r.e2z * r.qvz;
         r.pad0 = r.pad1 = r.pad2 = 0.0f;
+        if (p.model == kModelSigned) {             // Triangle::computeNormal, Triangle.inl:170-178
+            const float nx = r.e1y * r.e2z - r.e1z * r.e2y;
+            const float ny = r.e1z * r.e2x - r.e1x * r.e2z;
+            const float nz = r.e1x * r.e2y - r.e1y * r.e2x;
+            const float len = sqrtf((nx * nx + ny * ny) + nz * nz);
+            r.pad0 = nx / len;
+            r.pad1 = ny / len;
+            r.pad2 = nz / len;
+        }
         recs[i] = r;
         if (culls) {
             fp = compute_footprint(r, p, cp);
@@ -1349,6 +1457,20 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     hl.push_if(h, t);
 }
 
+// The signed model's: the term's triangle id from the footprint (e0.w) and its
+// sign from the record's unit normal (pad0..2).
+__device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
+                                                float dz, float sx, float sy, float sz, SignedHits& hl)
+{
+    const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k], a3 = st.q[7][k];
+    float det, u, v;
+    mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
+                  det, u, v);
+    bool h;
+    const float t = mt_finish(det, u, v, a3.x, h);
+    if (__ballot(h)) hl.push_if(h, t, __float_as_uint(st.q[0][k].w), hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
+}
+
 // Two survivors at once: independent dependency chains for the scheduler to
 // interleave (the hit set, and so the sorted list, does not depend on the order).
 __device__ __forceinline__ void test_staged_pair(const RegionStage& st, uint32_t k0, uint32_t k1, bool two,
@@ -1381,7 +1503,8 @@ __device__ __forceinline__ void test_staged_pair(const RegionStage& st, uint32_t
 // tiles), regions in the launch order of bins.order; each wave stores its own
 // statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
 // occupancy is what hides it.
-__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(XRT_RENDER_WAVES, 8))) void k_render_binned(
+template <bool kSigned>
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(kSigned ? 5 : XRT_RENDER_WAVES, 8))) void k_render_binned(
     const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
     BinBuffers bins, const BinState* __restrict__ bs)
 {
@@ -1436,8 +1559,9 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
+    float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
     bool have_ray = false;                         // wave-uniform
-    HitList hl;
+    typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
     // every wave of the workgroup takes part in every round's staging and barriers
@@ -1459,10 +1583,18 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
             if (!m) continue;
             tests += (uint32_t)__popcll(m);
             if (!have_ray) {
-                if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
+                if constexpr (kSigned) make_tile_ray(p, out, row, col, dx, dy, dz, sx, sy, sz);
+                else if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
                 have_ray = true;
             }
             if (ablation(p) & kAblateExact) continue;
+            if constexpr (kSigned) {
+                while (m) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1ull;
+                    test_staged_one(st, k0 + b, dx, dy, dz, sx, sy, sz, hl);
+                }
+            } else {
 #if XRT_STAGED_PAIRS
             while (m) {
                 const uint32_t b0 = (uint32_t)__builtin_ctzll(m);
@@ -1479,6 +1611,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
                 test_staged_one(st, k0 + b, dx, dy, dz, hl);
             }
 #endif
+            }
         }
     }
     WaveStats ws = {};
@@ -1486,9 +1619,16 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     if (tile_live) {
         if (have_ray) {
             const uint32_t nl = whole ? 0u : n_local;
-            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, [=](uint32_t k) {
+            auto fetch = [=](uint32_t k) {
                 return whole ? k : __float_as_uint((k < nl ? local[k] : glob[k - nl]).e0.w);
-            });
+            };
+            if constexpr (kSigned)
+                finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch);
+            else
+                finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
+        } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
+            ws.rays += (uint32_t)__popcll(__ballot(active));
+            if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
         } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
             ws.rays += (uint32_t)__popcll(__ballot(active));
             if (active && !(ablation(p) & kAblateStores)) {
@@ -1501,6 +1641,55 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     }
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
+}
+
+// ---------------------------------------------------------------------------
+// k_hole_fill: the L-buffer fork's "error correction" pass
+// (main-pthreads-lbuffer.cxx:327-404) over a whole frame's L-buffer: a pixel
+// flagged -1 takes the mean of the first unflagged non-zero value within 4
+// steps in each of four directions (+-1 along the row-major index, running on
+// into the next / previous row, and +-1 row; unsigned 32-bit index arithmetic
+// as written, a walk ends past the buffer -- the fork also reads one element
+// past it, taken as the end); no value gives 0.0f / 0.  Others keep their
+// value.  Reads lbuffer only, so the pass does not cascade.  NaN results
+// carry x86's bits: the mean of values with a NaN (the render's 0x7FC00000)
+// keeps that NaN; 0.0f / 0 is the default NaN 0xFFC00000.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hole_fill(const float* __restrict__ lbuffer, float* __restrict__ image,
+                                                   uint8_t* __restrict__ image_u8, uint32_t width, uint32_t height)
+{
+    const uint64_t size = (uint64_t)width * height;
+    const uint64_t pixel = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pixel >= size) return;
+    const uint32_t row = (uint32_t)(pixel / width), col = (uint32_t)(pixel % width);
+    float photon = lbuffer[pixel];
+    if (photon == -1.0f) {
+        float sum = 0.0f;
+        uint32_t count = 0;
+        for (int dir = 0; dir < 4; ++dir) {
+            float value = 0.0f;
+            for (uint32_t i = 1; i <= 4u; ++i) {
+                const uint32_t idx = dir == 0 ? row * width + (col + i)
+                                   : dir == 1 ? (row - i) * width + col
+                                   : dir == 2 ? row * width + (col - i)
+                                              : (row + i) * width + col;
+                if ((uint64_t)idx >= size) break;
+                const float l = lbuffer[idx];
+                if (l != -1.0f) {
+                    value = l;
+                    break;
+                }
+            }
+            if (value != 0.0f) {                   // :353 (NaN != 0 is kept)
+                sum += value;
+                ++count;
+            }
+        }
+        photon = sum / (float)count;
+        if (photon != photon) photon = xrt_f32_from_bits(count ? kX86SignedNaN : kX86DefaultNaN);
+    }
+    if (image) image[pixel] = photon;
+    if (image_u8) image_u8[pixel] = lut_u8(photon);
 }
 
 // ---------------------------------------------------------------------------
@@ -1599,6 +1788,7 @@ __global__ void k_probe_math(int op, const float* __restrict__ in, float* __rest
     case 1: y = sqrtf(x); break;
     case 2: y = inv_det_of(x); break;
     case 4: y = rcp_newton_exact_for(x) ? rcp_newton(x) : inv_det_of(x); break;   // inv_det_fast per lane
+    case 5: y = signed_lbuffer(x, 0, 0.1037f); break;   // the fork's 80 * exp(-(mu * (d * 0.1)))
     default: y = (float)lut_u8(x); break;
     }
     outp[i] = y;

@@ -139,6 +139,8 @@ struct xrt_context {
     static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
+    uint32_t model = kModelAttenuation;   // xrt_set_model
+    float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
     xrt_camera cull_cam = {};          // camera of the cached cull parameters
     CullParams cull = {};
     bool cull_valid = false;
@@ -476,13 +478,22 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     // AUTO: the per-region footprint sweep of TILED costs T x regions box
     // tests; past kAutoSweep of them binning once per frame is cheaper.
     const uint64_t sweep = T * (uint64_t)rx * ry;
-    const int kernel = ctx->kernel != XRT_KERNEL_AUTO ? ctx->kernel
-                       : sweep > kAutoSweep          ? XRT_KERNEL_BINNED
-                                                     : XRT_KERNEL_TILED;
-    const bool culled = kernel != XRT_KERNEL_BRUTE;
+    const bool signed_model = ctx->model == kModelSigned;
+    int kernel = ctx->kernel != XRT_KERNEL_AUTO ? ctx->kernel
+                 : signed_model || sweep > kAutoSweep ? XRT_KERNEL_BINNED
+                                                      : XRT_KERNEL_TILED;
+    if (signed_model) {
+        if (kernel == XRT_KERNEL_TILED)
+            return fail(ctx, XRT_ERR_ARGUMENT, "the signed model renders with the BRUTE or BINNED kernel");
+        if (d_image || d_u8)
+            return fail(ctx, XRT_ERR_ARGUMENT,
+                        "the signed model writes the L-buffer only (the image is xrt_hole_fill's)");
+    }
     // k_prep packs a footprint's region rectangle in 16-bit fields: grids past
-    // 65535 regions a side render TILED (exact, slower).
+    // 65535 regions a side render TILED (exact, slower) -- BRUTE for the signed model.
     const bool binned = kernel == XRT_KERNEL_BINNED && rows > 0 && T > 0 && rx <= 0xFFFFu && ry <= 0xFFFFu;
+    if (signed_model && !binned) kernel = XRT_KERNEL_BRUTE;
+    const bool culled = kernel != XRT_KERNEL_BRUTE;
 
     // This frame's buffer set.  The render that last used it (kFrameSets
     // frames ago) must be complete before the set is prepared again.
@@ -514,6 +525,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     if ((rc = ensure(ctx, fs.offsets, fs.offsets_cap, (size_t)cam->height + cam->width))) return rc;
 
     RenderParams p = make_params(*cam, row_begin, row_end, T, ctx->hit_capacity);
+    p.model = ctx->model;
     if (!ctx->cull_valid || std::memcmp(&ctx->cull_cam, cam, sizeof *cam) != 0) {
         ctx->cull = make_cull_params(*cam);      // a scan over the rows / columns: once per camera
         ctx->cull_cam = *cam;
@@ -529,6 +541,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     out.off.u = fs.offsets + cam->height;
     const uint32_t miss_bits = ctx->miss_code ? ctx->miss_code : 0x7F800000u;   // +inf
     std::memcpy(&out.miss_l, &miss_bits, sizeof miss_bits);
+    out.mu = ctx->mu;
     const uint32_t n_regions = rows ? rx * ry : 0u;
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup
     dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
@@ -665,14 +678,16 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         t1 = fs.done;
     }
     if (rows > 0) {
+        const bool sgn = p.model == kModelSigned;
         if (kernel == XRT_KERNEL_BRUTE)
-            hipExtLaunchKernelGGL(k_render_brute, grid, dim3(256), 0, stream, t0, t1, 0, fs.recs, p, out);
+            hipExtLaunchKernelGGL(sgn ? k_render_brute<true> : k_render_brute<false>, grid, dim3(256), 0, stream,
+                                  t0, t1, 0, fs.recs, p, out);
         else if (kernel == XRT_KERNEL_TILED || !binned)
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
                                   fs.recs, fs.cull, p, out);
         else
-            hipExtLaunchKernelGGL(k_render_binned, grid, dim3(64 * kTileWaves), 0, stream, t0, t1, 0, fs.recs,
-                                  fs.cull, p, out, bins, (const BinState*)bin_ctl);
+            hipExtLaunchKernelGGL(sgn ? k_render_binned<true> : k_render_binned<false>, grid, dim3(64 * kTileWaves),
+                                  0, stream, t0, t1, 0, fs.recs, fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         if (t0) {
             ctx->last_t0 = t0;
@@ -830,6 +845,31 @@ int xrt_mesh_bbox(const float* tris, uint64_t n, float lower[3], float upper[3])
     return XRT_OK;
 }
 
+int xrt_scene_bbox(const float* tris, const uint64_t* mesh_triangles, uint32_t num_meshes, float lower[3],
+                   float upper[3])
+{
+    if ((num_meshes && !mesh_triangles) || !lower || !upper) return XRT_ERR_ARGUMENT;
+    const float inf = std::numeric_limits<float>::infinity();
+    for (int k = 0; k < 3; ++k) {
+        lower[k] = inf;
+        upper[k] = -inf;
+    }
+    // getBBox, src/main.cxx:545-562: the corners of each mesh's box in turn
+    uint64_t first = 0;
+    for (uint32_t m = 0; m < num_meshes; ++m) {
+        float lo[3], hi[3];
+        const uint64_t n = mesh_triangles[m];
+        if (n && !tris) return XRT_ERR_ARGUMENT;
+        xrt_mesh_bbox(n ? tris + 9 * first : nullptr, n, lo, hi);
+        for (int k = 0; k < 3; ++k) {
+            lower[k] = stdmin(lower[k], lo[k]);
+            upper[k] = stdmax(upper[k], hi[k]);
+        }
+        first += n;
+    }
+    return XRT_OK;
+}
+
 int xrt_camera_from_bbox(const float lower[3], const float upper[3], uint32_t width,
                          uint32_t height, xrt_camera* out)
 {
@@ -869,6 +909,81 @@ int xrt_set_kernel(xrt_context* ctx, int kernel)
         return fail(ctx, XRT_ERR_ARGUMENT, "unknown kernel");
     ctx->kernel = kernel;
     return XRT_OK;
+}
+
+int xrt_set_model(xrt_context* ctx, int model, float mu)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (model != XRT_MODEL_ATTENUATION && model != XRT_MODEL_SIGNED)
+        return fail(ctx, XRT_ERR_ARGUMENT, "unknown model");
+    ctx->model = (uint32_t)model;
+    ctx->mu = mu;
+    return XRT_OK;
+}
+
+int xrt_hole_fill_device(xrt_context* ctx, uint32_t width, uint32_t height, const float* d_lbuffer,
+                         float* d_image, uint8_t* d_u8, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    const uint64_t n = (uint64_t)width * height;
+    if (n > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "image larger than 2^32-1 pixels");
+    if (!n) return XRT_OK;
+    if (!d_lbuffer) return fail(ctx, XRT_ERR_ARGUMENT, "L-buffer is NULL");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_hole_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_lbuffer, d_image, d_u8, width, height);
+    XRT_HIP(ctx, hipGetLastError());
+    return XRT_OK;
+}
+
+int xrt_hole_fill(xrt_context* ctx, uint32_t width, uint32_t height, const float* lbuffer, float* image,
+                  uint8_t* image_u8)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    const size_t n = (size_t)width * height;
+    if (!n) return XRT_OK;
+    if (!lbuffer) return fail(ctx, XRT_ERR_ARGUMENT, "L-buffer is NULL");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    int rc;
+    size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
+    if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
+    ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
+    XRT_HIP(ctx, hipMemcpy(ctx->d_lbuffer, lbuffer, n * sizeof(float), hipMemcpyHostToDevice));
+    if ((rc = xrt_hole_fill_device(ctx, width, height, ctx->d_lbuffer, image ? ctx->d_image : nullptr,
+                                   image_u8 ? ctx->d_u8 : nullptr, nullptr)))
+        return rc;
+    if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
+    return XRT_OK;
+}
+
+int xrt_render_signed(xrt_context* ctx, const xrt_camera* camera, float* image, float* lbuffer,
+                      uint8_t* image_u8, xrt_stats* stats)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (ctx->model != kModelSigned) return fail(ctx, XRT_ERR_ARGUMENT, "xrt_render_signed needs XRT_MODEL_SIGNED");
+    int rc = check_camera(ctx, camera, 0, camera ? camera->height : 0);
+    if (rc) return rc;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)camera->width * camera->height;
+    size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
+    if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
+    ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
+    if ((rc = enqueue_render(ctx, camera, 0, camera->height, nullptr, ctx->d_lbuffer, nullptr, nullptr))) return rc;
+    if ((rc = xrt_hole_fill_device(ctx, camera->width, camera->height, ctx->d_lbuffer,
+                                   image ? ctx->d_image : nullptr, image_u8 ? ctx->d_u8 : nullptr, nullptr)))
+        return rc;
+    if (n) {
+        if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (lbuffer) XRT_HIP(ctx, hipMemcpy(lbuffer, ctx->d_lbuffer, n * sizeof(float), hipMemcpyDeviceToHost));
+        if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
+    }
+    xrt_stats local;
+    return xrt_read_stats(ctx, stats ? stats : &local);
 }
 
 int xrt_set_miss_code(xrt_context* ctx, uint32_t bits)
@@ -1084,7 +1199,7 @@ int xrt_probe_intersect(xrt_context* ctx, const float* rays, const float* tris, 
 int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* outp, uint64_t n)
 {
     if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
-    if (op < XRT_PROBE_EXPF || op > XRT_PROBE_RCP_FAST) return fail(ctx, XRT_ERR_ARGUMENT, "bad op");
+    if (op < XRT_PROBE_EXPF || op > XRT_PROBE_SIGNED_L) return fail(ctx, XRT_ERR_ARGUMENT, "bad op");
     if (n == 0) return XRT_OK;
     if (!in || !outp) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
     XRT_HIP(ctx, hipSetDevice(ctx->device));
@@ -1120,6 +1235,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
     if ((rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
     RenderParams p = make_params(*camera, 0, camera->height, T, ctx->hit_capacity);
+    p.model = ctx->model;
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads), 0, 0, ctx->d_tris,
@@ -1158,6 +1274,17 @@ void xrt_host_mt_check(const float* det, const float* a, const float* b, const f
 void xrt_host_expf_batch(const float* in, float* outp, uint64_t n)
 {
     for (uint64_t i = 0; i < n; ++i) outp[i] = xrt_expf(in[i]);
+}
+
+void xrt_host_exp_batch(const double* in, double* outp, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) outp[i] = xrt_exp(in[i]);
+}
+
+void xrt_host_signed_lbuffer_batch(const float* distance, const int32_t* sign_sum, float mu, float* outp,
+                                   uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) outp[i] = signed_lbuffer(distance[i], sign_sum ? sign_sum[i] : 0, mu);
 }
 
 }  // extern "C"

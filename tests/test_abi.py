@@ -38,7 +38,7 @@ def test_libxrt_host_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.load().xrt_abi_version() == 2
+    assert _abi.load().xrt_abi_version() == 3
 
 
 def test_create_without_gpu_fails_cleanly():
@@ -202,3 +202,79 @@ def test_host_ray_intersect_kat_matches_oracle():
     h2, t2 = oracle.intersect_batch(rays, tris)
     assert np.array_equal(hit, h2)
     assert np.array_equal(bits(t), bits(t2))
+
+
+# --------------------------------------------------------------------------- the L-buffer fork, scenes
+def test_host_exp_restatement_matches_libm():
+    """The device glibc exp source (host-compiled) vs libm exp: the exponents
+    the signed model forms from a stride over every f32 distance, random
+    doubles over the whole range, specials.  (tools/check_exp.cpp covers all
+    2^32 distances: 0 mismatches.)"""
+    lib = _abi.load()
+    d = np.arange(0, 1 << 32, 4099, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    with np.errstate(invalid="ignore"):
+        x1 = -(np.float64(np.float32(0.1037)) * (d.astype(np.float64) * 0.1))
+    rng = np.random.default_rng(1)
+    x2 = rng.uniform(-746, 710, 200000)
+    x3 = np.array([0.0, -0.0, 1e-300, -1e-300, 5e-324, 709.78, 709.79, -708.4, -745.13, -745.2, 1024, -1024,
+                   np.inf, -np.inf, np.nan, 512.0, -512.0], np.float64)
+    x = np.ascontiguousarray(np.concatenate([x1, x2, x3]))
+    got = np.empty_like(x)
+    lib.xrt_host_exp_batch(x.ctypes.data_as(_abi._dp), got.ctypes.data_as(_abi._dp), x.size)
+    want = oracle.exp(x)
+    same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), x[~same][:8]
+
+
+def test_host_signed_lbuffer_update():
+    """(float)(80 * exp(-(mu * (d * 0.1)))) as the fork evaluates it, -1 for a
+    non-zero sign sum, and x86's NaN for a NaN distance (0x7FC00000)."""
+    lib = _abi.load()
+    rng = np.random.default_rng(2)
+    d = np.concatenate([rng.uniform(-50, 400, 100000), [0.0, -0.0, np.inf, -np.inf, 1e30, -1e30]]).astype(np.float32)
+    d = np.concatenate([d, np.array([0xFFC00000], np.uint32).view(np.float32)])
+    ss = np.zeros(d.size, np.int32)
+    ss[::97] = rng.choice([-2, -1, 1, 3], ss[::97].size)
+    mu = np.float32(0.1037)
+    got = np.empty_like(d)
+    lib.xrt_host_signed_lbuffer_batch(d.ctypes.data_as(_abi._fp), ss.ctypes.data_as(_abi._i32p), mu,
+                                      got.ctypes.data_as(_abi._fp), d.size)
+    with np.errstate(over="ignore", invalid="ignore"):
+        want = (np.float64(80.0) * oracle.exp(-(np.float64(mu) * (d.astype(np.float64) * 0.1)))).astype(np.float32)
+    want[np.isnan(d)] = np.array([0x7FC00000], np.uint32).view(np.float32)[0]
+    want[ss != 0] = -1
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_obj_scene_loading(tmp_path):
+    p = tmp_path / "scene.obj"
+    p.write_text("# two objects\nmtllib x.mtl\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvt 0 0\nvn 0 0 1\n"
+                 "o first\nusemtl a\nf 1/1/1 2/1/1 3/1/1 4/1/1\n"
+                 "o empty\n"
+                 "g second\nv 5 5 5\nv 6 5 5\nv 5 6 7\nf -3 -2 -1\nf 1//1 3//1 5//1\nl 1 2\n")
+    meshes = xrt.load_meshes(str(p))
+    assert [len(m) for m in meshes] == [2, 2]
+    assert np.array_equal(meshes[0], np.array([[0, 0, 0, 1, 0, 0, 1, 1, 0], [0, 0, 0, 1, 1, 0, 0, 1, 0]], np.float32))
+    assert np.array_equal(meshes[1][0], np.array([5, 5, 5, 6, 5, 5, 5, 6, 7], np.float32))
+    assert np.array_equal(meshes[1][1], np.array([0, 0, 0, 1, 1, 0, 5, 5, 5], np.float32))
+    lo, hi = xrt.scene_bbox(meshes)
+    lo2, hi2 = oracle.scene_bbox(meshes)
+    assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2)
+    assert list(lo) == [0, 0, 0] and list(hi) == [6, 6, 7]
+    ply = xrt.load_meshes(DRAGON)
+    assert len(ply) == 1 and ply[0].shape == (22866, 9)
+    bad = tmp_path / "bad.obj"
+    bad.write_text("v 0 0 0\nf 1 2 3\n")
+    with pytest.raises(xrt.XrtError):
+        xrt.load_meshes(str(bad))
+
+
+def test_scene_camera_differs_from_mesh0_camera(dragon):
+    from scene_kit import second_mesh_for
+    meshes = [dragon, second_mesh_for(dragon)]
+    cam = xrt.camera_for_scene(meshes, 256, 256)
+    c13 = oracle.camera_for_scene(meshes, 256, 256)
+    got = np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) + [cam.pixel_spacing],
+                   np.float32)
+    assert np.array_equal(bits(got), bits(c13))
+    assert not np.array_equal(c13, oracle.camera_for_mesh(dragon, 256, 256))

@@ -15,6 +15,7 @@ from simpleraytracing_amd.scenes import tiled_mesh
 from oracle import oracle
 from conftest import DRAGON, GOLDEN, ROOT, bits
 from kat import kat_vectors
+from scene_kit import corner_soup, synthetic_soup
 
 pytestmark = pytest.mark.gpu
 KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED]
@@ -269,18 +270,6 @@ def test_empty_mesh(ctx, dragon, kernel):
     assert st.hits == 0
 
 
-def synthetic_soup(seed=11, n=3000):
-    rng = np.random.default_rng(seed)
-    c = rng.uniform(-50, 50, (n, 1, 3))
-    t = (c + rng.normal(0, 6, (n, 3, 3))).astype(np.float32)
-    soup = t.reshape(n, 9)
-    k = n // 10
-    soup[:k, 6:9] = (soup[:k, 0:3] + 2 * (soup[:k, 3:6] - soup[:k, 0:3])).astype(np.float32)  # collinear
-    soup[k:2 * k] = soup[2 * k:3 * k]                                                    # duplicates (ties)
-    soup[3 * k:3 * k + 20, 3:6] = soup[3 * k:3 * k + 20, 0:3]                             # zero-length edge
-    return np.ascontiguousarray(soup)
-
-
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_synthetic_soup_with_degenerates(ctx, kernel):
     soup = synthetic_soup()
@@ -302,21 +291,6 @@ def test_custom_camera_triangles_around_source(ctx, kernel):
     got = ctx.render_rows(cam)
     ref = oracle.render_rows(soup, cam13(cam), 64, 48)
     assert_same(got, ref, KNAME[kernel])
-
-
-def corner_soup():
-    """Triangles with 1e-20 edges one unit in front of the source, on the image's
-    centre column (odd W: the ray direction's y component is exactly 0 there):
-    det is a nonzero denormal, 1/det overflows to inf, a = u * det is exactly
-    0, so Ray.cxx:99-122 computes u = 0 * inf = NaN (passes both u tests),
-    v = +inf, u + v = NaN (passes) and t = +inf > 1e-7: the reference records
-    a hit at infinity for rays nowhere near the triangle.  The frame triangles
-    fix a bbox symmetric about y = 0 and z = 0 (the source's y and z)."""
-    tris = [[40, -10, -10, 40, 10, -10, 40, 10, 10], [60, -10, -10, 60, 10, 10, 60, -10, 10]]
-    for x0, sz in [(45, 1), (47, -1), (50, 1), (52, -1), (55, 1)]:
-        tris.append([x0, 0, 0, x0, 1e-20, 0, x0, 0, sz * 1e-20])
-        tris.append([x0, 0, 0, x0, 0, sz * 1e-20, x0, 1e-20, 0])
-    return np.array(tris, np.float32)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
