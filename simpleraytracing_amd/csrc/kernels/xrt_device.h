@@ -63,6 +63,12 @@
 #ifndef XRT_STAGE
 #define XRT_STAGE 128     // binned render: candidates staged in LDS per round (16 KB)
 #endif
+#ifndef XRT_FOLD_CMP
+#define XRT_FOLD_CMP 1       // Ray::intersect's four range tests folded into two (min / max)
+#endif
+#ifndef XRT_DESC_MED3
+#define XRT_DESC_MED3 1      // hit-list insertion from the top slot down (in place, no copies)
+#endif
 #ifndef XRT_PREP_THREADS
 #define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)
 #endif
@@ -380,7 +386,17 @@ __host__ __device__ __forceinline__ float mt_finish_inv(float det, float inv_det
     const float u = a * inv_det;                          // Ray.cxx:105
     const float v = b * inv_det;                          // Ray.cxx:115
     const float t = tnum * inv_det;                       // Ray.cxx:122
+#if XRT_FOLD_CMP
+    // Ray.cxx:106 and :116 with two compares: !(u < 0) && !(v < 0) is
+    // !(min(u, v) < 0), and !(u > 1) && !(u + v > 1) is !(max(u, u + v) > 1),
+    // because IEEE minNum / maxNum return the other operand when one is a
+    // (quiet) NaN -- and a NaN passes the reference's tests -- and a NaN only
+    // when both are.
+    // (bitwise &: evaluated without branches)
+    hit = (det != 0.0f) & !(fminf(u, v) < 0.0f) & !(fmaxf(u, u + v) > 1.0f) & accept_t(t);
+#else
     hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
+#endif
     return t;
 }
 
@@ -434,6 +450,13 @@ struct HitList {
         return;
 #endif
         const float x = hit ? t : __builtin_inff();
+#if XRT_DESC_MED3
+        // top slot first: each slot's new value is its last reader's, so the
+        // list is updated in place
+#pragma unroll
+        for (int k = kMaxHits - 1; k >= 1; --k) h[k] = __builtin_amdgcn_fmed3f(h[k - 1], h[k], x);
+        h[0] = __builtin_amdgcn_fmed3f(-__builtin_inff(), h[0], x);   // min(h[0], x), no canonicalisation
+#else
         float prev = h[0];
         h[0] = fminf(prev, x);
 #pragma unroll
@@ -442,6 +465,7 @@ struct HitList {
             h[k] = __builtin_amdgcn_fmed3f(prev, cur, x);
             prev = cur;
         }
+#endif
         n += hit ? 1u : 0u;
     }
 

@@ -7,7 +7,7 @@ OUT=../lib/ab
 mkdir -p $OUT
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -fno-fast-math \
       -I../../include -DXRT_KERNEL_NS=xrt_$name $flags -shared -o $OUT/libxrt_$name.so xrt_abi.hip \
       -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
 done
