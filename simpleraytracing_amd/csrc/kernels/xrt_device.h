@@ -69,6 +69,12 @@
 #ifndef XRT_DESC_MED3
 #define XRT_DESC_MED3 1      // hit-list insertion from the top slot down (in place, no copies)
 #endif
+#ifndef XRT_BRANCHLESS_EXPF
+#define XRT_BRANCHLESS_EXPF 1   // expf's special cases as selects (no divergent branches)
+#endif
+#ifndef XRT_BRANCHLESS_LUT
+#define XRT_BRANCHLESS_LUT 1    // the 8-bit LUT as selects
+#endif
 #ifndef XRT_PREP_THREADS
 #define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)
 #endif
@@ -221,7 +227,7 @@ __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_o
     float Y = ((p.cy + p.uy * v_off) + p.ry * u_off) - p.oy;
     float Z = ((p.cz + p.uz * v_off) + p.rz * u_off) - p.oz;
     // :660  Vec3::normalise (Vec3.inl:469-476)
-    float len = sqrtf((X * X + Y * Y) + Z * Z);
+    const float len = sqrtf((X * X + Y * Y) + Z * Z);
     X = X / len;
     Y = Y / len;
     Z = Z / len;
@@ -229,7 +235,7 @@ __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_o
     sy = Y;
     sz = Z;
     // Ray ctor normalises again; a zero length keeps the default (0,0,0).
-    float len2 = sqrtf((X * X + Y * Y) + Z * Z);
+    const float len2 = sqrtf((X * X + Y * Y) + Z * Z);
     if (len2 != 0.0f) {
         dx = X / len2;
         dy = Y / len2;
@@ -595,12 +601,14 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     uint32_t ix;
     __builtin_memcpy(&ix, &x, 4);
     uint32_t abstop = (ix >> 20) & 0x7ff;
+#if !XRT_BRANCHLESS_EXPF
     if (abstop >= 0x42b) {                  // |x| >= 88 or NaN
         if (ix == 0xff800000u) return 0.0f; // -inf
         if (abstop >= 0x7f8) return x + x;  // +inf or NaN
         if (x > 0x1.62e42ep6f) return __builtin_inff();   // overflow
         if (x < -0x1.9fe368p6f) return 0.0f;              // underflow
     }
+#endif
     double xd = (double)x;
     double kd = __builtin_fma(kInvLn2N, xd, kShift);
     uint64_t ki = xrt_double_as_u64(kd);
@@ -613,7 +621,20 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     double y = __builtin_fma(kC2, r, 1.0);
     y = __builtin_fma(z, r2, y);
     y = y * s;
+#if XRT_BRANCHLESS_EXPF
+    // the special cases as selects over the main path's value (which is
+    // computed, and discarded, for them too): no divergent branches
+    float out = (float)y;
+    if (abstop >= 0x42b) {
+        out = x < -0x1.9fe368p6f ? 0.0f : out;                   // underflow
+        out = x > 0x1.62e42ep6f ? __builtin_inff() : out;        // overflow
+        out = abstop >= 0x7f8 ? x + x : out;                     // +inf or NaN
+        out = ix == 0xff800000u ? 0.0f : out;                    // -inf
+    }
+    return out;
+#else
     return (float)y;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -799,6 +820,14 @@ __host__ __device__ __forceinline__ float signed_lbuffer(float distance, int sig
 __host__ __device__ __forceinline__ uint8_t lut_u8(float v)
 {
     const float vmin = 0.0f, vmax = 80.0f;
+#if XRT_BRANCHLESS_LUT
+    // 255.0 * v / 80.0 == v * 3.1875 exactly (below); for x = v * 3.1875 >= 0
+    // (at most 30 significant bits, < 256) x + 0.5 is exact, so round-half-
+    // away-from-zero is floor(x + 0.5).  Selects instead of branches; the
+    // product is computed, and discarded, for out-of-range v and NaN.
+    const uint32_t r = (uint32_t)__builtin_floor((double)v * 3.1875 + 0.5);
+    return v > vmax ? (uint8_t)255u : v >= vmin ? (uint8_t)r : (uint8_t)0u;
+#else
     if (v < vmin) return 0;
     if (v > vmax) return 255;
     if (v != v) return 0;
@@ -807,6 +836,7 @@ __host__ __device__ __forceinline__ uint8_t lut_u8(float v)
     // rounded division returns it unchanged (checked for every f32 in
     // [0, 80]: tools/check_fp_identities.c).
     return (uint8_t)__builtin_round((double)(v - vmin) * 3.1875);
+#endif
 }
 
 }  // namespace XRT_KERNEL_NS

@@ -267,13 +267,35 @@ __device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x)
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// Sum of a and maximum of b over the wave, the two DPP chains interleaved (each
+// step's DPP read of the other chain's last write fills the hazard gap).
+__device__ __forceinline__ void wave_reduce_sum_max(uint32_t a, uint32_t b, uint32_t& sum, uint32_t& mx)
+{
+#define XRT_DPP_STEP(ctrl, rmask, bc)                                                                     \
+    a += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, ctrl, rmask, 0xf, bc);                         \
+    {                                                                                                     \
+        const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, ctrl, rmask, 0xf, bc);        \
+        b = b > o ? b : o;                                                                                \
+    }
+    XRT_DPP_STEP(0x111, 0xf, true)
+    XRT_DPP_STEP(0x112, 0xf, true)
+    XRT_DPP_STEP(0x114, 0xf, true)
+    XRT_DPP_STEP(0x118, 0xf, true)
+    XRT_DPP_STEP(0x142, 0xa, false)
+    XRT_DPP_STEP(0x143, 0xc, false)
+#undef XRT_DPP_STEP
+    sum = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+    mx = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
+}
+
 // One wave's statistics as one BlockStats record (no LDS, no barrier): the
 // lane sums are reduced across the wave and lane 0 stores the record.
 __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t candidates,
-                                                 BlockStats* out, uint32_t index, uint64_t t_start = 0)
+                                                 BlockStats* out, uint32_t index, uint64_t t_start = 0,
+                                                 uint32_t stamp_extra = 0)
 {
-    const uint32_t hits = wave_reduce_u32<false>(ws.lane_hits);
-    const uint32_t mx = wave_reduce_u32<true>(ws.lane_max);
+    uint32_t hits, mx;
+    wave_reduce_sum_max(ws.lane_hits, ws.lane_max, hits, mx);
     if ((threadIdx.x & 63u) == 0u) {
         BlockStats b;
         b.rays = ws.rays;
@@ -285,6 +307,11 @@ __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t c
         b.candidates = candidates;
         b.max_hits = mx;
         stamp_record(b, t_start);
+#if XRT_STAMPS
+        b.hits = stamp_extra;       // XRT_STAMPS: ticks from the wave's start to its first staged round
+#else
+        (void)stamp_extra;
+#endif
         out[index] = b;
     }
 }
@@ -1564,6 +1591,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
+    uint64_t t_staged = t_start;                   // XRT_STAMPS diagnostics
     // every wave of the workgroup takes part in every round's staging and barriers
     for (uint32_t base = 0; base < n_cand; base += kBinStage) {
         const uint32_t cnt = min(kBinStage, n_cand - base);
@@ -1572,6 +1600,9 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         else stage_entries(st, local, n_local, glob, base, cnt);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
         __syncthreads();                           // and every wave's
+#if XRT_STAMPS
+        if (!base) t_staged = __builtin_amdgcn_s_memrealtime();
+#endif
         if (!tile_live) continue;
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64u) {
             const uint32_t k = k0 + lane;
@@ -1640,7 +1671,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         }
     }
     // candidates are counted once per region (by the wave holding tile 0)
-    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start);
+    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start, (uint32_t)(t_staged - t_start));
 }
 
 // ---------------------------------------------------------------------------
