@@ -69,6 +69,9 @@
 #ifndef XRT_DESC_MED3
 #define XRT_DESC_MED3 1      // hit-list insertion from the top slot down (in place, no copies)
 #endif
+#ifndef XRT_PREFETCH_OFFSETS
+#define XRT_PREFETCH_OFFSETS 1  // binned render: the tile's pixel offsets loaded at the wave's start
+#endif
 #ifndef XRT_BRANCHLESS_EXPF
 #define XRT_BRANCHLESS_EXPF 1   // expf's special cases as selects (no divergent branches)
 #endif

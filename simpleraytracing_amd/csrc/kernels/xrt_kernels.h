@@ -1588,6 +1588,12 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
     bool have_ray = false;                         // wave-uniform
+#if XRT_PREFETCH_OFFSETS
+    // the tile's pixel offsets, loaded beside the region's counts: a tile with
+    // survivors generates its rays without another memory round trip
+    const float pre_v = out.off.v[min(row, p.height - 1u)];
+    const float pre_u = out.off.u[min(col, p.width - 1u)];
+#endif
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
@@ -1614,8 +1620,12 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
             if (!m) continue;
             tests += (uint32_t)__popcll(m);
             if (!have_ray) {
+#if XRT_PREFETCH_OFFSETS
+                make_ray_from(*out.frame, pre_v, pre_u, dx, dy, dz, sx, sy, sz);
+#else
                 if constexpr (kSigned) make_tile_ray(p, out, row, col, dx, dy, dz, sx, sy, sz);
                 else if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
+#endif
                 have_ray = true;
             }
             if (ablation(p) & kAblateExact) continue;
