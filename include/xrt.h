@@ -290,6 +290,13 @@ int xrt_render_rows_multi(xrt_multi* m, const xrt_camera* camera, float* image, 
 int xrt_render_rows_multi_device(xrt_multi* m, const xrt_camera* camera, float* d_image,
                                  float* d_lbuffer, uint8_t* d_image_u8, void* stream);
 
+/*
+ * The per-ray model of every device (xrt_set_model).  With XRT_MODEL_SIGNED the
+ * gathered planes are the fork's: lbuffer = its L_buffer, image / image_u8 =
+ * the hole-filled image (device 0 fills the assembled frame).
+ */
+int xrt_multi_set_model(xrt_multi* m, int model, float mu);
+
 /* Waits for the last frame's gathers; the devices' statistics, summed. */
 int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
 

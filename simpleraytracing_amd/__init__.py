@@ -327,6 +327,9 @@ class MultiContext:
     def set_kernel(self, kernel: int):
         self._check(self._lib.xrt_multi_set_kernel(self._m, int(kernel)), "xrt_multi_set_kernel")
 
+    def set_model(self, model: int, mu: float = 0.1037):
+        self._check(self._lib.xrt_multi_set_model(self._m, int(model), float(np.float32(mu))), "xrt_multi_set_model")
+
     def render(self, cam: Camera, image=True, lbuffer=True, u8=True):
         """The whole frame, gathered to the host: (image, lbuffer, u8, stats)."""
         n = cam.width * cam.height

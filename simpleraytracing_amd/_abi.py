@@ -134,6 +134,7 @@ XRT_SYMBOLS = {
     "xrt_multi_num_devices": (ctypes.c_int, [_MultiP]),
     "xrt_multi_upload_mesh": (ctypes.c_int, [_MultiP, _fp, _u64]),
     "xrt_multi_set_kernel": (ctypes.c_int, [_MultiP, ctypes.c_int]),
+    "xrt_multi_set_model": (ctypes.c_int, [_MultiP, ctypes.c_int, _f]),
     "xrt_render_rows_multi": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _fp, _fp, _u8p,
                                              ctypes.POINTER(Stats)]),
     "xrt_render_rows_multi_device": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _vp, _vp, _vp, _vp]),

@@ -236,11 +236,18 @@ unsigned long long renderLoopLBuffer(Image& image, const std::vector<TriangleMes
     return stats.odd_rays;
 }
 
-// Row strips over num_gpus devices gathered into device 0 with RCCL
-// (xrt_render_rows_multi).  $XRT_MULTI_DEVICES ("0,0" ...) overrides the
-// device list -- a device listed twice rehearses the strip path on one GPU.
-unsigned long long renderLoopMultiGPU(Image& image, const std::vector<TriangleMesh>& meshes,
-                                      RayTracerInfo& info, int num_gpus)
+namespace {
+
+// One multi-device context per device list for the process lifetime: the
+// devices 0 .. num_gpus-1, or $XRT_MULTI_DEVICES ("0,0" ...; a device listed
+// twice rehearses the strip path on one GPU).  Guarded by multi_lock().
+std::mutex& multi_lock()
+{
+    static std::mutex lock;
+    return lock;
+}
+
+xrt_multi* multi_context(int num_gpus)
 {
     std::vector<int> devices;
     if (const char* env = std::getenv("XRT_MULTI_DEVICES")) {
@@ -258,25 +265,56 @@ unsigned long long renderLoopMultiGPU(Image& image, const std::vector<TriangleMe
                                      std::to_string(available) + " available");
         for (int g = 0; g < num_gpus; ++g) devices.push_back(g);
     }
-    xrt_camera cam = camera_for(image, meshes, info);
-    std::vector<float> soup = mesh0_soup(meshes);
-    // one multi-device context per device list for the process lifetime
-    static std::mutex lock;
     static std::map<std::vector<int>, xrt_multi*> contexts;
-    std::lock_guard<std::mutex> g(lock);
     xrt_multi*& m = contexts[devices];
     if (!m && xrt_multi_create(devices.data(), (int)devices.size(), &m) != XRT_OK) {
         m = nullptr;
         throw std::runtime_error(std::string("xrt_multi_create: ") + xrt_multi_last_error(nullptr));
     }
-    auto mcheck = [&](int rc, const char* what) {
-        if (rc != XRT_OK) throw std::runtime_error(std::string(what) + ": " + xrt_multi_last_error(m));
-    };
-    mcheck(xrt_multi_set_kernel(m, kernel_choice()), "xrt_multi_set_kernel");
-    mcheck(xrt_multi_upload_mesh(m, soup.data(), soup.size() / 9), "xrt_multi_upload_mesh");
+    return m;
+}
+
+void mcheck(xrt_multi* m, int rc, const char* what)
+{
+    if (rc != XRT_OK) throw std::runtime_error(std::string(what) + ": " + xrt_multi_last_error(m));
+}
+
+}  // namespace
+
+// Row strips over num_gpus devices gathered into device 0 with RCCL
+// (xrt_render_rows_multi).
+unsigned long long renderLoopMultiGPU(Image& image, const std::vector<TriangleMesh>& meshes,
+                                      RayTracerInfo& info, int num_gpus)
+{
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    std::lock_guard<std::mutex> g(multi_lock());
+    xrt_multi* m = multi_context(num_gpus);
+    mcheck(m, xrt_multi_set_model(m, XRT_MODEL_ATTENUATION, 0.0f), "xrt_multi_set_model");
+    mcheck(m, xrt_multi_set_kernel(m, kernel_choice()), "xrt_multi_set_kernel");
+    mcheck(m, xrt_multi_upload_mesh(m, soup.data(), soup.size() / 9), "xrt_multi_upload_mesh");
     xrt_stats stats;
-    mcheck(xrt_render_rows_multi(m, &cam, image.getData(), nullptr, nullptr, &stats), "xrt_render_rows_multi");
+    mcheck(m, xrt_render_rows_multi(m, &cam, image.getData(), nullptr, nullptr, &stats), "xrt_render_rows_multi");
     report_odd(stats.odd_rays);
+    return stats.odd_rays;
+}
+
+unsigned long long renderLoopLBufferMultiGPU(Image& image, const std::vector<TriangleMesh>& meshes,
+                                             RayTracerInfo& info, int num_gpus, std::vector<float>* lbuffer)
+{
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    std::lock_guard<std::mutex> g(multi_lock());
+    xrt_multi* m = multi_context(num_gpus);
+    const int k = kernel_choice();
+    mcheck(m, xrt_multi_set_kernel(m, k == XRT_KERNEL_TILED ? XRT_KERNEL_BINNED : k), "xrt_multi_set_kernel");
+    mcheck(m, xrt_multi_upload_mesh(m, soup.data(), soup.size() / 9), "xrt_multi_upload_mesh");
+    mcheck(m, xrt_multi_set_model(m, XRT_MODEL_SIGNED, 0.1037f), "xrt_multi_set_model");   // :800
+    if (lbuffer) lbuffer->resize((size_t)image.getWidth() * image.getHeight());
+    xrt_stats stats;
+    const int rc = xrt_render_rows_multi(m, &cam, image.getData(), lbuffer ? lbuffer->data() : nullptr, nullptr, &stats);
+    xrt_multi_set_model(m, XRT_MODEL_ATTENUATION, 0.0f);
+    mcheck(m, rc, "xrt_render_rows_multi");
     return stats.odd_rays;
 }
 

@@ -67,6 +67,11 @@ void renderLoopRows(Image& output_image, const std::vector<TriangleMesh>& meshes
 unsigned long long renderLoopLBuffer(Image& output_image, const std::vector<TriangleMesh>& meshes,
                                      RayTracerInfo& info, std::vector<float>* lbuffer = nullptr);
 
+// The same as row strips over `num_gpus` devices (the L-buffer strips gathered
+// to device 0, which fills the holes of the assembled frame).
+unsigned long long renderLoopLBufferMultiGPU(Image& output_image, const std::vector<TriangleMesh>& meshes,
+                                             RayTracerInfo& info, int num_gpus, std::vector<float>* lbuffer = nullptr);
+
 // Row strips over `num_gpus` devices (rows_per = H / n, remainder to the first
 // strips), one host thread per device; returns the number of odd rays.
 unsigned long long renderLoopMultiGPU(Image& output_image, const std::vector<TriangleMesh>& meshes,

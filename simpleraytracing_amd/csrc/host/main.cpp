@@ -153,7 +153,9 @@ int main(int argc, char** argv)
 
         auto r0 = std::chrono::high_resolution_clock::now();
         std::vector<float> lb;
-        if (opt.signed_model) {
+        if (opt.signed_model && opt.gpus > 1) {
+            renderLoopLBufferMultiGPU(image, meshes, info, opt.gpus, opt.lbuffer.empty() ? nullptr : &lb);
+        } else if (opt.signed_model) {
             renderLoopLBuffer(image, meshes, info, opt.lbuffer.empty() ? nullptr : &lb);
         } else if (opt.gpus > 1) {
             renderLoopMultiGPU(image, meshes, info, opt.gpus);

@@ -204,3 +204,42 @@ def test_cli_signed_text(tmp_path, dragon):
     rlb, _, _ = oracle.render_signed_rows(meshes, oracle.camera_for_scene(meshes, 64, 64), 64, 64)
     assert np.array_equal(bits(np.fromfile(tmp_path / "l.f32", np.float32)), bits(rlb))
     assert (tmp_path / "out" / "l.txt").read_bytes() == oracle.text_bytes(oracle.hole_fill(rlb, 64, 64), 64, 64)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_signed_strips(signed, dragon, devices):
+    """The signed model over row strips: L-buffer strips gathered to device 0,
+    which fills the holes of the assembled frame -- equal to one device's
+    render and to the oracle (flagged pixels near strip boundaries included)."""
+    meshes = [striped_sheets(seed=6)]
+    W, H = 96, 83
+    cam = xrt.camera_for_scene(meshes, W, H)
+    signed.set_kernel(xrt.XRT_KERNEL_BINNED)
+    signed.upload_mesh(meshes[0])
+    ref = signed.render_signed(cam)
+    with xrt.MultiContext(devices) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(meshes[0])
+        m.set_model(xrt.XRT_MODEL_SIGNED, 0.1037)
+        for _ in range(3):                              # the strip buffers rotate
+            img, lb, u8, st = m.render(cam)
+            assert np.array_equal(bits(lb), bits(ref[1])) and np.array_equal(bits(img), bits(ref[0]))
+            assert np.array_equal(u8, ref[2]) and st.odd_rays == ref[3].odd_rays
+        m.set_model(xrt.XRT_MODEL_ATTENUATION, 0.0)      # back to the attenuation model: unchanged
+        att = m.render(cam)
+    rlb, _, _ = oracle.render_signed_rows(meshes, cam13(cam), W, H)
+    assert np.array_equal(bits(lb), bits(rlb))
+    signed.set_model(xrt.XRT_MODEL_ATTENUATION, 0.0)
+    one = signed.render_rows(cam)
+    assert np.array_equal(bits(att[0]), bits(one[0])) and np.array_equal(bits(att[1]), bits(one[1]))
+
+
+def test_cli_signed_two_gpus_rehearsal(tmp_path, dragon):
+    """xrt_main --signed -g 2 (XRT_MULTI_DEVICES=0,0): the same text as one GPU."""
+    (tmp_path / "out").mkdir()
+    env = dict(os.environ, XRT_MULTI_DEVICES="0,0")
+    for name, extra in (("one.txt", []), ("two.txt", ["-g", "2"])):
+        r = subprocess.run([EXE, "--signed", "-s", "80", "72", "-i", DRAGON, "-f", name] + extra,
+                           capture_output=True, text=True, cwd=tmp_path, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+    assert (tmp_path / "out" / "one.txt").read_bytes() == (tmp_path / "out" / "two.txt").read_bytes()
