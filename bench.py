@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--size", type=int, nargs=2, default=None, metavar=("W", "H"),
                     help="default 2048 2048; 4096 4096 for strips over N > 1 GPUs (BASELINE configs[3])")
     ap.add_argument("--kernel", choices=["auto", "binned", "tiled", "brute"], default="auto")
+    ap.add_argument("--model", choices=["attenuation", "signed"], default="attenuation",
+                    help="signed: the L-buffer fork (main-pthreads-lbuffer.cxx) -- signed L-buffer render "
+                         "+ hole fill per step (frames mode; not the headline metric)")
     ap.add_argument("--mode", choices=["frames", "strips"], default=None,
                     help="default: frames on one GPU, strips over N > 1")
     ap.add_argument("--mesh", default=os.path.join(ROOT, "data", "dragon.ply"))
@@ -187,7 +190,9 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # N > 1: BASELINE configs[3] -- one frame split into row strips, gathered to rank 0
-    mode = args.mode or ("strips" if world > 1 else "frames")
+    mode = args.mode or ("strips" if world > 1 and args.model == "attenuation" else "frames")
+    if args.model == "signed" and mode == "strips":
+        raise SystemExit("--model signed measures frames (the strip gather is the attenuation model's)")
     W, H = args.size or ((4096, 4096) if mode == "strips" and world > 1 else (2048, 2048))
     device_index = 0 if args.same_device else local_rank
     torch.cuda.set_device(device_index)
@@ -213,6 +218,9 @@ def main():
     ctx.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
                     "tiled": xrt.XRT_KERNEL_TILED, "binned": xrt.XRT_KERNEL_BINNED}[args.kernel])
     ctx.upload_mesh(tris)
+    signed = args.model == "signed"
+    if signed:
+        ctx.set_model(xrt.XRT_MODEL_SIGNED, 0.1037)   # main-pthreads-lbuffer.cxx:800
     stream = torch.cuda.current_stream(dev)
 
     # Rank 0 (and every rank in frames mode) holds a whole frame's planes.  In
@@ -255,7 +263,10 @@ def main():
     def step():
         k = frame_no[0]
         frame_no[0] += 1
-        if root:
+        if signed:                            # the fork: signed L-buffer, then the hole fill
+            ctx.render_rows_device(cam, 0, H, 0, lb.data_ptr(), 0, stream.cuda_stream)
+            ctx.hole_fill_device(W, H, lb.data_ptr(), img.data_ptr(), u8.data_ptr(), stream.cuda_stream)
+        elif root:
             o = r0 * W
             ctx.render_rows_device(cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
                                    u8.data_ptr() + o, stream.cuda_stream)
@@ -315,7 +326,8 @@ def main():
         avg_kernel_s = kernel_ms / max(launches, 1) / 1e3
         result_kernel = {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel]
         workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
-                                                         if args.tile_mesh > 1 else "") + f" {W}x{H}"
+                                                         if args.tile_mesh > 1 else "") + f" {W}x{H}" + \
+            (" signed L-buffer + hole fill" if signed else "")
         roofline = make_roofline(args, result_kernel, workload, stats, T, rays_per_launch, avg_kernel_s,
                                  launches)
         result = {
@@ -357,7 +369,7 @@ def main():
             "dist_backend": args.dist_backend if world > 1 else None,
         }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not signed:
         full = ctx.render_rows(cam)     # the same frame, fetched to the host for the parity check
         result["cpu_baseline"] = cpu_baseline(tris, W, H, args.cpu_seconds, full[:3])
 
