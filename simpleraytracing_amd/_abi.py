@@ -176,6 +176,16 @@ def load():
             raise RuntimeError(
                 f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "or `make -C simpleraytracing_amd/csrc` (there is no CPU fallback)")
+        # torch's ROCm libraries first: they are NEEDED by unversioned names
+        # (libamdhip64.so, librccl.so), so a torch imported after libxrt.so
+        # (which needs libamdhip64.so.7, librccl.so.1) would load a second HIP
+        # and HSA runtime into the process -- two runtimes that corrupt the heap
+        # at exit.  Imported first, torch's copies carry the versioned sonames
+        # and libxrt.so binds to them.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), XRT_SYMBOLS)
     return _lib
 
