@@ -38,6 +38,21 @@ void xrt_host_free(void* p);
  */
 void xrt_host_intersect_batch(const float* rays, const float* triangles, uint64_t n, uint8_t* hit, float* t);
 
+/*
+ * Image writers of the drop-in Image class on a width x height row-major float
+ * image (Image::setPixel's layout, include/Image.inl:147):
+ *   XRT_IMAGE_TEXT  saveTextFile (src/Image.cxx:210-235)
+ *   XRT_IMAGE_TGA   saveTGAFile (src/Image.cxx:148-206): 18-byte header, rows
+ *                   bottom-up, the LUT over [vmin, vmax] in all three channels
+ *                   (applyLUT's intended mapping, include/Image.inl:189-216,
+ *                   without its [i] / [i*3] indexing bug)
+ *   XRT_IMAGE_PGM   the same LUT as binary 8-bit PGM
+ *   XRT_IMAGE_JPEG  saveJPEGFile: XRT_ERR_IO (no libjpeg headers in this build)
+ */
+enum { XRT_IMAGE_TEXT = 0, XRT_IMAGE_TGA = 1, XRT_IMAGE_PGM = 2, XRT_IMAGE_JPEG = 3 };
+int xrt_host_save_image(const float* pixels, uint32_t width, uint32_t height, const char* path, int format,
+                        float vmin, float vmax);
+
 #ifdef __cplusplus
 }
 

@@ -36,6 +36,11 @@ XRT_PROBE_SIGNED_L = 5
 XRT_MODEL_ATTENUATION = 0
 XRT_MODEL_SIGNED = 1
 
+XRT_IMAGE_TEXT = 0
+XRT_IMAGE_TGA = 1
+XRT_IMAGE_PGM = 2
+XRT_IMAGE_JPEG = 3
+
 _f = ctypes.c_float
 _fp = ctypes.POINTER(ctypes.c_float)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -148,6 +153,7 @@ XRT_HOST_SYMBOLS = {
                                             ctypes.POINTER(_u32)]),
     "xrt_host_free": (None, [_vp]),
     "xrt_host_intersect_batch": (None, [_fp, _fp, _u64, _u8p, _fp]),
+    "xrt_host_save_image": (ctypes.c_int, [_fp, _u32, _u32, ctypes.c_char_p, ctypes.c_int, _f, _f]),
 }
 
 _lib = None

@@ -1,6 +1,8 @@
 // Image.cpp -- see Image.h.
 #include "Image.h"
 
+#include "xrt_host.h"
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -169,4 +171,25 @@ void Image::savePGMFile(const std::string& file_name, float vmin, float vmax) co
     for (size_t i = 0; i < g.size(); ++i) g[i] = lutValue(m_data[i], vmin, vmax);
     std::fwrite(g.data(), 1, g.size(), f);
     std::fclose(f);
+}
+
+// C entry point of the image writers (include/xrt_host.h).
+extern "C" int xrt_host_save_image(const float* pixels, uint32_t width, uint32_t height, const char* path,
+                                   int format, float vmin, float vmax)
+{
+    if (!path || (!pixels && width && height)) return XRT_ERR_ARGUMENT;
+    try {
+        Image image(width, height);
+        if (width && height) std::memcpy(image.getData(), pixels, sizeof(float) * (size_t)width * height);
+        switch (format) {
+        case XRT_IMAGE_TEXT: image.saveTextFile(path); break;
+        case XRT_IMAGE_TGA: image.saveTGAFile(path, vmin, vmax); break;
+        case XRT_IMAGE_PGM: image.savePGMFile(path, vmin, vmax); break;
+        case XRT_IMAGE_JPEG: image.saveJPEGFile(path, vmin, vmax); break;
+        default: return XRT_ERR_ARGUMENT;
+        }
+    } catch (const std::exception&) {
+        return XRT_ERR_IO;
+    }
+    return XRT_OK;
 }

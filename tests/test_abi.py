@@ -278,3 +278,40 @@ def test_scene_camera_differs_from_mesh0_camera(dragon):
                    np.float32)
     assert np.array_equal(bits(got), bits(c13))
     assert not np.array_equal(c13, oracle.camera_for_mesh(dragon, 256, 256))
+
+
+def test_image_writers(tmp_path):
+    """Image::saveTextFile / saveTGAFile / savePGMFile through xrt_host_save_image:
+    the text as the oracle writes it (src/Image.cxx:210-235), the TGA's 18-byte
+    header and bottom-up rows (src/Image.cxx:148-206) and the PGM carrying the
+    LUT over [0, 80] (applyLUT's intended mapping, include/Image.inl:189-216);
+    JPEG needs libjpeg and fails with XRT_ERR_IO."""
+    H, W = 5, 7
+    rng = np.random.default_rng(3)
+    img = rng.uniform(-10, 90, (H, W)).astype(np.float32)
+    img[0, 0], img[1, 2], img[4, 6] = np.nan, 0.0, 80.0
+    flat = np.ascontiguousarray(img.reshape(-1))
+    host = _abi.load_host()
+    lut = np.array([oracle.lut_u8(v) for v in flat], np.uint8).reshape(H, W)
+
+    def save(name, fmt):
+        path = tmp_path / name
+        rc = host.xrt_host_save_image(flat.ctypes.data_as(_abi._fp), W, H, str(path).encode(), fmt, 0.0, 80.0)
+        return rc, path
+
+    rc, path = save("i.txt", _abi.XRT_IMAGE_TEXT)
+    assert rc == _abi.XRT_OK and path.read_bytes() == oracle.text_bytes(flat, W, H)
+    rc, path = save("i.tga", _abi.XRT_IMAGE_TGA)
+    data = path.read_bytes()
+    assert rc == _abi.XRT_OK and len(data) == 18 + 3 * W * H
+    assert data[:18] == bytes([0, 0, 2] + [0] * 9 + [W & 255, W >> 8, H & 255, H >> 8, 24, 0])
+    px = np.frombuffer(data[18:], np.uint8).reshape(H, W, 3)
+    assert np.array_equal(px, np.repeat(lut[::-1, :, None], 3, axis=2))
+    rc, path = save("i.pgm", _abi.XRT_IMAGE_PGM)
+    data = path.read_bytes()
+    head = f"P5\n{W} {H}\n255\n".encode()
+    assert rc == _abi.XRT_OK and data[:len(head)] == head
+    assert np.array_equal(np.frombuffer(data[len(head):], np.uint8).reshape(H, W), lut)
+    assert save("i.jpg", _abi.XRT_IMAGE_JPEG)[0] == _abi.XRT_ERR_IO
+    assert save("no/such/dir.tga", _abi.XRT_IMAGE_TGA)[0] == _abi.XRT_ERR_IO
+    assert save("x", 9)[0] == _abi.XRT_ERR_ARGUMENT
