@@ -464,7 +464,9 @@ struct HitList {
         // list is updated in place
 #pragma unroll
         for (int k = kMaxHits - 1; k >= 1; --k) h[k] = __builtin_amdgcn_fmed3f(h[k - 1], h[k], x);
-        h[0] = __builtin_amdgcn_fmed3f(-__builtin_inff(), h[0], x);   // min(h[0], x), no canonicalisation
+        // min(h[0], x): the values are never NaN, so one plain v_min_f32 (the
+        // compiler's fminnum adds a canonicalising v_max of the loop-carried h[0])
+        asm("v_min_f32 %0, %1, %2" : "=v"(h[0]) : "v"(h[0]), "v"(x));
 #else
         float prev = h[0];
         h[0] = fminf(prev, x);

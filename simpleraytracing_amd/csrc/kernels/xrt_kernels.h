@@ -254,6 +254,13 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
 // row_shr:n (0x110 + n) reads lane i-n of the same 16-lane row (0 past the
 // row start: bound_ctrl); row_bcast:15 (0x142) adds lane 15 of rows 0 / 2 to
 // rows 1 / 3; row_bcast:31 (0x143) adds lane 31 to rows 2 and 3.
+// m with bit b (its lowest set bit) cleared: one s_bitset0_b64 instead of the
+// three SALU ops of m & (m - 1).
+__device__ __forceinline__ void clear_lane_bit(unsigned long long& m, uint32_t b)
+{
+    asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(b));
+}
+
 template <bool kMax>
 __device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x)
 {
@@ -1632,7 +1639,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
             if constexpr (kSigned) {
                 while (m) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                    m &= m - 1ull;
+                    clear_lane_bit(m, b);
                     test_staged_one(st, k0 + b, dx, dy, dz, sx, sy, sz, hl);
                 }
             } else {
@@ -1648,7 +1655,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 #else
             while (m) {
                 const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1ull;
+                clear_lane_bit(m, b);
                 test_staged_one(st, k0 + b, dx, dy, dz, hl);
             }
 #endif
