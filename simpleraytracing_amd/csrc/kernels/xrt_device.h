@@ -54,9 +54,6 @@
 #define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
                           // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
-#ifndef XRT_STAGED_PAIRS
-#define XRT_STAGED_PAIRS 0   // binned render: survivors tested two at a time (A/B: spills at 8 waves/SIMD, slower)
-#endif
 #ifndef XRT_RENDER_WAVES
 #define XRT_RENDER_WAVES 8   // binned render: minimum waves per SIMD (8 = 64 VGPRs)
 #endif

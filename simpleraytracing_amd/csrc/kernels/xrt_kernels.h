@@ -1505,34 +1505,6 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     if (__ballot(h)) hl.push_if(h, t, __float_as_uint(st.q[0][k].w), hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
 }
 
-// Two survivors at once: independent dependency chains for the scheduler to
-// interleave (the hit set, and so the sorted list, does not depend on the order).
-__device__ __forceinline__ void test_staged_pair(const RegionStage& st, uint32_t k0, uint32_t k1, bool two,
-                                                 float dx, float dy, float dz, HitList& hl)
-{
-    const float4 a0 = st.q[4][k0], a1 = st.q[5][k0], a2 = st.q[6][k0];
-    const float4 b0 = st.q[4][k1], b1 = st.q[5][k1], b2 = st.q[6][k1];
-    const float ta = st.q[7][k0].x, tb = st.q[7][k1].x;
-    float det0, u0, v0, det1, u1, v1;
-    mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
-                  det0, u0, v0);
-    mt_numerators(dx, dy, dz, b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w,
-                  det1, u1, v1);
-    float i0, i1;
-    if (__builtin_expect(__ballot(!(rcp_newton_exact_for(det0) && rcp_newton_exact_for(det1))) == 0ull, 1)) {
-        i0 = rcp_newton(det0);
-        i1 = rcp_newton(det1);
-    } else {
-        i0 = inv_det_of(det0);
-        i1 = inv_det_of(det1);
-    }
-    bool h0, h1;
-    const float t0 = mt_finish_inv(det0, i0, u0, v0, ta, h0);
-    const float t1 = mt_finish_inv(det1, i1, u1, v1, tb, h1);
-    hl.push_if(h0, t0);
-    hl.push_if(two && h1, t1);
-}
-
 // Binned render: kTileWaves waves per workgroup (one 32x8 row of a region's
 // tiles), regions in the launch order of bins.order; each wave stores its own
 // statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
@@ -1643,22 +1615,11 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
                     test_staged_one(st, k0 + b, dx, dy, dz, sx, sy, sz, hl);
                 }
             } else {
-#if XRT_STAGED_PAIRS
-            while (m) {
-                const uint32_t b0 = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1ull;
-                const bool two = m != 0ull;
-                const uint32_t b1 = two ? (uint32_t)__builtin_ctzll(m) : b0;
-                m &= m - 1ull;
-                test_staged_pair(st, k0 + b0, k0 + b1, two, dx, dy, dz, hl);
-            }
-#else
-            while (m) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                clear_lane_bit(m, b);
-                test_staged_one(st, k0 + b, dx, dy, dz, hl);
-            }
-#endif
+                while (m) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                    clear_lane_bit(m, b);
+                    test_staged_one(st, k0 + b, dx, dy, dz, hl);
+                }
             }
         }
     }
