@@ -361,6 +361,18 @@ int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
 int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
 
 /*
+ * The BINNED kernel's fill plan (DESIGN.md "Fill plan"): regions whose lists
+ * the geometry's sizing frame counted empty render as one miss-filling
+ * workgroup each instead of 16 tile waves.  mode 1 (default) on, 0 off;
+ * test hook 2 plans every region as empty, so every workgroup takes the
+ * exact fallback of a region that is not.  The next frame re-sizes.
+ */
+int xrt_set_fill_plan(xrt_context* ctx, int mode);
+
+/* Diagnostics: regions the last enqueued BINNED frame rendered through the fill plan. */
+int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
+
+/*
  * Diagnostics: copies the last render's statistics records (32 bytes each, one
  * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
  * overflow rays, hits, wave-level triangle tests, candidates, max hits; builds

@@ -207,6 +207,16 @@ class Context:
     def set_bin_capacity(self, entries: int):
         self._check(self._lib.xrt_set_bin_capacity(self._ctx, int(entries)), "xrt_set_bin_capacity")
 
+    def set_fill_plan(self, mode: int):
+        """BINNED fill plan: 1 on (default), 0 off, 2 every region planned empty (test hook)."""
+        self._check(self._lib.xrt_set_fill_plan(self._ctx, int(mode)), "xrt_set_fill_plan")
+
+    def fill_regions(self) -> int:
+        """Regions the last enqueued BINNED frame rendered through the fill plan."""
+        n = ctypes.c_uint32()
+        self._check(self._lib.xrt_debug_fill_regions(self._ctx, ctypes.byref(n)), "xrt_debug_fill_regions")
+        return n.value
+
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
                     image=True, lbuffer=True, u8=True):
         """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats)."""

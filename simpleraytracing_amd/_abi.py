@@ -129,6 +129,8 @@ XRT_SYMBOLS = {
                                  ctypes.POINTER(ctypes.c_uint8), _fp]),
     "xrt_set_hit_capacity": (ctypes.c_int, [_CtxP, _u32]),
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
+    "xrt_set_fill_plan": (ctypes.c_int, [_CtxP, ctypes.c_int]),
+    "xrt_debug_fill_regions": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint32)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),

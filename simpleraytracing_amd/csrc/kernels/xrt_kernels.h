@@ -1109,6 +1109,13 @@ struct BinBuffers {
     // from the counts of the first frame of the geometry (identical for every
     // frame of it).  Null: fixed capacity `cap` per slot (that first frame).
     const uint32_t* offsets;
+    // Slots [0, tile_slots) render as tiles (16 waves a region); the rest are
+    // the fill plan's empty regions (one workgroup each).  = regions: no plan.
+    uint32_t tile_slots;
+    // Fill plan: k_prep stores 1 here (host-mapped memory, read by the host
+    // before it launches the render) when it bins a pair past tile_slots or a
+    // triangle into the global list.  Null: no plan to check.
+    uint32_t* plan_miss;
 };
 
 __device__ __forceinline__ uint32_t list_base(const BinBuffers& b, uint32_t slot)
@@ -1257,6 +1264,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     bool global = false;
     const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
     if (valid && global) {                         // footprint over > kGlobalRegions regions
+        if (bins.plan_miss) *bins.plan_miss = 1u;  // the plan assumed an empty global list
         RegionEntry* e = bins.global_list + atomicAdd(&bs->global_count, 1u);
         e->e0 = fp.e0;
         e->e1 = fp.e1;
@@ -1307,6 +1315,11 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
                     own[b] = s_qown[wave][q];
                 }
             }
+            bool planned_empty = false;            // a pair for a region the fill plan fills
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) planned_empty |= reg[b] != kEmpty && reg[b] >= bins.tile_slots;
+            if (__builtin_expect(bins.plan_miss != nullptr && __ballot(planned_empty) != 0ull, 0) && lane == 0)
+                *bins.plan_miss = 1u;
             uint32_t lbase[kBinBatch], lcap[kBinBatch];
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
@@ -1388,6 +1401,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 6);
     commit();                                      // (2)
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
     // A region count past the list capacity: the render of that region falls
@@ -1505,41 +1519,19 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     if (__ballot(h)) hl.push_if(h, t, __float_as_uint(st.q[0][k].w), hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
 }
 
-// Binned render: kTileWaves waves per workgroup (one 32x8 row of a region's
-// tiles), regions in the launch order of bins.order; each wave stores its own
-// statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
-// occupancy is what hides it.
+// One wave's 8x8 tile `tile` of the region in launch slot `slot`: the body of
+// k_render_binned.  Every wave of the workgroup calls it for the same slot
+// (they stage the region's candidates together); the statistics accumulate in
+// ws, and `cand` gets the region's candidate count.
 template <bool kSigned>
-__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(kSigned ? 5 : XRT_RENDER_WAVES, 8))) void k_render_binned(
-    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
-    BinBuffers bins, const BinState* __restrict__ bs)
+__device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __restrict__ recs,
+                                            const float4* __restrict__ culls, const RenderParams& p,
+                                            const Outputs& out, const BinBuffers& bins, uint32_t n_glob,
+                                            uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand,
+                                            uint64_t& t_staged)
 {
-    static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
-                  "a workgroup's waves render tiles of one region");
-    __shared__ RegionStage st;
-    const uint64_t t_start = block_start_stamp();
-#if XRT_XCD_REMAP
-    // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
-    // each run of 8 regions, give XCD x all workgroups of region x, so a region's
-    // candidate list and triangle records are cached by one L2 instead of four.
-    // A bijection on full runs; the tail keeps the identity.
-    constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
-    constexpr uint32_t kPerXcd = XRT_XCD_REMAP * kBlocksPerRegion;   // XRT_XCD_REMAP regions per XCD per run
-    constexpr uint32_t kRun = 8u * kPerXcd;
-    uint32_t blk = blockIdx.x;
-    if (blk < (gridDim.x / kRun) * kRun) {
-        const uint32_t within = blk % kRun;
-        blk = (blk - within) + (within & 7u) * kPerXcd + (within >> 3);
-    }
-    const uint32_t g = blk * kTileWaves + wave_in_block();                // wave of the grid
-#else
-    const uint32_t g = blockIdx.x * kTileWaves + wave_in_block();        // wave of the grid
-#endif
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
-    const uint32_t tile = g % kWavesPerRegion;
     const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
-    const uint32_t n_glob = wave_uniform(bs->global_count);
     uint32_t reg_x, reg_y;
     if (bins.order) {
         const uint32_t xy = wave_uniform(bins.order[slot]);
@@ -1554,6 +1546,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t T = p.num_triangles;
     const bool whole = n_local > list_cap(bins, slot);   // the list overflowed: whole mesh (exact, slower)
     const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole ? T : n_local + n_glob;
+    cand = n_cand;
 
     const uint32_t tx0 = reg_x * kRegion + (tile & 3u) * 8u;
     const uint32_t ty0 = p.row_begin + reg_y * kRegion + (tile >> 2) * 8u;
@@ -1576,7 +1569,6 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
-    uint64_t t_staged = t_start;                   // XRT_STAMPS diagnostics
     // every wave of the workgroup takes part in every round's staging and barriers
     for (uint32_t base = 0; base < n_cand; base += kBinStage) {
         const uint32_t cnt = min(kBinStage, n_cand - base);
@@ -1623,33 +1615,130 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
             }
         }
     }
-    WaveStats ws = {};
-    ws.tile_tests = tests;
-    if (tile_live) {
-        if (have_ray) {
-            const uint32_t nl = whole ? 0u : n_local;
-            auto fetch = [=](uint32_t k) {
-                return whole ? k : __float_as_uint((k < nl ? local[k] : glob[k - nl]).e0.w);
-            };
-            if constexpr (kSigned)
-                finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch);
-            else
-                finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
-        } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
-            ws.rays += (uint32_t)__popcll(__ballot(active));
-            if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
-        } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
-            ws.rays += (uint32_t)__popcll(__ballot(active));
-            if (active && !(ablation(p) & kAblateStores)) {
-                const size_t o = (size_t)(row - p.row_begin) * p.width + col;
+    ws.tile_tests += tests;
+    if (!tile_live) return;
+    if (have_ray) {
+        const uint32_t nl = whole ? 0u : n_local;
+        auto fetch = [=](uint32_t k) {
+            return whole ? k : __float_as_uint((k < nl ? local[k] : glob[k - nl]).e0.w);
+        };
+        if constexpr (kSigned)
+            finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch);
+        else
+            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
+    } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
+        ws.rays += (uint32_t)__popcll(__ballot(active));
+        if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
+    } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
+        ws.rays += (uint32_t)__popcll(__ballot(active));
+        if (active && !(ablation(p) & kAblateStores)) {
+            const size_t o = (size_t)(row - p.row_begin) * p.width + col;
+            if (out.image) out.image[o] = 80.0f;
+            if (out.lbuffer) out.lbuffer[o] = out.miss_l;
+            if (out.image_u8) out.image_u8[o] = 255u;
+        }
+    }
+}
+
+// The misses of a planned-empty region: wave w stores rows [w * kRows, ...)
+// of it, 64 / kRegion rows per store (128-B row segments); ws.rays counts them.
+__device__ __forceinline__ void fill_region_rows(const RenderParams& p, const Outputs& out,
+                                                 const BinBuffers& bins, uint32_t slot, uint32_t wave,
+                                                 WaveStats& ws)
+{
+    uint32_t reg_x, reg_y;
+    if (bins.order) {
+        const uint32_t xy = wave_uniform(bins.order[slot]);
+        reg_x = xy & 0xFFFFu;
+        reg_y = xy >> 16;
+    } else {
+        reg_x = slot % bins.regions_x;
+        reg_y = slot / bins.regions_x;
+    }
+    constexpr uint32_t kRows = kRegion / kTileWaves;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t col = reg_x * kRegion + (lane % kRegion);
+    const uint32_t r0 = p.row_begin + reg_y * kRegion + wave * kRows;
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kRows; i += 64u / kRegion) {
+        const uint32_t row = r0 + i + lane / kRegion;
+        if (col < p.width && row < p.row_end) {
+            ++n;
+            const size_t o = (size_t)(row - p.row_begin) * p.width + col;
+            if (!(ablation(p) & kAblateStores)) {
                 if (out.image) out.image[o] = 80.0f;
                 if (out.lbuffer) out.lbuffer[o] = out.miss_l;
                 if (out.image_u8) out.image_u8[o] = 255u;
             }
         }
     }
+    ws.rays = wave_reduce_u32<false>(n);
+}
+
+// Binned render: kTileWaves waves per workgroup (one 32x8 row of a region's
+// tiles), regions in the launch order of bins.order; each wave stores its own
+// statistics record.  8 waves per SIMD: the tile waves are latency-bound, and
+// occupancy is what hides it.
+//
+// Fill plan (bins.tile_slots < regions): the slots past tile_slots hold the
+// regions the geometry's sizing frame counted empty (no list entry, no global
+// list); each gets ONE workgroup -- wave w stores the misses of the region's
+// rows [w * 32 / kTileWaves, ...) -- instead of 16 / kTileWaves tile
+// workgroups.  The counts are a function of the geometry, and the host only
+// launches a plan that this frame's k_prep confirmed (no pair binned past
+// tile_slots, an empty global list: BinBuffers::plan_miss); otherwise every
+// region renders as tiles.  The signed model always renders tiles.
+template <bool kSigned>
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(kSigned ? 5 : XRT_RENDER_WAVES, 8))) void k_render_binned(
+    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
+    BinBuffers bins, const BinState* __restrict__ bs)
+{
+    static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
+                  "a workgroup's waves render tiles of one region");
+    constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
+    __shared__ RegionStage st;
+    const uint64_t t_start = block_start_stamp();
+    const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
+    const uint32_t wave = wave_in_block();
+    const uint32_t n_glob = wave_uniform(bs->global_count);
+    uint64_t t_staged = t_start;                   // XRT_STAMPS diagnostics
+    WaveStats ws = {};
+    uint32_t cand = 0;
+    if (!kSigned && blockIdx.x >= tile_blocks) {   // a planned-empty region (workgroup-uniform)
+        const uint32_t slot = bins.tile_slots + (blockIdx.x - tile_blocks);
+        // statistics records: kBlocksPerRegion per wave, after the tile waves'
+        const uint32_t rec0 =
+            tile_blocks * kTileWaves + ((blockIdx.x - tile_blocks) * kTileWaves + wave) * kBlocksPerRegion;
+        fill_region_rows(p, out, bins, slot, wave, ws);
+        store_wave_stats(ws, 0u, out.block_stats, rec0, t_start);
+        if ((threadIdx.x & 63u) == 0u) {
+#pragma unroll
+            for (uint32_t k = 1; k < kBlocksPerRegion; ++k) out.block_stats[rec0 + k] = BlockStats{};
+        }
+        return;
+    }
+#if XRT_XCD_REMAP
+    // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
+    // each run of 8 regions, give XCD x all workgroups of region x, so a region's
+    // candidate list and triangle records are cached by one L2 instead of four.
+    // A bijection on full runs of the tile workgroups; the tail keeps the identity.
+    constexpr uint32_t kPerXcd = XRT_XCD_REMAP * kBlocksPerRegion;   // XRT_XCD_REMAP regions per XCD per run
+    constexpr uint32_t kRun = 8u * kPerXcd;
+    uint32_t blk = blockIdx.x;
+    if (blk < (tile_blocks / kRun) * kRun) {
+        const uint32_t within = blk % kRun;
+        blk = (blk - within) + (within & 7u) * kPerXcd + (within >> 3);
+    }
+    const uint32_t g = blk * kTileWaves + wave;                      // wave of the grid
+#else
+    const uint32_t g = blockIdx.x * kTileWaves + wave;               // wave of the grid
+#endif
+    const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
+    const uint32_t tile = g % kWavesPerRegion;
+    render_tile<kSigned>(st, recs, culls, p, out, bins, n_glob, slot, tile, ws, cand, t_staged);
     // candidates are counted once per region (by the wave holding tile 0)
-    store_wave_stats(ws, tile == 0u ? n_cand : 0u, out.block_stats, g, t_start, (uint32_t)(t_staged - t_start));
+    store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, t_start, (uint32_t)(t_staged - t_start));
 }
 
 // ---------------------------------------------------------------------------

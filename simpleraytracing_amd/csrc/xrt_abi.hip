@@ -80,6 +80,9 @@ struct FrameSet {
     hipEvent_t done = nullptr;         // render end (unsampled frames of a timed region)
     hipEvent_t done_ev = nullptr;      // the event that marks the set's last render complete
     bool done_valid = false;
+    // Fill plan check (BinBuffers::plan_miss): host-mapped, cleared by the host
+    // before k_prep, read after the host has waited for k_prep's completion.
+    volatile uint32_t* plan_flag = nullptr;
 };
 
 struct xrt_context {
@@ -104,6 +107,17 @@ struct xrt_context {
     uint32_t* d_order = nullptr;       // render launch order of the regions (launch_order)
     size_t order_cap = 0;
     uint32_t order_rx = 0, order_ry = 0;
+    std::vector<uint32_t> h_order;     // slot -> region (x | y << 16) of d_order
+    // Fill plan of the current geometry (bin_key): launch order with the
+    // regions its sizing frame counted empty last, one workgroup each
+    // (DESIGN.md "Fill plan").  fill_plan: 1 on (XRT_FILL=0 / xrt_set_fill_plan
+    // turn it off); 2 plans EVERY region as empty (tests of the exact fallback).
+    int fill_plan = 1;
+    uint32_t* d_plan = nullptr;        // [slot -> region | region -> slot]
+    size_t plan_cap = 0;
+    uint32_t plan_tile_slots = 0;
+    bool plan_valid = false;
+    uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
 
     // staging for the host-pointer entry point
     float* d_image = nullptr;
@@ -437,12 +451,43 @@ int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
         int rc = ensure(ctx, ctx->d_order, ctx->order_cap, 2 * n);
         if (rc) return rc;
         XRT_HIP(ctx, hipMemcpy(ctx->d_order, order.data(), 2 * n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        order.resize(n);
+        ctx->h_order.swap(order);
         ctx->order_rx = rx;
         ctx->order_ry = ry;
     }
     bins.order = ctx->d_order;
     bins.rank = ctx->d_order + (size_t)rx * ry;
     return XRT_OK;
+}
+
+// Region (row-major index) of a launch slot under the base launch order
+// (launch_order's host copy; raster without one).
+inline uint32_t slot_to_region(const xrt_context* ctx, const BinBuffers& bins, uint32_t slot)
+{
+    if (!bins.order) return slot;
+    const uint32_t xy = ctx->h_order[slot];
+    return (xy & 0xFFFFu) + (xy >> 16) * ctx->order_rx;
+}
+
+// The current geometry's fill plan as the launch order (DESIGN.md "Fill plan").
+// The signed model keeps the plan's order (the compact lists are sized by its
+// slots) but renders every region as tiles.
+void use_plan(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fill)
+{
+    bins.order = ctx->d_plan;
+    bins.rank = ctx->d_plan + n_regions;
+    bins.tile_slots = fill ? ctx->plan_tile_slots : n_regions;
+}
+
+// Arms the k_prep check of a frame that uses the fill plan.
+void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins)
+{
+    bins.plan_miss = nullptr;
+    if (bins.tile_slots < n_regions) {
+        *fs.plan_flag = 0u;
+        bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
+    }
 }
 
 // A frame between its preparation (enqueued) and its render launch.  Split so
@@ -513,6 +558,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     }();
     hipStream_t ps = pipeline == 1 ? ctx->prep_stream : stream;
     unsigned prep_flags = pipeline == 2 ? hipExtAnyOrderLaunch : 0u;
+    // The fill plan needs the host between k_prep and the render (the plan
+    // check) and the attenuation model (the signed render fills nothing).
+    const bool fill_ok = ps != stream && !signed_model;
     const auto t_call = HostClock::now();
     if (fs.done_valid) {
         const auto t = HostClock::now();
@@ -543,17 +591,6 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     std::memcpy(&out.miss_l, &miss_bits, sizeof miss_bits);
     out.mu = ctx->mu;
     const uint32_t n_regions = rows ? rx * ry : 0u;
-    // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup
-    dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
-              : binned                     ? dim3(kWavesPerRegion / kTileWaves * n_regions)
-                                           : dim3(rx, ry);
-    // stats records: one per workgroup, one per tile wave for BINNED
-    const uint32_t n_blocks = rows ? grid.x * grid.y * (binned ? kTileWaves : 1u) : 0u;
-    if ((rc = ensure(ctx, fs.block_stats, fs.block_stats_cap, n_blocks))) return rc;
-    fs.n_blocks = n_blocks;
-    fs.binned = binned;
-    out.block_stats = fs.block_stats;
-
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
     xrt_context::BinKey key = {};                  // the frame geometry of the region lists
@@ -571,6 +608,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared))) return rc;
         if (cleared) prep_flags = 0u;              // an any-order k_prep could start before the memset
         if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
+        bins.tile_slots = n_regions;
+        if (!new_geometry && ctx->compact && ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
+        arm_plan_check(fs, n_regions, bins);
     }
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
@@ -580,14 +620,34 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // strip): a synchronous read of every region's count, slot offsets
         // from them, and a re-run of k_prep into the compact lists.
         std::vector<uint32_t> counts((size_t)n_regions * kCounterStride);
+        BinState st = {};
         XRT_HIP(ctx, hipMemcpyAsync(counts.data(), bins.counts, counts.size() * sizeof(uint32_t),
                                     hipMemcpyDeviceToHost, ps));
+        XRT_HIP(ctx, hipMemcpyAsync(&st, bin_ctl, sizeof st, hipMemcpyDeviceToHost, ps));
         XRT_HIP(ctx, hipStreamSynchronize(ps));
+        // The fill plan: the regions this frame counted empty (with an empty
+        // global list) go to the end of the launch order, one workgroup each.
+        // The slots are renumbered; the counts above are by the old slots.
+        std::vector<uint32_t> slot_region(n_regions);   // new slot -> region
+        for (uint32_t s = 0; s < n_regions; ++s) slot_region[s] = slot_to_region(ctx, bins, s);
+        uint32_t tile_slots = n_regions;
+        const int plan = ctx->fill_plan;
+        if (plan != 0 && st.global_count == 0u && bins.order) {
+            std::vector<uint32_t> full, empty;
+            for (uint32_t s = 0; s < n_regions; ++s)
+                (counts[(size_t)s * kCounterStride] == 0u || plan == 2 ? empty : full).push_back(slot_region[s]);
+            tile_slots = (uint32_t)full.size();
+            full.insert(full.end(), empty.begin(), empty.end());
+            slot_region.swap(full);
+        }
+        std::vector<uint32_t> count_of(n_regions);     // by region
+        for (uint32_t s = 0; s < n_regions; ++s)
+            count_of[slot_to_region(ctx, bins, s)] = counts[(size_t)s * kCounterStride];
         std::vector<uint32_t> off(n_regions + 1u);
         uint64_t run = 0;
-        for (uint32_t r = 0; r < n_regions; ++r) {
-            off[r] = (uint32_t)run;
-            const uint64_t c = counts[(size_t)r * kCounterStride];
+        for (uint32_t s = 0; s < n_regions; ++s) {
+            off[s] = (uint32_t)run;
+            const uint64_t c = count_of[slot_region[s]];
             run += c + c / 8u + 4u;
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
@@ -595,14 +655,43 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         XRT_HIP(ctx, hipDeviceSynchronize());      // frames in flight may read the previous offsets
         if ((rc = ensure(ctx, ctx->d_slot_off, ctx->slot_off_cap, off.size()))) return rc;
         XRT_HIP(ctx, hipMemcpy(ctx->d_slot_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ctx->plan_valid = false;
+        if (tile_slots < n_regions) {
+            // [slot -> region as (x | y << 16) | region -> slot], as launch_order's
+            std::vector<uint32_t> ord(2 * (size_t)n_regions);
+            for (uint32_t s = 0; s < n_regions; ++s) {
+                const uint32_t r = slot_region[s];
+                ord[s] = (r % rx) | ((r / rx) << 16);
+                ord[(size_t)n_regions + r] = s;
+            }
+            if ((rc = ensure(ctx, ctx->d_plan, ctx->plan_cap, ord.size()))) return rc;
+            XRT_HIP(ctx, hipMemcpy(ctx->d_plan, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            ctx->plan_tile_slots = tile_slots;
+            ctx->plan_valid = true;
+        }
         ctx->slot_pool = run;
         ctx->compact = true;
         ctx->bin_key = key;
         ctx->bin_key_valid = true;
         bool cleared = false;
         if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
+        if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
+        bins.tile_slots = n_regions;
+        if (ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
+        arm_plan_check(fs, n_regions, bins);
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
     }
+    // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
+    // one workgroup per region of the fill plan
+    const dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
+                    : binned ? dim3(kWavesPerRegion / kTileWaves * bins.tile_slots + (n_regions - bins.tile_slots))
+                             : dim3(rx, ry);
+    // stats records: one per workgroup; BINNED one per tile wave, 16 per fill region
+    const uint32_t n_blocks = !rows ? 0u : binned ? kWavesPerRegion * n_regions : grid.x * grid.y;
+    if ((rc = ensure(ctx, fs.block_stats, fs.block_stats_cap, n_blocks))) return rc;
+    fs.n_blocks = n_blocks;
+    fs.binned = binned;
+    out.block_stats = fs.block_stats;
     pf.fs = &fs;
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
@@ -627,10 +716,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     const int kernel = pf.kernel;
     const bool binned = pf.binned;
     const uint32_t rows = pf.rows, rx = pf.rx, ry = pf.ry;
-    const dim3 grid = pf.grid;
     const RenderParams& p = pf.p;
     const Outputs& out = pf.out;
-    const BinBuffers& bins = pf.bins;
     BinState* bin_ctl = pf.bin_ctl;
     const auto t_call = pf.t_call;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
@@ -642,6 +729,16 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         XRT_HIP(ctx, hipEventSynchronize(prep_done));
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
     }
+    dim3 grid = pf.grid;
+    BinBuffers bins = pf.bins;
+    if (binned && bins.plan_miss && *fs.plan_flag != 0u) {
+        // k_prep binned a pair into a region the plan fills (or into the global
+        // list): this frame renders every region as tiles, the next re-plans.
+        bins.tile_slots = rx * ry;
+        grid = dim3(kWavesPerRegion / kTileWaves * bins.tile_slots);
+        ctx->bin_key_valid = false;
+    }
+    ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
 
     // Events ride on the render's own dispatch (hipExtLaunchKernel).  Outside
     // timed regions every frame carries the set's start/end pair (stats
@@ -748,6 +845,8 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
+    const char* fp = std::getenv("XRT_FILL");       // A/B: "0" = no fill plan
+    if (fp) ctx->fill_plan = std::atoi(fp);
     // The prep stream gets the highest queue priority: its small workgroups
     // must find CU slots while the previous frame's render fills the chip.
     int prio_least = 0, prio_greatest = 0;
@@ -759,7 +858,8 @@ int xrt_create(int device, xrt_context** out)
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
-             hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess;
+             hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
+             hipHostMalloc((void**)&fs.plan_flag, sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
         return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
@@ -785,6 +885,7 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.cull);
         (void)hipFree(fs.block_stats);
         (void)hipFree(fs.frame);
+        if (fs.plan_flag) (void)hipHostFree((void*)fs.plan_flag);
         (void)hipFree(fs.offsets);
         (void)hipFree(fs.bin_counts);
         (void)hipFree(fs.bin_list);
@@ -794,6 +895,7 @@ void xrt_destroy(xrt_context* ctx)
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
     (void)hipFree(ctx->d_order);
+    (void)hipFree(ctx->d_plan);
     (void)hipFree(ctx->d_slot_off);
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
@@ -1021,6 +1123,23 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->bin_force_cap = (size_t)entries;
+    return XRT_OK;
+}
+
+int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions)
+{
+    if (!ctx || !regions) return XRT_ERR_ARGUMENT;
+    *regions = ctx->last_fill_regions;
+    return XRT_OK;
+}
+
+int xrt_set_fill_plan(xrt_context* ctx, int mode)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (mode < 0 || mode > 2) return fail(ctx, XRT_ERR_ARGUMENT, "fill plan mode must be 0, 1 or 2");
+    ctx->fill_plan = mode;
+    ctx->bin_key_valid = false;         // the next frame re-sizes and re-plans
+    ctx->plan_valid = false;
     return XRT_OK;
 }
 

@@ -401,6 +401,61 @@ def test_all_kernels_equal_2048(ctx, dragon):
     assert np.all(a[1][~miss] >= 0) and np.all(a[0] <= np.float32(80.0)) and np.all(a[0] > 0)
 
 
+STAT_FIELDS = ("rays", "hit_rays", "odd_rays", "overflow_rays", "hits", "max_hits", "tile_tests", "candidates")
+
+
+def _stats(st):
+    return tuple(getattr(st, f) for f in STAT_FIELDS)
+
+
+@pytest.mark.parametrize("W,H,r0,r1", [(2048, 2048, 0, None), (1024, 1024, 0, None), (1000, 700, 0, None),
+                                       (333, 517, 100, 400), (4096, 4096, 1536, 2048)])
+def test_fill_plan_changes_nothing(ctx, dragon, W, H, r0, r1):
+    """The fill plan (regions the sizing frame counted empty rendered as one
+    miss-filling workgroup each, DESIGN.md "Fill plan") leaves every bit and
+    every statistic of the frame as the plan-free render has them, on the
+    sizing frame and on a later frame of the geometry."""
+    ctx.set_fill_plan(0)
+    try:
+        off = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED, r0, r1)
+        assert ctx.fill_regions() == 0
+    finally:
+        ctx.set_fill_plan(1)
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    for frame in range(2):          # the sizing frame, then a frame reusing the geometry's plan
+        on = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED, r0, r1) if frame == 0 else ctx.render_rows(cam, r0, r1)
+        n_fill = ctx.fill_regions()
+        rows = (r1 or H) - r0
+        regions = -(-W // 32) * -(-rows // 32)
+        assert 0 < n_fill < regions, (frame, n_fill, regions)
+        for x, y in zip(on[:3], off[:3]):
+            assert np.array_equal(bits(x), bits(y)), frame
+        assert _stats(on[3]) == _stats(off[3]), frame
+
+
+def test_fill_plan_rejected_when_k_prep_bins_into_it(ctx, dragon):
+    """Test hook 2 plans every region as empty.  k_prep then bins pairs into
+    planned-empty regions and flags it, and the host launches that frame with
+    every region rendered as tiles (no region is filled) -- exact against the
+    oracle and the plan-free render."""
+    W, H = 160, 96
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    ref = oracle.render_rows(dragon, cam, W, H)
+    ctx.set_fill_plan(2)
+    try:
+        got = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED)
+        assert ctx.fill_regions() == 0
+        assert_same(got, ref, "rejected plan")
+        big = render(ctx, dragon, 1024, 1024, xrt.XRT_KERNEL_BINNED)
+        assert ctx.fill_regions() == 0
+    finally:
+        ctx.set_fill_plan(1)
+    plain = render(ctx, dragon, 1024, 1024, xrt.XRT_KERNEL_BINNED)
+    for x, y in zip(big[:3], plain[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    assert _stats(big[3]) == _stats(plain[3])
+
+
 @pytest.mark.parametrize("kernel", [xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED])
 def test_culled_4096_rows_vs_oracle(ctx, dragon, kernel):
     W = H = 4096

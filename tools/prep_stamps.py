@@ -72,6 +72,11 @@ def main():
         d = (prep[have, k] - prep[have, k - 1 if k != 5 else 4]) * TICK_US
         res[f"phase{k}"] = {"n": int(have.sum()), "med_us": round(float(np.median(d)), 2),
                             "max_us": round(float(d.max()), 2), "last_end_us": round(float(rel(prep[have, k].max())), 2)}
+    if (prep[:, 6] > 0).any():          # stamp 6: before the final commit (inside phase 3)
+        have = prep[:, 6] > 0
+        for name, a, b in (("phase3_expand", 2, 6), ("phase3_commit", 6, 3)):
+            d = (prep[have, b] - prep[have, a]) * TICK_US
+            res[name] = {"med_us": round(float(np.median(d)), 2), "max_us": round(float(d.max()), 2)}
     scan = st[60000:60004].astype(np.int64)
     res["scan_us"] = [round(float(rel(x)), 2) for x in scan]
     fill = st[32768:32768 + 2 * 4096].reshape(4096, 2).astype(np.int64)
