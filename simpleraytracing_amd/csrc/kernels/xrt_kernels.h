@@ -1073,9 +1073,15 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
 // Region counters touched by atomics are padded to one 128-B L2 line each:
 // atomics on one line serialise, and neighbouring regions are hot together.
 constexpr uint32_t kCounterStride = 32;
-constexpr uint32_t kBinBatch = 4;            // queued pairs per lane per commit round (their atomics in flight together)
+#ifndef XRT_BIN_BATCH
+#define XRT_BIN_BATCH 4
+#endif
+#ifndef XRT_BIN_QUEUE
+#define XRT_BIN_QUEUE 256
+#endif
+constexpr uint32_t kBinBatch = XRT_BIN_BATCH;  // queued pairs per lane per commit round (their atomics in flight together)
 constexpr uint32_t kBinSmall = 64;           // region rectangles up to this many cells are flattened over the wave
-constexpr uint32_t kBinQueue = 256;          // passing (region, triangle) pairs queued per wave before a commit         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics         // cells per batch of back-to-back count atomics
+constexpr uint32_t kBinQueue = XRT_BIN_QUEUE;  // passing (region, triangle) pairs queued per wave before a commit
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -1490,7 +1496,7 @@ __device__ __forceinline__ void stage_mesh(RegionStage& st, const float4* __rest
 }
 
 __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
-                                                float dz, HitList& hl)
+                                                float dz, HitList& hl, bool push = true)
 {
     // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[7].x)
     const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k];
@@ -1502,7 +1508,8 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
                                                                                       : inv_det_of(det);
     bool h;
     const float t = mt_finish_inv(det, inv, u, v, tnum, h);
-    hl.push_if(h, t);
+    if (push) hl.push_if(h, t);
+    else hl.n += h && t < 1e30f ? 1u : 0u;         // XRT_ABLATE kAblatePush: the test without the insert
 }
 
 // The signed model's: the term's triangle id from the footprint (e0.w) and its
@@ -1610,7 +1617,7 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
                 while (m) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(m);
                     clear_lane_bit(m, b);
-                    test_staged_one(st, k0 + b, dx, dy, dz, hl);
+                    test_staged_one(st, k0 + b, dx, dy, dz, hl, !(ablation(p) & kAblatePush));
                 }
             }
         }

@@ -85,6 +85,8 @@ struct FrameSet {
     volatile uint32_t* plan_flag = nullptr;
 };
 
+using HostClock = std::chrono::steady_clock;
+
 struct xrt_context {
     int device = 0;
     std::string error;
@@ -162,11 +164,11 @@ struct xrt_context {
     uint32_t hit_capacity = kMaxHits;
     // XRT_HOST_PROFILE=1: host time per enqueue, split by wait (printed at destroy)
     bool host_profile = false;
-    double hp_total = 0, hp_done = 0, hp_prep = 0;
+    double hp_total = 0, hp_done = 0, hp_prep = 0, hp_lprep = 0, hp_lrender = 0, hp_gap = 0;
     uint64_t hp_calls = 0;
+    HostClock::time_point hp_last_end{};
 };
 
-using HostClock = std::chrono::steady_clock;
 inline double seconds_since(HostClock::time_point t)
 {
     return std::chrono::duration<double>(HostClock::now() - t).count();
@@ -361,11 +363,13 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
     const uint64_t T = ctx->num_tris;
     const uint64_t threads =
         std::max<uint64_t>(std::max<uint64_t>(T, (uint64_t)p.height + p.width), bins.clear ? bins.clear_regions : 0u);
+    const auto t_launch = HostClock::now();
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads),
                           0, stream, nullptr, done, flags,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
+    if (ctx->host_profile) ctx->hp_lprep += seconds_since(t_launch);
     return XRT_OK;
 }
 
@@ -776,6 +780,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     }
     if (rows > 0) {
         const bool sgn = p.model == kModelSigned;
+        const auto t_launch = HostClock::now();
         if (kernel == XRT_KERNEL_BRUTE)
             hipExtLaunchKernelGGL(sgn ? k_render_brute<true> : k_render_brute<false>, grid, dim3(256), 0, stream,
                                   t0, t1, 0, fs.recs, p, out);
@@ -786,6 +791,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
             hipExtLaunchKernelGGL(sgn ? k_render_binned<true> : k_render_binned<false>, grid, dim3(64 * kTileWaves),
                                   0, stream, t0, t1, 0, fs.recs, fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
+        if (ctx->host_profile) ctx->hp_lrender += seconds_since(t_launch);
         if (t0) {
             ctx->last_t0 = t0;
             ctx->last_t1 = t1;
@@ -797,6 +803,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     }
     if (ctx->host_profile) {
         ctx->hp_total += seconds_since(t_call);
+        if (ctx->hp_calls) ctx->hp_gap += std::chrono::duration<double>(t_call - ctx->hp_last_end).count();
+        ctx->hp_last_end = HostClock::now();
         ++ctx->hp_calls;
     }
     ctx->last_set = &fs;
@@ -873,9 +881,11 @@ void xrt_destroy(xrt_context* ctx)
     if (!ctx) return;
     if (ctx->host_profile && ctx->hp_calls)
         std::fprintf(stderr, "xrt host profile: %llu enqueues, per call %.1f us (waiting: set reuse %.1f us, "
-                     "preparation %.1f us)\n", (unsigned long long)ctx->hp_calls,
-                     ctx->hp_total / ctx->hp_calls * 1e6, ctx->hp_done / ctx->hp_calls * 1e6,
-                     ctx->hp_prep / ctx->hp_calls * 1e6);
+                     "preparation %.1f us; launching: k_prep %.1f us, render %.1f us; between calls %.1f us)\n",
+                     (unsigned long long)ctx->hp_calls, ctx->hp_total / ctx->hp_calls * 1e6,
+                     ctx->hp_done / ctx->hp_calls * 1e6, ctx->hp_prep / ctx->hp_calls * 1e6,
+                     ctx->hp_lprep / ctx->hp_calls * 1e6, ctx->hp_lrender / ctx->hp_calls * 1e6,
+                     ctx->hp_gap / ctx->hp_calls * 1e6);
     (void)hipSetDevice(ctx->device);
     if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
     (void)hipDeviceSynchronize();
