@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
                          "N ranks on fewer GPUs")
+    ap.add_argument("--transit", choices=["packed", "dense"], default="packed",
+                    help="strips mode: send the regions the strip's fill plan did not fill (packed) or the "
+                         "whole L-buffer strip (dense)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses device 0 (with --dist-backend gloo)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -230,6 +233,7 @@ def main():
     # its frame's L plane and expands the image and u8 planes from them
     # (xrt_expand_rows_device) -- frame k's gather overlaps frame k+1's render.
     root = rank == 0 or not strips
+    packed = gathering and args.transit == "packed"
     if root:
         img = torch.zeros(W * H, dtype=torch.float32, device=dev)
         lb = torch.zeros(W * H, dtype=torch.float32, device=dev)
@@ -242,6 +246,33 @@ def main():
     o0 = bounds[0][1] * W
     frame_no = [0]
 
+    # Packed transit: a sender's strip travels as the 32x32 blocks of the regions
+    # its fill plan did not fill (those hold only misses).  The map of each
+    # strip is a function of its geometry: one untimed frame sizes it, and the
+    # senders send their maps to rank 0 once.
+    if packed:
+        if not root:
+            ctx.render_rows_device(cam, r0, r1, 0, tbufs[0].data_ptr(), 0, stream.cuda_stream)
+            rmap, n_packed = ctx.plan_region_map(W, r1 - r0)
+            expect_fill = len(rmap) - n_packed
+            d_map = torch.from_numpy(rmap.view(np.int32)).to(dev)
+            pbufs = [torch.zeros(max(n_packed, 1) * 1024, dtype=torch.float32, device=dev) for _ in range(2)]
+            meta = torch.tensor([n_packed], dtype=torch.int64)
+            dist.send(meta.to(dev) if nccl else meta, dst=0)
+            dist.send(d_map if nccl else d_map.cpu(), dst=0)
+        else:
+            peer = {}
+            for g, (b, e) in enumerate(bounds):
+                if not g:
+                    continue
+                meta = torch.zeros(1, dtype=torch.int64, device=dev if nccl else "cpu")
+                dist.recv(meta, src=g)
+                n_regions = -(-W // 32) * -(-(e - b) // 32)
+                m = torch.zeros(n_regions, dtype=torch.int32, device=dev if nccl else "cpu")
+                dist.recv(m, src=g)
+                npk = int(meta.item())
+                peer[g] = (m.to(dev), npk, torch.zeros(max(npk, 1) * 1024, dtype=torch.float32, device=dev))
+
     def send_strip(t):
         if nccl:
             return dist.isend(t, dst=0)
@@ -249,16 +280,25 @@ def main():
         return None
 
     def recv_strips():
+        if packed:
+            bufs = {g: peer[g][2][:max(peer[g][1], 1) * 1024] for g in peer}
+        else:
+            bufs = {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
         if nccl:
-            ops = [dist.P2POp(dist.irecv, lb[b * W:e * W], g) for g, (b, e) in enumerate(bounds) if g]
+            ops = [dist.P2POp(dist.irecv, t, g) for g, t in bufs.items()]
             for w in dist.batch_isend_irecv(ops):
                 w.wait()                      # the current stream waits for the receives
         else:
+            for g, t in bufs.items():
+                host = torch.empty(t.numel(), dtype=torch.float32)
+                dist.recv(host, src=g)
+                t.copy_(host, non_blocking=False)
+        if packed:
             for g, (b, e) in enumerate(bounds):
                 if g:
-                    host = torch.empty((e - b) * W, dtype=torch.float32)
-                    dist.recv(host, src=g)
-                    lb[b * W:e * W].copy_(host, non_blocking=False)
+                    d_map, _, buf = peer[g]
+                    ctx.unpack_regions_device(W, e - b, d_map.data_ptr(), buf.data_ptr(), lb.data_ptr() + 4 * b * W,
+                                              img.data_ptr() + 4 * b * W, u8.data_ptr() + b * W, stream.cuda_stream)
 
     def step():
         k = frame_no[0]
@@ -272,14 +312,22 @@ def main():
                                    u8.data_ptr() + o, stream.cuda_stream)
             if gathering:
                 recv_strips()
-                ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0,
-                                       u8.data_ptr() + o0, stream.cuda_stream)
+                if not packed:
+                    ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0,
+                                           u8.data_ptr() + o0, stream.cuda_stream)
         else:
             b = k % 2
             if pending[b] is not None:
                 pending[b].wait()             # the send of frame k-2 has read this buffer
             ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
-            pending[b] = send_strip(tbufs[b])
+            if packed:
+                if expect_fill and ctx.fill_regions() != expect_fill:   # the map assumes this frame filled them
+                    raise RuntimeError(f"rank {rank}: the strip's fill plan did not hold for frame {k}")
+                ctx.pack_regions_device(W, r1 - r0, d_map.data_ptr(), tbufs[b].data_ptr(), pbufs[b].data_ptr(),
+                                        stream.cuda_stream)
+                pending[b] = send_strip(pbufs[b])
+            else:
+                pending[b] = send_strip(tbufs[b])
 
     for _ in range(args.warmup):
         step()
@@ -315,8 +363,12 @@ def main():
         ok = (np.array_equal(img.cpu().numpy().view(np.uint32), full[0].view(np.uint32))
               and np.array_equal(lb.cpu().numpy().view(np.uint32), full[1].view(np.uint32))
               and np.array_equal(u8.cpu().numpy(), full[2]))
+        moved = sum(4096 * max(v[1], 1) for v in peer.values()) if packed else 4 * rest
         gather = {"bit_exact_vs_single_device_frame": bool(ok),
-                  "bytes_gathered_per_step": 4 * rest, "transit": "L-buffer strips, misses as XRT_MISS_TRANSIT"}
+                  "bytes_gathered_per_step": moved, "dense_bytes_per_step": 4 * rest,
+                  "transit": ("L-buffer strips, misses as XRT_MISS_TRANSIT, packed by region (the regions "
+                              "each strip's fill plan filled stay behind)") if packed
+                  else "L-buffer strips, misses as XRT_MISS_TRANSIT"}
 
     result = None
     if rank == 0:

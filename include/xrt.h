@@ -369,6 +369,30 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
  */
 int xrt_set_fill_plan(xrt_context* ctx, int mode);
 
+/*
+ * Region-packed strips for multi-GPU gathers (DESIGN.md "Multi-GPU").  A strip
+ * rendered as an L-buffer with misses coded XRT_MISS_TRANSIT travels as the
+ * 32x32 blocks of the regions its fill plan did NOT fill (the filled ones hold
+ * only misses): 1024 floats per packed region.
+ *
+ * xrt_plan_region_map: map[r] for the n_regions = ceil(width/32) x
+ * ceil(rows/32) regions of the strip (row-major) -- the packed index of
+ * region r, or 0xFFFFFFFF for a region the last enqueued frame filled;
+ * *n_packed = packed regions.  Without a plan in that frame every region is
+ * packed (map[r] = r).  The map belongs to the strip's geometry: a receiver
+ * needs the sender's map once, not per frame.
+ * xrt_pack_regions_device: d_lbuffer (the strip, rows x width) -> d_packed
+ * (n_packed x 1024 floats, 16-B aligned) on `stream`.
+ * xrt_unpack_regions_device: d_packed -> the strip's three planes (any may be
+ * NULL), with xrt_expand_rows_device's values.
+ */
+int xrt_plan_region_map(xrt_context* ctx, uint32_t width, uint32_t rows, uint32_t* map, uint64_t n_regions,
+                        uint32_t* n_packed);
+int xrt_pack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
+                            const float* d_lbuffer, float* d_packed, void* stream);
+int xrt_unpack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
+                              const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
+
 /* Diagnostics: regions the last enqueued BINNED frame rendered through the fill plan. */
 int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
 

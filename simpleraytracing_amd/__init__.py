@@ -258,6 +258,29 @@ class Context:
                                               d_u8 or None, stream or None)
         self._check(rc, "xrt_expand_rows_device")
 
+    def plan_region_map(self, width: int, rows: int):
+        """(map, n_packed) of the last frame's strip: map[r] = packed index of region r
+        (row-major 32x32 regions), 0xFFFFFFFF for a region its fill plan filled."""
+        n = -(-width // 32) * -(-rows // 32)
+        m = np.zeros(n, np.uint32)
+        k = ctypes.c_uint32()
+        self._check(self._lib.xrt_plan_region_map(self._ctx, width, rows,
+                                                  m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                                  ctypes.byref(k)), "xrt_plan_region_map")
+        return m, k.value
+
+    def pack_regions_device(self, width: int, rows: int, d_map: int, d_lbuffer: int, d_packed: int, stream: int = 0):
+        """A transit L-buffer strip into its packed regions (device pointers)."""
+        self._check(self._lib.xrt_pack_regions_device(self._ctx, width, rows, d_map, d_lbuffer, d_packed,
+                                                      stream or None), "xrt_pack_regions_device")
+
+    def unpack_regions_device(self, width: int, rows: int, d_map: int, d_packed: int, d_lbuffer: int, d_image: int,
+                              d_u8: int, stream: int = 0):
+        """Packed regions into a strip's L / image / u8 planes (device pointers; 0 skips a plane)."""
+        self._check(self._lib.xrt_unpack_regions_device(self._ctx, width, rows, d_map, d_packed, d_lbuffer or None,
+                                                        d_image or None, d_u8 or None, stream or None),
+                    "xrt_unpack_regions_device")
+
     def timing_begin(self):
         self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
 

@@ -135,6 +135,11 @@ XRT_SYMBOLS = {
     "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
     "xrt_expand_rows_device": (ctypes.c_int, [_CtxP, _u64, _vp, _vp, _vp, _vp]),
+    "xrt_plan_region_map": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_uint32), _u64, ctypes.POINTER(ctypes.c_uint32)]),
+    "xrt_pack_regions_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp]),
+    "xrt_unpack_regions_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
+                                                 _vp]),
     "xrt_multi_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_MultiP)]),
     "xrt_multi_destroy": (None, [_MultiP]),
     "xrt_multi_last_error": (ctypes.c_char_p, [_MultiP]),

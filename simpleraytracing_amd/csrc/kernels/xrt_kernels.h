@@ -1190,7 +1190,15 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
 constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 
-__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_prep(const float* __restrict__ tris, uint32_t T,
+#ifndef XRT_PREP_MAX_VGPR
+#define XRT_PREP_MAX_VGPR 0     // A/B: cap k_prep's VGPRs (0 = the compiler's choice)
+#endif
+#if XRT_PREP_MAX_VGPR
+#define XRT_PREP_VGPR_ATTR __attribute__((amdgpu_num_vgpr(XRT_PREP_MAX_VGPR)))
+#else
+#define XRT_PREP_VGPR_ATTR
+#endif
+__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) XRT_PREP_VGPR_ATTR void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
@@ -1795,6 +1803,62 @@ __global__ __launch_bounds__(256) void k_hole_fill(const float* __restrict__ lbu
     }
     if (image) image[pixel] = photon;
     if (image_u8) image_u8[pixel] = lut_u8(photon);
+}
+
+// ---------------------------------------------------------------------------
+// Region-packed strips in transit (multi-GPU gathers, DESIGN.md "Multi-GPU"):
+// the regions a strip's fill plan filled hold nothing but misses, so only the
+// others travel -- region r's 32x32 block of L values at packed[map[r] * 1024]
+// (rows of the block row-major; past the strip or the image width the block
+// holds kMissTransit).  map[r] = kEmpty for a filled region.  One workgroup of
+// 256 threads per region, 4 pixels per thread.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPackBlock = kRegion * kRegion;
+
+__global__ __launch_bounds__(256) void k_pack_regions(const float* __restrict__ lbuffer, float* __restrict__ packed,
+                                                      const uint32_t* __restrict__ map, uint32_t width,
+                                                      uint32_t rows, uint32_t regions_x)
+{
+    const uint32_t r = blockIdx.x;
+    const uint32_t slot = map[r];
+    if (slot == kEmpty) return;
+    const uint32_t row = (r / regions_x) * kRegion + threadIdx.x / 8u;
+    const uint32_t col = (r % regions_x) * kRegion + 4u * (threadIdx.x % 8u);
+    float v[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        v[k] = row < rows && col + k < width ? lbuffer[(size_t)row * width + col + k] : __uint_as_float(kMissTransit);
+    *reinterpret_cast<float4*>(packed + (size_t)slot * kPackBlock + 4u * threadIdx.x) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// The receiving side: a packed strip into the frame's three planes (k_expand's
+// values: misses -- kMissTransit, or a filled region -- give image 80, u8 255,
+// L +inf; hits the shade of L and its LUT).
+__global__ __launch_bounds__(256) void k_unpack_regions(const float* __restrict__ packed,
+                                                        const uint32_t* __restrict__ map,
+                                                        float* __restrict__ lbuffer, float* __restrict__ image,
+                                                        uint8_t* __restrict__ image_u8, uint32_t width,
+                                                        uint32_t rows, uint32_t regions_x)
+{
+    const uint32_t r = blockIdx.x;
+    const uint32_t slot = map[r];
+    const uint32_t row = (r / regions_x) * kRegion + threadIdx.x / 8u;
+    const uint32_t col = (r % regions_x) * kRegion + 4u * (threadIdx.x % 8u);
+    if (row >= rows) return;
+    float4 v = make_float4(__uint_as_float(kMissTransit), __uint_as_float(kMissTransit),
+                           __uint_as_float(kMissTransit), __uint_as_float(kMissTransit));
+    if (slot != kEmpty) v = *reinterpret_cast<const float4*>(packed + (size_t)slot * kPackBlock + 4u * threadIdx.x);
+    const float l[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (col + k >= width) break;
+        const bool miss = __float_as_uint(l[k]) == kMissTransit;
+        const float img = miss ? 80.0f : shade(l[k]);
+        const size_t o = (size_t)row * width + col + k;
+        if (image) image[o] = img;
+        if (image_u8) image_u8[o] = miss ? (uint8_t)255u : lut_u8(img);
+        if (lbuffer) lbuffer[o] = miss ? __builtin_inff() : l[k];
+    }
 }
 
 // ---------------------------------------------------------------------------

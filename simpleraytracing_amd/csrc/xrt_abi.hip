@@ -120,6 +120,8 @@ struct xrt_context {
     uint32_t plan_tile_slots = 0;
     bool plan_valid = false;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
+    std::vector<uint32_t> h_plan_region;   // the plan's slot -> region (row-major over the strip)
+    uint32_t plan_rx = 0, plan_ry = 0;
 
     // staging for the host-pointer entry point
     float* d_image = nullptr;
@@ -672,6 +674,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
             XRT_HIP(ctx, hipMemcpy(ctx->d_plan, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
             ctx->plan_tile_slots = tile_slots;
             ctx->plan_valid = true;
+            ctx->h_plan_region = slot_region;
+            ctx->plan_rx = rx;
+            ctx->plan_ry = ry;
         }
         ctx->slot_pool = run;
         ctx->compact = true;
@@ -1133,6 +1138,56 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->bin_force_cap = (size_t)entries;
+    return XRT_OK;
+}
+
+int xrt_plan_region_map(xrt_context* ctx, uint32_t width, uint32_t rows, uint32_t* map, uint64_t n_regions,
+                        uint32_t* n_packed)
+{
+    if (!ctx || !map || !n_packed) return fail(ctx, XRT_ERR_ARGUMENT, "NULL argument");
+    const uint32_t rx = (width + kRegion - 1) / kRegion, ry = (rows + kRegion - 1) / kRegion;
+    if (n_regions != (uint64_t)rx * ry)
+        return fail(ctx, XRT_ERR_ARGUMENT, "map must hold ceil(width/32) x ceil(rows/32) regions");
+    const bool planned = ctx->last_fill_regions > 0 && ctx->plan_valid && ctx->plan_rx == rx &&
+                         ctx->plan_ry == ry && ctx->h_plan_region.size() == n_regions;
+    if (!planned) {                                 // every region travels
+        for (uint64_t r = 0; r < n_regions; ++r) map[r] = (uint32_t)r;
+        *n_packed = (uint32_t)n_regions;
+        return XRT_OK;
+    }
+    for (uint64_t s = 0; s < n_regions; ++s)
+        map[ctx->h_plan_region[s]] = s < ctx->plan_tile_slots ? (uint32_t)s : kEmpty;
+    *n_packed = ctx->plan_tile_slots;
+    return XRT_OK;
+}
+
+int xrt_pack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
+                            const float* d_lbuffer, float* d_packed, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    const uint32_t rx = (width + kRegion - 1) / kRegion, ry = (rows + kRegion - 1) / kRegion;
+    if (!rx || !ry) return XRT_OK;
+    if (!d_map || !d_lbuffer || !d_packed) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    if (reinterpret_cast<uintptr_t>(d_packed) & 15u) return fail(ctx, XRT_ERR_ARGUMENT, "packed buffer not 16-B aligned");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_pack_regions, dim3(rx * ry), dim3(256), 0, (hipStream_t)stream, d_lbuffer, d_packed, d_map,
+                       width, rows, rx);
+    XRT_HIP(ctx, hipGetLastError());
+    return XRT_OK;
+}
+
+int xrt_unpack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
+                              const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    const uint32_t rx = (width + kRegion - 1) / kRegion, ry = (rows + kRegion - 1) / kRegion;
+    if (!rx || !ry) return XRT_OK;
+    if (!d_map || !d_packed) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    if (reinterpret_cast<uintptr_t>(d_packed) & 15u) return fail(ctx, XRT_ERR_ARGUMENT, "packed buffer not 16-B aligned");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_unpack_regions, dim3(rx * ry), dim3(256), 0, (hipStream_t)stream, d_packed, d_map,
+                       d_lbuffer, d_image, d_u8, width, rows, rx);
+    XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
 

@@ -679,17 +679,56 @@ def test_transit_expand_equals_direct_render(ctx, dragon, soup):
     assert np.array_equal(u8.cpu().numpy(), ref[2])
 
 
-def test_bench_strips_two_ranks_one_gpu(tmp_path):
-    """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0,
-    expanded there) with 2 ranks on the one GPU (gloo, host-staged): the
-    gathered frame is bit-equal to rank 0's single-device render."""
+@pytest.mark.parametrize("W,H,r0,r1", [(1000, 700, 0, 700), (2048, 2048, 1024, 2048), (333, 517, 100, 400)])
+def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
+    """A transit L-buffer strip packed by its fill plan (only the regions the
+    plan did not fill travel) and unpacked into the three planes equals the
+    direct render of the strip; the packed size is the unfilled regions'."""
+    import torch
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    ctx.upload_mesh(dragon)
+    ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+    ref = ctx.render_rows(cam, r0, r1)
+    rows = r1 - r0
+    dev = torch.device("cuda", ctx.device)
+    stream = torch.cuda.current_stream(dev)
+    lb = torch.full((W * rows,), -1.0, device=dev)
+    ctx.set_miss_code(xrt._abi.XRT_MISS_TRANSIT)
+    try:
+        ctx.render_rows_device(cam, r0, r1, 0, lb.data_ptr(), 0, stream.cuda_stream)
+        rmap, n_packed = ctx.plan_region_map(W, rows)
+        n_fill = ctx.fill_regions()
+    finally:
+        ctx.set_miss_code(0)
+    assert 0 < n_fill and n_packed == len(rmap) - n_fill
+    assert np.count_nonzero(rmap == 0xFFFFFFFF) == n_fill
+    assert sorted(rmap[rmap != 0xFFFFFFFF].tolist()) == list(range(n_packed))
+    d_map = torch.from_numpy(rmap.view(np.int32)).to(dev)
+    packed = torch.zeros(n_packed * 1024, device=dev)
+    ctx.pack_regions_device(W, rows, d_map.data_ptr(), lb.data_ptr(), packed.data_ptr(), stream.cuda_stream)
+    out = [torch.full((W * rows,), -2.0, device=dev), torch.zeros(W * rows, device=dev),
+           torch.zeros(W * rows, dtype=torch.uint8, device=dev)]
+    ctx.unpack_regions_device(W, rows, d_map.data_ptr(), packed.data_ptr(), out[0].data_ptr(), out[1].data_ptr(),
+                              out[2].data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert np.array_equal(bits(out[1].cpu().numpy()), bits(ref[0]))
+    assert np.array_equal(bits(out[0].cpu().numpy()), bits(ref[1]))
+    assert np.array_equal(out[2].cpu().numpy(), ref[2])
+
+
+@pytest.mark.parametrize("transit", ["packed", "dense"])
+def test_bench_strips_two_ranks_one_gpu(tmp_path, transit):
+    """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
+    packed by region or dense --, expanded there) with 2 ranks on the one GPU
+    (gloo, host-staged): the gathered frame is bit-equal to rank 0's
+    single-device render."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    port = 29500 + (os.getpid() % 1000)
+    port = 29500 + (os.getpid() % 1000) + (7 if transit == "dense" else 0)
     cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
-           "--steps", "4", "--warmup", "1"]
+           "--steps", "4", "--warmup", "1", "--transit", transit, "--kernel", "binned"]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
     if r.returncode != 0:
         print(r.stderr[-6000:])
@@ -698,6 +737,11 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path):
     d = json.loads(line)
     assert d["config"]["mode"] == "strips" and d["n_gpus"] == 2
     assert d["gather_check"]["bit_exact_vs_single_device_frame"] is True
+    g = d["gather_check"]
+    if transit == "packed":
+        assert g["bytes_gathered_per_step"] < g["dense_bytes_per_step"]
+    else:
+        assert g["bytes_gathered_per_step"] == g["dense_bytes_per_step"]
 
 
 def test_cli_multi_gpu_golden_text(tmp_path):
