@@ -650,6 +650,10 @@ constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
 #ifndef XRT_GLOBAL_REGIONS
 #define XRT_GLOBAL_REGIONS 4096
 #endif
+#ifndef XRT_GLOBAL_REGIONS_UNBOUNDED
+#define XRT_GLOBAL_REGIONS_UNBOUNDED 65536
+#endif
+constexpr uint32_t kGlobalRegionsUnbounded = XRT_GLOBAL_REGIONS_UNBOUNDED;
 constexpr uint32_t kGlobalRegions = XRT_GLOBAL_REGIONS;   // footprints over more regions go to the global list
 
 // Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
@@ -934,6 +938,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     c.e0 = make_float4(0.0f, 0.0f, kInf, 0.0f);
     c.e1 = c.e0;
     c.e2 = c.e0;
+    c.e2.w = kInf;     // the regions the footprint reaches: unknown (bin_rect)
 
     bool finite = isfinite(r.tnum) && isfinite(r.qvx) && isfinite(r.qvy) && isfinite(r.qvz);
     if (finite && r.tnum == 0.0f) {
@@ -1004,7 +1009,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
             if (s * alpha + M < 0.0) {
                 c.bbox = make_float4(kInf, -kInf, kInf, -kInf);
                 c.e0 = make_float4(0.0f, 0.0f, -kInf, 0.0f);
-                c.e1 = c.e2 = make_float4(0.0f, 0.0f, kInf, 0.0f);
+                c.e1 = c.e2 = make_float4(0.0f, 0.0f, kInf, kInf);
                 return c;
             }
             ea[k] = 0.0f;
@@ -1023,7 +1028,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     }
     c.e0 = make_float4(ea[0], eb[0], ec[0], 0.0f);
     c.e1 = make_float4(ea[1], eb[1], ec[1], 0.0f);
-    c.e2 = make_float4(ea[2], eb[2], ec[2], 0.0f);
+    c.e2 = make_float4(ea[2], eb[2], ec[2], kInf);
 
     if (!constant_edge) {
         // Loosened triangle {a_k x + b_k y + c_k >= 0}: bounded iff the inward
@@ -1048,9 +1053,18 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
             double ymin = fmin(vy[0], fmin(vy[1], vy[2])), ymax = fmax(vy[0], fmax(vy[1], vy[2]));
             double sx = 0.01 + 1e-4 * (fabs(xmin) + fabs(xmax));
             double sy = 0.01 + 1e-4 * (fabs(ymin) + fabs(ymax));
-            if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax))
+            if (isfinite(xmin) && isfinite(xmax) && isfinite(ymin) && isfinite(ymax)) {
                 c.bbox = make_float4((float)(xmin - sx), (float)(xmax + sx), (float)(ymin - sy),
                                      (float)(ymax + sy));
+                // Regions the loosened triangle can touch, by its size rather than
+                // its box (a sliver's box is far larger): area / 32^2 + perimeter / 32
+                // + the corners' cells (bin_rect's global-list choice).
+                const double area = 0.5 * fabs((vx[1] - vx[0]) * (vy[2] - vy[0]) - (vx[2] - vx[0]) * (vy[1] - vy[0]));
+                double perim = 0.0;
+                for (int q = 0; q < 3; ++q)
+                    perim += sqrt((vx[pj[q]] - vx[q]) * (vx[pj[q]] - vx[q]) + (vy[pj[q]] - vy[q]) * (vy[pj[q]] - vy[q]));
+                c.e2.w = (float)(area / (kRegion * kRegion) + 2.0 * perim / kRegion + 8.0);
+            }
         } else {
             clipped_box(A, Bq, Cq, cp.width, cp.height, c.bbox);
         }
@@ -1166,13 +1180,20 @@ __device__ __forceinline__ bool footprint_regions(float4 bb, const RenderParams&
 
 // Region rectangle of a footprint; false when the triangle is in no region
 // list (no region, or in the global list -- `global` tells which).
-__device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const BinBuffers& bins,
+__device__ __forceinline__ bool bin_rect(float4 bb, float reach, const RenderParams& p, const BinBuffers& bins,
                                          uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1,
                                          bool& global)
 {
     global = false;
     if (!footprint_regions(bb, p, bins, x0, x1, y0, y1)) return false;
-    if ((uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1) > kGlobalRegions) {
+    // Past kGlobalRegions regions a footprint goes to the global list (every
+    // region's candidate) -- unless the loosened triangle itself reaches few
+    // regions (`reach`, compute_footprint: a sliver, whose box is much larger
+    // than it), which are found by walking its box, up to
+    // kGlobalRegionsUnbounded cells.  In the global list a sliver would leave
+    // no region empty (no fill plan) and cost every region a staged candidate.
+    const uint64_t cells = (uint64_t)(x1 - x0 + 1) * (y1 - y0 + 1);
+    if (cells > kGlobalRegions && (cells > kGlobalRegionsUnbounded || !(reach <= (float)kGlobalRegions))) {
         global = true;
         return false;
     }
@@ -1189,6 +1210,11 @@ __device__ __forceinline__ bool bin_rect(float4 bb, const RenderParams& p, const
 // on all four SIMDs of a CU at once).
 constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
 constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
+#ifndef XRT_PREP_TRIS
+#define XRT_PREP_TRIS 32
+#endif
+constexpr uint32_t kPrepTris = XRT_PREP_TRIS;     // triangles per k_prep wave (1..64)
+static_assert(kPrepTris >= 1u && kPrepTris <= 64u, "kPrepTris");
 
 #ifndef XRT_PREP_MAX_VGPR
 #define XRT_PREP_MAX_VGPR 0     // A/B: cap k_prep's VGPRs (0 = the compiler's choice)
@@ -1209,8 +1235,13 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     // The preparation of frame N+1 shares the CUs with frame N's render (prep
     // stream): top wave priority keeps this latency-bound chain short.
     XRT_PREP_PRIO();
+    // i: the thread's index over the grid (pixel-offset tables, counter
+    // clears); tri: its triangle -- kPrepTris per wave (fewer than 64 spreads
+    // the binning's cells and commits of a frame over more waves).
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < T;
+    const uint32_t tri_lane = threadIdx.x & 63u;
+    const uint32_t tri = (blockIdx.x * kPrepWaves + (threadIdx.x >> 6)) * kPrepTris + tri_lane;
+    const bool valid = tri_lane < kPrepTris && tri < T;
     if (i == 0 && frame_out) *frame_out = p;       // the render's make_ray reads it (Outputs::frame)
     if (offsets_out) {                             // v_off of every row, then u_off of every column
         if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
@@ -1220,7 +1251,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     Footprint fp;
     TriRec r = {};
     if (valid) {
-        const float* P = tris + 9ull * i;
+        const float* P = tris + 9ull * tri;
         float p1x = P[0], p1y = P[1], p1z = P[2];
         float p2x = P[3], p2y = P[4], p2z = P[5];
         float p3x = P[6], p3y = P[7], p3z = P[8];
@@ -1242,14 +1273,14 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
             r.pad1 = ny / len;
             r.pad2 = nz / len;
         }
-        recs[i] = r;
+        recs[tri] = r;
         if (culls) {
             fp = compute_footprint(r, p, cp);
-            culls[i] = fp.bbox;
-            culls[(size_t)T + i] = fp.e0;
-            culls[2 * (size_t)T + i] = fp.e1;
-            culls[3 * (size_t)T + i] = fp.e2;
-            fp.e0.w = __uint_as_float(i);          // the region entries carry the id (make_entry's layout)
+            culls[tri] = fp.bbox;
+            culls[(size_t)T + tri] = fp.e0;
+            culls[2 * (size_t)T + tri] = fp.e1;
+            culls[3 * (size_t)T + tri] = fp.e2;
+            fp.e0.w = __uint_as_float(tri);          // the region entries carry the id (make_entry's layout)
         }
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
@@ -1276,7 +1307,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
-    const bool has = valid && bin_rect(fp.bbox, p, bins, x0, x1, y0, y1, global);
+    const bool has = valid && bin_rect(fp.bbox, fp.e2.w, p, bins, x0, x1, y0, y1, global);
     if (valid && global) {                         // footprint over > kGlobalRegions regions
         if (bins.plan_miss) *bins.plan_miss = 1u;  // the plan assumed an empty global list
         RegionEntry* e = bins.global_list + atomicAdd(&bs->global_count, 1u);

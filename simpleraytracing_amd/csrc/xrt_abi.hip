@@ -363,10 +363,12 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                 unsigned flags)
 {
     const uint64_t T = ctx->num_tris;
-    const uint64_t threads =
-        std::max<uint64_t>(std::max<uint64_t>(T, (uint64_t)p.height + p.width), bins.clear ? bins.clear_regions : 0u);
+    // kPrepTris triangles per wave; every thread covers a pixel-offset entry / counter
+    const uint64_t threads = std::max<uint64_t>((uint64_t)p.height + p.width, bins.clear ? bins.clear_regions : 0u);
+    const uint64_t blocks = std::max<uint64_t>((T + kPrepWaves * kPrepTris - 1) / (kPrepWaves * kPrepTris),
+                                               (threads + kPrepThreads - 1) / kPrepThreads);
     const auto t_launch = HostClock::now();
-    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)((threads + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads),
+    hipExtLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(kPrepThreads),
                           0, stream, nullptr, done, flags,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
@@ -1422,7 +1424,8 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     p.model = ctx->model;
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepThreads - 1) / kPrepThreads)), dim3(kPrepThreads), 0, 0, ctx->d_tris,
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepWaves * kPrepTris - 1) / (kPrepWaves * kPrepTris))),
+                       dim3(kPrepThreads), 0, 0, ctx->d_tris,
                        (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)

@@ -60,7 +60,8 @@ def main():
     assert L.xrt_debug_stamps(ctx, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n) == 0
     L.xrt_destroy(ctx)
     prep_threads = int(os.environ.get("XRT_PREP_THREADS", "64"))
-    nwg = (max(len(tris), W + H) + prep_threads - 1) // prep_threads
+    prep_tris = int(os.environ.get("XRT_PREP_TRIS", "32"))      # the stamps build's -DXRT_PREP_TRIS
+    nwg = max((len(tris) + prep_tris - 1) // prep_tris, (W + H + prep_threads - 1) // prep_threads)
     prep = st[:8 * nwg].reshape(nwg, 8).astype(np.int64)
     t0 = prep[:, 0].min()
     rel = lambda x: (x - t0) * TICK_US  # noqa: E731
