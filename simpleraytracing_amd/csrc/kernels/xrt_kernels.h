@@ -656,11 +656,21 @@ constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
 constexpr uint32_t kGlobalRegionsUnbounded = XRT_GLOBAL_REGIONS_UNBOUNDED;
 constexpr uint32_t kGlobalRegions = XRT_GLOBAL_REGIONS;   // footprints over more regions go to the global list
 
-// Max over the rectangle [xc-hx, xc+hx] x [yc-hy, yc+hy] of one relaxed edge
-// function a*col + b*row + c.
-__device__ __forceinline__ float edge_max(float4 e, float xc, float yc, float hx, float hy)
+// Relaxed edge functions are stored as (a, b, c_t) with c_t = c + kTileHalf *
+// (|a| + |b|) rounded up (compute_footprint): the edge's maximum over an 8x8
+// tile's pixel-centre square [xc +- 3.5] x [yc +- 3.5] is a*xc + b*yc + c_t --
+// two FMAs per edge for the render's per-candidate tile test.  Over a 32x32
+// region's square (+- 15.5) it is 12 more half-widths.  (Conservative: c_t is
+// not below the exact value, and the margin in c covers the f32 evaluation,
+// DESIGN.md "Tile cull", step 5.)
+constexpr float kTileHalf = 3.5f;
+__device__ __forceinline__ float edge_tile(float4 e, float xc, float yc)
 {
-    return (e.x * xc + e.y * yc) + (e.z + (fabsf(e.x) * hx + fabsf(e.y) * hy));
+    return __builtin_fmaf(e.x, xc, __builtin_fmaf(e.y, yc, e.z));
+}
+__device__ __forceinline__ float edge_region(float4 e, float xc, float yc)
+{
+    return __builtin_fmaf(e.x, xc, __builtin_fmaf(e.y, yc, e.z)) + (15.5f - kTileHalf) * (fabsf(e.x) + fabsf(e.y));
 }
 
 // Footprint box (xmin, xmax, ymin, ymax) against the pixel-centre rectangle
@@ -673,18 +683,16 @@ __device__ __forceinline__ bool box_overlaps(float4 bb, float x0, float x1, floa
 // All three edges evaluated, combined with `&` (not `&&`): a short-circuit
 // lets the compiler sink each edge's load behind the previous edge's compare,
 // three dependent memory round trips per candidate chunk instead of one.
-__device__ __forceinline__ bool edges_pass(float4 e0, float4 e1, float4 e2, float xc, float yc,
-                                           float hx, float hy)
+// (xc, yc): the centre of an 8x8 tile.
+__device__ __forceinline__ bool edges_pass_tile(float4 e0, float4 e1, float4 e2, float xc, float yc)
 {
-    return (edge_max(e0, xc, yc, hx, hy) >= 0.0f) & (edge_max(e1, xc, yc, hx, hy) >= 0.0f) &
-           (edge_max(e2, xc, yc, hx, hy) >= 0.0f);
+    return (edge_tile(e0, xc, yc) >= 0.0f) & (edge_tile(e1, xc, yc) >= 0.0f) & (edge_tile(e2, xc, yc) >= 0.0f);
 }
-
-__device__ __forceinline__ bool edge_pass(const float4* __restrict__ culls, uint32_t T, uint32_t j,
-                                          float xc, float yc, float hx, float hy)
+// (xc, yc): the centre of a 32x32 region.
+__device__ __forceinline__ bool edges_pass_region(float4 e0, float4 e1, float4 e2, float xc, float yc)
 {
-    return edges_pass(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j], xc,
-                      yc, hx, hy);
+    return (edge_region(e0, xc, yc) >= 0.0f) & (edge_region(e1, xc, yc) >= 0.0f) &
+           (edge_region(e2, xc, yc) >= 0.0f);
 }
 
 // Phase 2, shared by the tiled and binned kernels.
@@ -742,7 +750,7 @@ __device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t cou
     uint32_t tests = 0;
     for (uint32_t base = 0; base < count; base += 64u) {
         const uint32_t k = base + lane;
-        const bool pass = k < count && edges_pass(st.e0[k], st.e1[k], st.e2[k], xc, yc, 3.5f, 3.5f);
+        const bool pass = k < count && edges_pass_tile(st.e0[k], st.e1[k], st.e2[k], xc, yc);
         unsigned long long m = __ballot(pass);
         tests += (uint32_t)__popcll(m);
         if (ablate & kAblateExact) m = 0ull;
@@ -994,6 +1002,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     double cu = ps * (0.5 - cp.width / 2.0);
 
     float ea[3], eb[3], ec[3];
+    double c_edge[3] = {0.0, 0.0, 0.0};   // the constants before the tile half-width (the box below)
     bool constant_edge = false;
     for (int k = 0; k < 3; ++k) {
         double upn = dot_d(Up, N[k]);
@@ -1024,7 +1033,9 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
         cc += 0.05 + 64.0 * kEps * (cp.width + cp.height + fabs(cc));
         ea[k] = (float)a;
         eb[k] = (float)b;
-        ec[k] = (float)cc;
+        c_edge[k] = (double)(float)cc;
+        // stored with an 8x8 tile's half-width folded in (edge_tile), rounded up
+        ec[k] = __double2float_ru(cc + (double)kTileHalf * (fabs((double)ea[k]) + fabs((double)eb[k])));
     }
     c.e0 = make_float4(ea[0], eb[0], ec[0], 0.0f);
     c.e1 = make_float4(ea[1], eb[1], ec[1], 0.0f);
@@ -1033,7 +1044,7 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     if (!constant_edge) {
         // Loosened triangle {a_k x + b_k y + c_k >= 0}: bounded iff the inward
         // normals positively span the plane (cross products share a sign).
-        double A[3] = {ea[0], ea[1], ea[2]}, Bq[3] = {eb[0], eb[1], eb[2]}, Cq[3] = {ec[0], ec[1], ec[2]};
+        double A[3] = {ea[0], ea[1], ea[2]}, Bq[3] = {eb[0], eb[1], eb[2]}, Cq[3] = {c_edge[0], c_edge[1], c_edge[2]};
         double x01 = A[0] * Bq[1] - A[1] * Bq[0];
         double x12 = A[1] * Bq[2] - A[2] * Bq[1];
         double x20 = A[2] * Bq[0] - A[0] * Bq[2];
@@ -1407,7 +1418,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     auto cell_pass = [&](uint32_t owner, uint32_t rx, uint32_t ry) {
         const float xc = (float)(rx * kRegion) + 15.5f;
         const float yc = (float)(p.row_begin + ry * kRegion) + 15.5f;
-        return edges_pass(s_fp[wave][0][owner], s_fp[wave][1][owner], s_fp[wave][2][owner], xc, yc, 15.5f, 15.5f);
+        return edges_pass_region(s_fp[wave][0][owner], s_fp[wave][1][owner], s_fp[wave][2][owner], xc, yc);
     };
     // (1a) small rectangles, flattened over the wave
     for (uint32_t base = 0; base < total; base += 64u) {
@@ -1631,7 +1642,7 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
             const uint32_t k = k0 + lane;
             bool pass = false;
             if (k < cnt)
-                pass = edges_pass(st.q[0][k], st.q[1][k], st.q[2][k], xc, yc, 3.5f, 3.5f) &
+                pass = edges_pass_tile(st.q[0][k], st.q[1][k], st.q[2][k], xc, yc) &
                        box_overlaps(st.q[3][k], fx0, fx1, fy0, fy1);
             unsigned long long m = __ballot(pass);
             if (!m) continue;
