@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--transit", choices=["packed", "dense"], default="packed",
                     help="strips mode: send the regions the strip's fill plan did not fill (packed) or the "
                          "whole L-buffer strip (dense)")
+    ap.add_argument("--root-share", default="auto",
+                    help="strips mode: fraction of the rows rank 0 renders ('auto': strips.root_share, "
+                         "'equal': H/N each as the reference's row partition)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses device 0 (with --dist-backend gloo)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -185,7 +188,7 @@ def main():
 
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.scenes import tiled_mesh
-    from simpleraytracing_amd.strips import strip_bounds
+    from simpleraytracing_amd.strips import root_share, strip_bounds, unpack_descriptors, weighted_bounds
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -214,8 +217,15 @@ def main():
     cam = xrt.camera_for_mesh(tris, W, H)
     strips = mode == "strips"
     gathering = strips and world > 1
-    r0, r1 = strip_bounds(H, world, rank) if strips else (0, H)
-    bounds = [strip_bounds(H, world, g) for g in range(world)]
+    # Row strips.  The root's own rows need no transfer: by default it renders a
+    # larger first strip (strips.root_share), the others split the rest.
+    if args.root_share == "equal" or not strips:
+        share0 = None
+        bounds = [strip_bounds(H, world, g) for g in range(world)]
+    else:
+        share0 = root_share(world) if args.root_share == "auto" else float(args.root_share)
+        bounds = [weighted_bounds(H, world, g, share0) for g in range(world)]
+    r0, r1 = bounds[rank] if strips else (0, H)
 
     ctx = xrt.Context(device_index)
     ctx.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
@@ -261,7 +271,8 @@ def main():
             dist.send(meta.to(dev) if nccl else meta, dst=0)
             dist.send(d_map if nccl else d_map.cpu(), dst=0)
         else:
-            peer = {}
+            # every sender's blocks back to back in one buffer, one unpack launch
+            maps, counts = [], []
             for g, (b, e) in enumerate(bounds):
                 if not g:
                     continue
@@ -270,8 +281,13 @@ def main():
                 n_regions = -(-W // 32) * -(-(e - b) // 32)
                 m = torch.zeros(n_regions, dtype=torch.int32, device=dev if nccl else "cpu")
                 dist.recv(m, src=g)
-                npk = int(meta.item())
-                peer[g] = (m.to(dev), npk, torch.zeros(max(npk, 1) * 1024, dtype=torch.float32, device=dev))
+                maps.append(m.cpu().numpy().view(np.uint32))
+                counts.append(int(meta.item()))
+            desc, bases, total = unpack_descriptors(W, bounds[1:], maps)
+            d_desc = torch.from_numpy(desc.reshape(-1).view(np.int32)).to(dev)
+            n_desc = len(desc)
+            rbuf = torch.zeros(max(total, 1) * 1024, dtype=torch.float32, device=dev)
+            segs = {g + 1: rbuf[bases[g] * 1024:(bases[g] + max(counts[g], 1)) * 1024] for g in range(world - 1)}
 
     def send_strip(t):
         if nccl:
@@ -279,26 +295,29 @@ def main():
         dist.send(t.cpu(), dst=0)             # gloo rehearsal: staged through the host
         return None
 
-    def recv_strips():
-        if packed:
-            bufs = {g: peer[g][2][:max(peer[g][1], 1) * 1024] for g in peer}
-        else:
-            bufs = {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
+    def post_recvs():
+        """RCCL: the frame's receives, posted before the root renders its own strip."""
+        if not nccl:
+            return None
+        bufs = segs if packed else {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
+        return dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, g) for g, t in bufs.items()])
+
+    def finish_recvs(works):
         if nccl:
-            ops = [dist.P2POp(dist.irecv, t, g) for g, t in bufs.items()]
-            for w in dist.batch_isend_irecv(ops):
+            for w in works:
                 w.wait()                      # the current stream waits for the receives
-        else:
+        else:                                 # gloo rehearsal: staged through the host
+            bufs = segs if packed else {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
             for g, t in bufs.items():
                 host = torch.empty(t.numel(), dtype=torch.float32)
                 dist.recv(host, src=g)
                 t.copy_(host, non_blocking=False)
         if packed:
-            for g, (b, e) in enumerate(bounds):
-                if g:
-                    d_map, _, buf = peer[g]
-                    ctx.unpack_regions_device(W, e - b, d_map.data_ptr(), buf.data_ptr(), lb.data_ptr() + 4 * b * W,
-                                              img.data_ptr() + 4 * b * W, u8.data_ptr() + b * W, stream.cuda_stream)
+            ctx.unpack_blocks_device(W, n_desc, d_desc.data_ptr(), rbuf.data_ptr(), lb.data_ptr(), img.data_ptr(),
+                                     u8.data_ptr(), stream.cuda_stream)
+        else:
+            ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0, u8.data_ptr() + o0,
+                                   stream.cuda_stream)
 
     def step():
         k = frame_no[0]
@@ -308,13 +327,11 @@ def main():
             ctx.hole_fill_device(W, H, lb.data_ptr(), img.data_ptr(), u8.data_ptr(), stream.cuda_stream)
         elif root:
             o = r0 * W
+            works = post_recvs() if gathering else None
             ctx.render_rows_device(cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
                                    u8.data_ptr() + o, stream.cuda_stream)
             if gathering:
-                recv_strips()
-                if not packed:
-                    ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0,
-                                           u8.data_ptr() + o0, stream.cuda_stream)
+                finish_recvs(works)
         else:
             b = k % 2
             if pending[b] is not None:
@@ -363,12 +380,13 @@ def main():
         ok = (np.array_equal(img.cpu().numpy().view(np.uint32), full[0].view(np.uint32))
               and np.array_equal(lb.cpu().numpy().view(np.uint32), full[1].view(np.uint32))
               and np.array_equal(u8.cpu().numpy(), full[2]))
-        moved = sum(4096 * max(v[1], 1) for v in peer.values()) if packed else 4 * rest
+        moved = 4096 * sum(max(c, 1) for c in counts) if packed else 4 * rest
         gather = {"bit_exact_vs_single_device_frame": bool(ok),
                   "bytes_gathered_per_step": moved, "dense_bytes_per_step": 4 * rest,
                   "transit": ("L-buffer strips, misses as XRT_MISS_TRANSIT, packed by region (the regions "
                               "each strip's fill plan filled stay behind)") if packed
-                  else "L-buffer strips, misses as XRT_MISS_TRANSIT"}
+                  else "L-buffer strips, misses as XRT_MISS_TRANSIT",
+                  "strip_rows": [e - b for b, e in bounds], "root_share": share0}
 
     result = None
     if rank == 0:

@@ -392,6 +392,14 @@ int xrt_pack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, con
                             const float* d_lbuffer, float* d_packed, void* stream);
 int xrt_unpack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
                               const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
+/*
+ * Many strips' packed regions in one launch: d_desc holds 4 u32 per block --
+ * first frame row, rows of the block inside its strip (<= 32), first column,
+ * packed block index in d_packed (0xFFFFFFFF: a filled region, all misses).
+ * The planes are whole frames (row-major, `width` columns).  16-B aligned.
+ */
+int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
+                             const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
 
 /* Diagnostics: regions the last enqueued BINNED frame rendered through the fill plan. */
 int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);

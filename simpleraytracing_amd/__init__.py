@@ -281,6 +281,13 @@ class Context:
                                                         d_image or None, d_u8 or None, stream or None),
                     "xrt_unpack_regions_device")
 
+    def unpack_blocks_device(self, width: int, n_blocks: int, d_desc: int, d_packed: int, d_lbuffer: int,
+                             d_image: int, d_u8: int, stream: int = 0):
+        """Many strips' packed regions into whole-frame planes in one launch (see xrt.h)."""
+        self._check(self._lib.xrt_unpack_blocks_device(self._ctx, width, n_blocks, d_desc, d_packed,
+                                                       d_lbuffer or None, d_image or None, d_u8 or None,
+                                                       stream or None), "xrt_unpack_blocks_device")
+
     def timing_begin(self):
         self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
 

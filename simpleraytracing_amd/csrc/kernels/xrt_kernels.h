@@ -1873,6 +1873,42 @@ __global__ __launch_bounds__(256) void k_pack_regions(const float* __restrict__ 
     *reinterpret_cast<float4*>(packed + (size_t)slot * kPackBlock + 4u * threadIdx.x) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// One block of the receiving side: 4 pixels of a 32x32 block (thread t: row
+// t / 8, columns 4 (t % 8) ..) from `v` into the planes at frame row `row`.
+__device__ __forceinline__ void unpack_pixels(float4 v, uint32_t row, uint32_t col, uint32_t width,
+                                              float* __restrict__ lbuffer, float* __restrict__ image,
+                                              uint8_t* __restrict__ image_u8)
+{
+    const float l[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (col + k >= width) break;
+        const bool miss = __float_as_uint(l[k]) == kMissTransit;
+        const float img = miss ? 80.0f : shade(l[k]);
+        const size_t o = (size_t)row * width + col + k;
+        if (image) image[o] = img;
+        if (image_u8) image_u8[o] = miss ? (uint8_t)255u : lut_u8(img);
+        if (lbuffer) lbuffer[o] = miss ? __builtin_inff() : l[k];
+    }
+}
+
+// Many strips' packed regions in one launch (the gather's root): block b is
+// described by desc[b] = (first frame row, rows of it in its strip, first
+// column, packed block index or kEmpty for a filled region).
+__global__ __launch_bounds__(256) void k_unpack_blocks(const float* __restrict__ packed,
+                                                       const uint4* __restrict__ desc,
+                                                       float* __restrict__ lbuffer, float* __restrict__ image,
+                                                       uint8_t* __restrict__ image_u8, uint32_t width)
+{
+    const uint4 d = desc[blockIdx.x];
+    const uint32_t r = threadIdx.x / 8u;
+    if (r >= d.y) return;
+    float4 v = make_float4(__uint_as_float(kMissTransit), __uint_as_float(kMissTransit),
+                           __uint_as_float(kMissTransit), __uint_as_float(kMissTransit));
+    if (d.w != kEmpty) v = *reinterpret_cast<const float4*>(packed + (size_t)d.w * kPackBlock + 4u * threadIdx.x);
+    unpack_pixels(v, d.x + r, d.z + 4u * (threadIdx.x % 8u), width, lbuffer, image, image_u8);
+}
+
 // The receiving side: a packed strip into the frame's three planes (k_expand's
 // values: misses -- kMissTransit, or a filled region -- give image 80, u8 255,
 // L +inf; hits the shade of L and its LUT).
@@ -1890,17 +1926,7 @@ __global__ __launch_bounds__(256) void k_unpack_regions(const float* __restrict_
     float4 v = make_float4(__uint_as_float(kMissTransit), __uint_as_float(kMissTransit),
                            __uint_as_float(kMissTransit), __uint_as_float(kMissTransit));
     if (slot != kEmpty) v = *reinterpret_cast<const float4*>(packed + (size_t)slot * kPackBlock + 4u * threadIdx.x);
-    const float l[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        if (col + k >= width) break;
-        const bool miss = __float_as_uint(l[k]) == kMissTransit;
-        const float img = miss ? 80.0f : shade(l[k]);
-        const size_t o = (size_t)row * width + col + k;
-        if (image) image[o] = img;
-        if (image_u8) image_u8[o] = miss ? (uint8_t)255u : lut_u8(img);
-        if (lbuffer) lbuffer[o] = miss ? __builtin_inff() : l[k];
-    }
+    unpack_pixels(v, row, col, width, lbuffer, image, image_u8);
 }
 
 // ---------------------------------------------------------------------------

@@ -1193,6 +1193,22 @@ int xrt_unpack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, c
     return XRT_OK;
 }
 
+int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
+                             const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (!n_blocks) return XRT_OK;
+    if (!d_desc || !d_packed) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    if (n_blocks > 0x7FFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many blocks");
+    if ((reinterpret_cast<uintptr_t>(d_packed) | reinterpret_cast<uintptr_t>(d_desc)) & 15u)
+        return fail(ctx, XRT_ERR_ARGUMENT, "packed buffer or descriptors not 16-B aligned");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_unpack_blocks, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream, d_packed,
+                       reinterpret_cast<const uint4*>(d_desc), d_lbuffer, d_image, d_u8, width);
+    XRT_HIP(ctx, hipGetLastError());
+    return XRT_OK;
+}
+
 int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions)
 {
     if (!ctx || !regions) return XRT_ERR_ARGUMENT;

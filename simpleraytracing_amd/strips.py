@@ -24,6 +24,64 @@ def strip_bounds(height: int, n: int, rank: int):
     return begin, end
 
 
+def root_share(n: int, rho: float = 2.5) -> float:
+    """Fraction of the rows the gather's root renders itself.  Its rows need no
+    transfer, the others' do: with rho = (transfer time / render time) per row of
+    a sender's strip, the steps balance when the root takes rho / (rho + n - 1)
+    (never less than 1/n).  rho = 2.5: a packed 4096-px row (~7.4 KB) over one
+    xGMI link against ~27 ns of render per row (DESIGN.md "Multi-GPU")."""
+    if n <= 1:
+        return 1.0
+    return max(1.0 / n, rho / (rho + n - 1))
+
+
+def weighted_bounds(height: int, n: int, rank: int, share0: float):
+    """[begin, end) rows of rank `rank`: rank 0 renders the first
+    round(share0 * height) rows (at least its equal share, at most all but one
+    row per other rank), the others split the rest as strip_bounds does."""
+    if not 0 <= rank < n:
+        raise ValueError("rank out of range")
+    if n == 1:
+        return 0, height
+    r0 = int(round(share0 * height))
+    r0 = min(max(r0, -(-height // n)), height - (n - 1))
+    if rank == 0:
+        return 0, r0
+    b, e = strip_bounds(height - r0, n - 1, rank - 1)
+    return r0 + b, r0 + e
+
+
+EMPTY = 0xFFFFFFFF
+
+
+def unpack_descriptors(width: int, spans, maps):
+    """Descriptors of xrt_unpack_blocks_device for the packed strips of `spans`
+    ([begin, end) rows) with region maps `maps` (xrt_plan_region_map, one per
+    strip): one (first row, rows, first column, block) per 32x32 region, the
+    strips' packed blocks back to back in one buffer (at least one per strip:
+    a strip with no unfilled region still sends one).  Returns (desc as an
+    (n, 4) uint32 array, first block of each strip, total blocks)."""
+    rows_out, bases, base = [], [], 0
+    rx = -(-width // 32)
+    for (b, e), m in zip(spans, maps):
+        m = np.asarray(m, np.uint32)
+        ry = -(-(e - b) // 32)
+        if m.size != rx * ry:
+            raise ValueError("region map does not match the strip")
+        r = np.arange(m.size, dtype=np.uint64)
+        y, x = r // rx, r % rx
+        d = np.empty((m.size, 4), np.uint32)
+        d[:, 0] = b + 32 * y
+        d[:, 1] = np.minimum(32, (e - b) - 32 * y)
+        d[:, 2] = 32 * x
+        d[:, 3] = np.where(m == EMPTY, EMPTY, m.astype(np.uint64) + base).astype(np.uint32)
+        rows_out.append(d)
+        bases.append(base)
+        base += max(int(np.count_nonzero(m != EMPTY)), 1)     # a strip with none still sends one block
+    desc = np.concatenate(rows_out) if rows_out else np.zeros((0, 4), np.uint32)
+    return desc, bases, base
+
+
 def max_strip_pixels(width: int, height: int, n: int) -> int:
     b, e = strip_bounds(height, n, 0)
     return (e - b) * width

@@ -14,6 +14,52 @@ from simpleraytracing_amd.strips import assemble, packed_size, strip_bounds, vie
 from conftest import DRAGON, ROOT
 
 
+def test_weighted_bounds_cover_image():
+    """Root-weighted strips (bench.py --root-share): contiguous, covering, rank 0
+    first with at least its equal share, the others within one row of each other."""
+    from simpleraytracing_amd.strips import root_share, weighted_bounds
+    for H in (1, 7, 100, 131, 4096):
+        for n in (1, 2, 3, 4, 8):
+            if n > H:
+                continue
+            for share in (root_share(n), 0.0, 0.5, 0.99):
+                spans = [weighted_bounds(H, n, r, share) for r in range(n)]
+                assert spans[0][0] == 0 and spans[-1][1] == H
+                assert all(spans[r][1] == spans[r + 1][0] for r in range(n - 1))
+                assert all(e > b for b, e in spans)
+                assert spans[0][1] >= -(-H // n)
+                rest = [e - b for b, e in spans[1:]]
+                assert not rest or max(rest) - min(rest) <= 1
+    assert root_share(1) == 1.0 and abs(root_share(2) - 2.5 / 3.5) < 1e-12
+    assert abs(root_share(8) - 2.5 / 9.5) < 1e-12 and root_share(8, rho=0.01) == 1.0 / 8
+
+
+def test_unpack_descriptors_cover_strips():
+    """The root's block descriptors (one unpack launch for every sender's packed
+    regions): every pixel of every strip covered once, packed blocks numbered
+    back to back per strip, filled regions marked empty."""
+    from simpleraytracing_amd.strips import EMPTY, unpack_descriptors
+    W = 100
+    spans = [(10, 77), (77, 131)]
+    rng = np.random.default_rng(3)
+    maps = []
+    for b, e in spans:
+        n = 4 * -(-(e - b) // 32)
+        m = np.full(n, EMPTY, np.uint32)
+        keep = np.sort(rng.choice(n, n // 2, replace=False))
+        m[keep] = rng.permutation(len(keep))
+        maps.append(m)
+    desc, bases, total = unpack_descriptors(W, spans, maps)
+    assert bases == [0, 6] and total == 6 + 4
+    cover = np.zeros((131, W), np.int32)
+    for r0, rows, c0, blk in desc:
+        assert 1 <= rows <= 32
+        cover[r0:r0 + rows, c0:c0 + 32] += 1
+    assert np.all(cover[10:131] == 1) and not cover[:10].any()
+    blocks = desc[desc[:, 3] != EMPTY, 3]
+    assert sorted(blocks.tolist()) == list(range(total))
+
+
 def test_strip_bounds_cover_image():
     for H in (1, 7, 128, 2048, 4097):
         for n in (1, 2, 3, 4, 8):

@@ -716,28 +716,35 @@ def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
     assert np.array_equal(out[2].cpu().numpy(), ref[2])
 
 
-@pytest.mark.parametrize("transit", ["packed", "dense"])
-def test_bench_strips_two_ranks_one_gpu(tmp_path, transit):
+@pytest.mark.parametrize("transit,ranks,share", [("packed", 2, "auto"), ("dense", 2, "auto"),
+                                                  ("packed", 3, "equal"), ("dense", 3, "0.5")])
+def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share):
     """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
     packed by region or dense --, expanded there) with 2 ranks on the one GPU
     (gloo, host-staged): the gathered frame is bit-equal to rank 0's
     single-device render."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    port = 29500 + (os.getpid() % 1000) + (7 if transit == "dense" else 0)
-    cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    port = 29500 + (os.getpid() % 1000) + (7 if transit == "dense" else 0) + 13 * ranks
+    cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
-           "--steps", "4", "--warmup", "1", "--transit", transit, "--kernel", "binned"]
+           "--gpus", str(ranks), "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
+           "--steps", "4", "--warmup", "1", "--transit", transit, "--kernel", "binned", "--root-share", share]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
     if r.returncode != 0:
         print(r.stderr[-6000:])
     assert r.returncode == 0
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
-    assert d["config"]["mode"] == "strips" and d["n_gpus"] == 2
+    assert d["config"]["mode"] == "strips" and d["n_gpus"] == ranks
     assert d["gather_check"]["bit_exact_vs_single_device_frame"] is True
     g = d["gather_check"]
+    rows = g["strip_rows"]
+    assert sum(rows) == 512 and len(rows) == ranks
+    if share == "equal":
+        assert max(rows) - min(rows) <= 1
+    else:
+        assert rows[0] > 512 // ranks
     if transit == "packed":
         assert g["bytes_gathered_per_step"] < g["dense_bytes_per_step"]
     else:
