@@ -209,6 +209,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        # a collective of every rank first: the point-to-point traffic below
+        # (map exchange, batch_isend_irecv on rank 0 only) must not be the
+        # group's first operation
+        dist.barrier()
 
     tris = xrt.load_ply(args.mesh)
     if args.tile_mesh > 1:
