@@ -1554,8 +1554,15 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
+#if XRT_RCP_FALLTHROUGH
+    // the short reciprocal on every survivor, the IEEE division only behind one
+    // rarely taken wave-uniform branch (straight-line common path)
+    float inv = rcp_newton(det);
+    if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) inv = inv_det_of(det);
+#else
     const float inv = __builtin_expect(__ballot(!rcp_newton_exact_for(det)) == 0ull, 1) ? rcp_newton(det)
                                                                                       : inv_det_of(det);
+#endif
     bool h;
     const float t = mt_finish_inv(det, inv, u, v, tnum, h);
     if (push) hl.push_if(h, t);

@@ -68,6 +68,7 @@ def main():
     if args.out:
         np.save(args.out, recs)
 
+    recs = recs[recs["t0"] != 0]        # the fill plan's padding records (no wave behind them)
     t0 = recs["t0"].astype(np.int64)
     t1 = recs["t1"].astype(np.int64)
     base = t0.min()
@@ -82,7 +83,7 @@ def main():
     span = e.max()
     order = np.argsort(e)
     res = {
-        "blocks": int(n.value),
+        "blocks": int(len(recs)),
         "span_us": round(float(span), 2),
         "start_last_us": round(float(s.max()), 2),
         "end_p50_us": round(float(np.percentile(e, 50)), 2),
