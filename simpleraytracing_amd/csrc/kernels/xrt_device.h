@@ -66,6 +66,9 @@
 #ifndef XRT_DESC_MED3
 #define XRT_DESC_MED3 1      // hit-list insertion from the top slot down (in place, no copies)
 #endif
+#ifndef XRT_RCP_FALLTHROUGH
+#define XRT_RCP_FALLTHROUGH 1  // binned survivors: short reciprocal always, IEEE division behind one rare branch (render -1.5..2.6 %)
+#endif
 #ifndef XRT_PREFETCH_OFFSETS
 #define XRT_PREFETCH_OFFSETS 1  // binned render: the tile's pixel offsets loaded at the wave's start
 #endif
