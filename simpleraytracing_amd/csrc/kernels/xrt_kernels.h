@@ -1227,15 +1227,7 @@ constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 constexpr uint32_t kPrepTris = XRT_PREP_TRIS;     // triangles per k_prep wave (1..64)
 static_assert(kPrepTris >= 1u && kPrepTris <= 64u, "kPrepTris");
 
-#ifndef XRT_PREP_MAX_VGPR
-#define XRT_PREP_MAX_VGPR 0     // A/B: cap k_prep's VGPRs (0 = the compiler's choice)
-#endif
-#if XRT_PREP_MAX_VGPR
-#define XRT_PREP_VGPR_ATTR __attribute__((amdgpu_num_vgpr(XRT_PREP_MAX_VGPR)))
-#else
-#define XRT_PREP_VGPR_ATTR
-#endif
-__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) XRT_PREP_VGPR_ATTR void k_prep(const float* __restrict__ tris, uint32_t T,
+__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
