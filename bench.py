@@ -299,12 +299,14 @@ def main():
         dist.send(t.cpu(), dst=0)             # gloo rehearsal: staged through the host
         return None
 
+    recv_ops = []
+    if gathering and root and nccl:           # the same receives every frame: built once
+        bufs = segs if packed else {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
+        recv_ops = [dist.P2POp(dist.irecv, t, g) for g, t in bufs.items()]
+
     def post_recvs():
         """RCCL: the frame's receives, posted before the root renders its own strip."""
-        if not nccl:
-            return None
-        bufs = segs if packed else {g: lb[b * W:e * W] for g, (b, e) in enumerate(bounds) if g}
-        return dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, g) for g, t in bufs.items()])
+        return dist.batch_isend_irecv(recv_ops) if recv_ops else None
 
     def finish_recvs(works):
         if nccl:
