@@ -433,6 +433,32 @@ def test_fill_plan_changes_nothing(ctx, dragon, W, H, r0, r1):
         assert _stats(on[3]) == _stats(off[3]), frame
 
 
+def test_global_list_and_fill_plan(ctx, dragon):
+    """The global list (footprints reaching more than 4,096 regions) against the
+    fill plan: dragon 4096^2 has edge-on slivers whose boxes span the frame but
+    whose loosened triangles reach few regions -- binned, not global, so regions
+    stay empty and the plan fills them; a genuinely big triangle goes global,
+    no region is empty and no plan is used.  Binned == brute on the latter."""
+    st = render(ctx, dragon, 4096, 4096, xrt.XRT_KERNEL_BINNED, 0, 64)[3]
+    assert st.global_triangles == 0 and ctx.fill_regions() > 0
+    W = H = 2112                                           # 66 x 66 = 4,356 regions
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    o, d = np.array(cam.origin, np.float64), np.array(cam.detector, np.float64)
+    up, right = np.array(cam.up, np.float64), np.array(cam.right, np.float64)
+    c = o + 0.95 * (d - o)                                 # a triangle across the whole view, behind the dragon
+    span = 4.0 * cam.pixel_spacing * W
+    big = np.array([np.concatenate([c - span * up - span * right, c - span * up + 2 * span * right,
+                                    c + 2 * span * up - span * right])], np.float32)
+    scene = np.ascontiguousarray(np.concatenate([dragon, big]))
+    a = render(ctx, scene, W, H, xrt.XRT_KERNEL_BINNED, cam=cam)
+    assert a[3].global_triangles >= 1 and ctx.fill_regions() == 0
+    assert a[3].hit_rays == W * H                          # every ray meets the big triangle
+    b = render(ctx, scene, W, H, xrt.XRT_KERNEL_BRUTE, cam=cam)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    assert (a[3].hit_rays, a[3].odd_rays, a[3].max_hits) == (b[3].hit_rays, b[3].odd_rays, b[3].max_hits)
+
+
 def test_fill_plan_rejected_when_k_prep_bins_into_it(ctx, dragon):
     """Test hook 2 plans every region as empty.  k_prep then bins pairs into
     planned-empty regions and flags it, and the host launches that frame with
