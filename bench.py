@@ -271,6 +271,9 @@ def main():
             expect_fill = len(rmap) - n_packed
             d_map = torch.from_numpy(rmap.view(np.int32)).to(dev)
             pbufs = [torch.zeros(max(n_packed, 1) * 1024, dtype=torch.float32, device=dev) for _ in range(2)]
+            # later frames render their L-buffer straight into the packed layout
+            if expect_fill:
+                ctx.set_transit_layout(pbufs[0].numel())
             meta = torch.tensor([n_packed], dtype=torch.int64)
             dist.send(meta.to(dev) if nccl else meta, dst=0)
             dist.send(d_map if nccl else d_map.cpu(), dst=0)
@@ -342,14 +345,18 @@ def main():
             b = k % 2
             if pending[b] is not None:
                 pending[b].wait()             # the send of frame k-2 has read this buffer
-            ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
-            if packed:
-                if expect_fill and ctx.fill_regions() != expect_fill:   # the map assumes this frame filled them
+            if packed and expect_fill:        # the render writes the packed blocks itself
+                ctx.render_rows_device(cam, r0, r1, 0, pbufs[b].data_ptr(), 0, stream.cuda_stream)
+                if ctx.fill_regions() != expect_fill:   # the map assumes this frame filled them
                     raise RuntimeError(f"rank {rank}: the strip's fill plan did not hold for frame {k}")
+                pending[b] = send_strip(pbufs[b])
+            elif packed:                      # no plan (every region travels): pack the row-major strip
+                ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
                 ctx.pack_regions_device(W, r1 - r0, d_map.data_ptr(), tbufs[b].data_ptr(), pbufs[b].data_ptr(),
                                         stream.cuda_stream)
                 pending[b] = send_strip(pbufs[b])
             else:
+                ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
                 pending[b] = send_strip(tbufs[b])
 
     for _ in range(args.warmup):

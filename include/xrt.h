@@ -393,6 +393,17 @@ int xrt_pack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, con
 int xrt_unpack_regions_device(xrt_context* ctx, uint32_t width, uint32_t rows, const uint32_t* d_map,
                               const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
 /*
+ * Renders of this context write the L-buffer in the packed layout directly
+ * (no xrt_pack_regions_device pass): region r of the strip to block map[r] of
+ * d_lbuffer, nothing for the regions the fill plan fills.  For BINNED
+ * attenuation renders of the L-buffer only (image and u8 NULL), typically with
+ * XRT_MISS_TRANSIT; `packed_floats` is the L-buffer's capacity in floats.  A
+ * frame whose fill plan does not hold (or does not fit) is not rendered and
+ * returns XRT_ERR_OVERFLOW.  0 restores the row-major layout.
+ */
+int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats);
+
+/*
  * Many strips' packed regions in one launch: d_desc holds 4 u32 per block --
  * first frame row, rows of the block inside its strip (<= 32), first column,
  * packed block index in d_packed (0xFFFFFFFF: a filled region, all misses).

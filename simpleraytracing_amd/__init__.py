@@ -281,6 +281,10 @@ class Context:
                                                         d_image or None, d_u8 or None, stream or None),
                     "xrt_unpack_regions_device")
 
+    def set_transit_layout(self, packed_floats: int):
+        """Render L-buffers in the packed layout (capacity in floats; 0: row-major)."""
+        self._check(self._lib.xrt_set_transit_layout(self._ctx, int(packed_floats)), "xrt_set_transit_layout")
+
     def unpack_blocks_device(self, width: int, n_blocks: int, d_desc: int, d_packed: int, d_lbuffer: int,
                              d_image: int, d_u8: int, stream: int = 0):
         """Many strips' packed regions into whole-frame planes in one launch (see xrt.h)."""

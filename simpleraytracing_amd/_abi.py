@@ -140,6 +140,7 @@ XRT_SYMBOLS = {
     "xrt_pack_regions_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp]),
     "xrt_unpack_regions_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
                                                  _vp]),
+    "xrt_set_transit_layout": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_unpack_blocks_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "xrt_multi_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_MultiP)]),
     "xrt_multi_destroy": (None, [_MultiP]),

@@ -84,6 +84,10 @@ struct Outputs {
     // (kMissTransit, expanded on the receiving device by k_expand).
     float miss_l;
     float mu;                  // kModelSigned: mesh 0's attenuation coefficient (fork :800)
+    // Packed transit layout (BINNED with a fill plan only): pixel (row, col) of
+    // the region in launch slot s goes to s * 1024 + its row-major offset in the
+    // region's 32x32 block; the plan's filled regions store nothing.
+    uint32_t packed;
 };
 
 // A signalling NaN no render produces (path lengths are >= 0, +inf, or x86's
@@ -462,7 +466,7 @@ __device__ float wave_overflow_distance(const TriRec* __restrict__ recs, uint32_
 // tested (fetch(k) = triangle of the k-th).
 template <typename Fetch>
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
-                                           uint32_t row, uint32_t col, const HitList& hl,
+                                           size_t o, const HitList& hl,
                                            WaveStats& ws, const TriRec* __restrict__ recs, float dx,
                                            float dy, float dz, uint32_t n_cand, Fetch fetch)
 {
@@ -495,7 +499,6 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         distance = xrt_f32_from_bits(kX86DefaultNaN);
         lval = distance;
     }
-    size_t o = (size_t)(row - p.row_begin) * p.width + col;
     if (ablation(p) & (kAblateStores | kAblateShade)) {
         if (!(ablation(p) & kAblateStores)) {
             if (out.image) out.image[o] = distance;
@@ -638,7 +641,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
     if constexpr (kSigned)
         finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, T, fetch);
     else
-        finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, T, fetch);
+        finish_ray(p, out, active, (size_t)(row - p.row_begin) * p.width + col, hl, ws, recs, dx, dy, dz, T, fetch);
     store_block_stats(ws, 0u, out.block_stats);
 }
 
@@ -646,6 +649,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
 // Tile cull (k_render_tiled, k_render_binned)
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRegion = 32;        // pixels per region side (one workgroup)
+constexpr uint32_t kPackBlock = kRegion * kRegion;   // floats per region in packed transit
 constexpr uint32_t kListCap = 2048;     // LDS candidate list capacity (tiled)
 #ifndef XRT_GLOBAL_REGIONS
 #define XRT_GLOBAL_REGIONS 4096
@@ -820,7 +824,8 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         }
         if (tile_live) {
             ws.tile_tests += tests;
-            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
+            finish_ray(p, out, active, (size_t)(row - p.row_begin) * p.width + col, hl, ws, recs, dx, dy, dz,
+                       n_cand, fetch);
         }
     }
 }
@@ -1612,6 +1617,10 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
     const bool active = col < p.width && row < p.row_end;
     const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
     const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
+    // the lane's output element: row-major in the strip, or in its slot's packed block
+    const size_t o = out.packed ? (size_t)slot * kPackBlock + ((tile >> 2) * 8u + (lane >> 3)) * kRegion +
+                                      (tile & 3u) * 8u + (lane & 7u)
+                                : (size_t)(row - p.row_begin) * p.width + col;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
@@ -1681,14 +1690,13 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
         if constexpr (kSigned)
             finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch);
         else
-            finish_ray(p, out, active, row, col, hl, ws, recs, dx, dy, dz, n_cand, fetch);
+            finish_ray(p, out, active, o, hl, ws, recs, dx, dy, dz, n_cand, fetch);
     } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
         ws.rays += (uint32_t)__popcll(__ballot(active));
         if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
     } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
         ws.rays += (uint32_t)__popcll(__ballot(active));
         if (active && !(ablation(p) & kAblateStores)) {
-            const size_t o = (size_t)(row - p.row_begin) * p.width + col;
             if (out.image) out.image[o] = 80.0f;
             if (out.lbuffer) out.lbuffer[o] = out.miss_l;
             if (out.image_u8) out.image_u8[o] = 255u;
@@ -1722,7 +1730,7 @@ __device__ __forceinline__ void fill_region_rows(const RenderParams& p, const Ou
         if (col < p.width && row < p.row_end) {
             ++n;
             const size_t o = (size_t)(row - p.row_begin) * p.width + col;
-            if (!(ablation(p) & kAblateStores)) {
+            if (!(ablation(p) & kAblateStores) && !out.packed) {
                 if (out.image) out.image[o] = 80.0f;
                 if (out.lbuffer) out.lbuffer[o] = out.miss_l;
                 if (out.image_u8) out.image_u8[o] = 255u;
@@ -1766,7 +1774,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         // statistics records: kBlocksPerRegion per wave, after the tile waves'
         const uint32_t rec0 =
             tile_blocks * kTileWaves + ((blockIdx.x - tile_blocks) * kTileWaves + wave) * kBlocksPerRegion;
-        fill_region_rows(p, out, bins, slot, wave, ws);
+        fill_region_rows(p, out, bins, slot, wave, ws);    // (packed layout: counts only)
         store_wave_stats(ws, 0u, out.block_stats, rec0, t_start);
         if ((threadIdx.x & 63u) == 0u) {
 #pragma unroll
@@ -1854,8 +1862,6 @@ __global__ __launch_bounds__(256) void k_hole_fill(const float* __restrict__ lbu
 // holds kMissTransit).  map[r] = kEmpty for a filled region.  One workgroup of
 // 256 threads per region, 4 pixels per thread.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPackBlock = kRegion * kRegion;
-
 __global__ __launch_bounds__(256) void k_pack_regions(const float* __restrict__ lbuffer, float* __restrict__ packed,
                                                       const uint32_t* __restrict__ map, uint32_t width,
                                                       uint32_t rows, uint32_t regions_x)

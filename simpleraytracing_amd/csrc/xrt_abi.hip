@@ -120,6 +120,7 @@ struct xrt_context {
     uint32_t plan_tile_slots = 0;
     bool plan_valid = false;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
+    uint64_t packed_cap = 0;           // xrt_set_transit_layout: the packed L-buffer's floats (0: row-major)
     std::vector<uint32_t> h_plan_region;   // the plan's slot -> region (row-major over the strip)
     uint32_t plan_rx = 0, plan_ry = 0;
 
@@ -598,6 +599,13 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     const uint32_t miss_bits = ctx->miss_code ? ctx->miss_code : 0x7F800000u;   // +inf
     std::memcpy(&out.miss_l, &miss_bits, sizeof miss_bits);
     out.mu = ctx->mu;
+    out.packed = 0u;
+    if (ctx->packed_cap) {                         // xrt_set_transit_layout
+        if (!binned || signed_model || d_image || d_u8)
+            return fail(ctx, XRT_ERR_ARGUMENT,
+                        "the packed layout is for BINNED attenuation renders of the L-buffer only");
+        out.packed = 1u;
+    }
     const uint32_t n_regions = rows ? rx * ry : 0u;
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
@@ -750,6 +758,10 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         ctx->bin_key_valid = false;
     }
     ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
+    if (pf.out.packed && rows > 0 &&
+        (bins.tile_slots >= rx * ry || (uint64_t)bins.tile_slots * kPackBlock > ctx->packed_cap))
+        return fail(ctx, XRT_ERR_OVERFLOW, "the packed layout needs this frame's fill plan (and room for its "
+                                        "unfilled regions): the frame was not rendered");
 
     // Events ride on the render's own dispatch (hipExtLaunchKernel).  Outside
     // timed regions every frame carries the set's start/end pair (stats
@@ -1206,6 +1218,13 @@ int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks
     hipLaunchKernelGGL(k_unpack_blocks, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream, d_packed,
                        reinterpret_cast<const uint4*>(d_desc), d_lbuffer, d_image, d_u8, width);
     XRT_HIP(ctx, hipGetLastError());
+    return XRT_OK;
+}
+
+int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    ctx->packed_cap = packed_floats;
     return XRT_OK;
 }
 

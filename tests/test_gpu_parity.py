@@ -743,6 +743,25 @@ def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
     assert np.array_equal(bits(out[1].cpu().numpy()), bits(ref[0]))
     assert np.array_equal(bits(out[0].cpu().numpy()), bits(ref[1]))
     assert np.array_equal(out[2].cpu().numpy(), ref[2])
+    # the same blocks written by the render itself (xrt_set_transit_layout)
+    direct = torch.full((n_packed * 1024,), -3.0, device=dev)
+    ctx.set_miss_code(xrt._abi.XRT_MISS_TRANSIT)
+    ctx.set_transit_layout(direct.numel())
+    try:
+        ctx.render_rows_device(cam, r0, r1, 0, direct.data_ptr(), 0, stream.cuda_stream)
+        assert ctx.fill_regions() == n_fill
+        with pytest.raises(RuntimeError):          # image / u8 planes have no packed layout
+            ctx.render_rows_device(cam, r0, r1, out[1].data_ptr(), direct.data_ptr(), 0, stream.cuda_stream)
+    finally:
+        ctx.set_transit_layout(0)
+        ctx.set_miss_code(0)
+    out2 = [torch.full((W * rows,), -2.0, device=dev), torch.zeros(W * rows, device=dev),
+            torch.zeros(W * rows, dtype=torch.uint8, device=dev)]
+    ctx.unpack_regions_device(W, rows, d_map.data_ptr(), direct.data_ptr(), out2[0].data_ptr(), out2[1].data_ptr(),
+                              out2[2].data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    for x, y in zip(out2, out):
+        assert np.array_equal(x.cpu().numpy().view(np.uint8), y.cpu().numpy().view(np.uint8))
 
 
 @pytest.mark.parametrize("transit,ranks,share", [("packed", 2, "auto"), ("dense", 2, "auto"),
