@@ -58,7 +58,7 @@
 #define XRT_RENDER_WAVES 8   // binned render: minimum waves per SIMD (8 = 64 VGPRs)
 #endif
 #ifndef XRT_STAGE
-#define XRT_STAGE 128     // binned render: candidates staged in LDS per round (16 KB)
+#define XRT_STAGE 64      // binned render: candidates staged in LDS per round (8 KB; 128: 16 KB, 4 % slower at 2048^2 with the heavy-first plan)
 #endif
 #ifndef XRT_FOLD_CMP
 #define XRT_FOLD_CMP 1       // Ray::intersect's four range tests folded into two (min / max)
