@@ -42,6 +42,12 @@ struct CullParams {
     int dir_grid;     // every nonzero component of every ray direction of the image is a
                       // multiple of 2^dir_grid (DESIGN.md "Tile cull", step 0)
     int pad;
+    // The camera in f64, formed on the host exactly as compute_footprint would
+    // (detector - origin, up, right, spacing and the centring offsets): kernel
+    // arguments stay in SGPRs, where converting the floats in the kernel held
+    // 24 VGPRs of uniform values through the edge loop.
+    double cvec[3], up[3], rt[3];
+    double ps, cv, cu;
 };
 
 // Grid exponent of a float: x is a multiple of 2^grid_exp(x), the weight of
@@ -999,12 +1005,10 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
     double Bx = 16.0 * kEps * l1e1 * l1e2;
     double B[3] = {Bd + Ba + Bb + Bx, Ba + Bx, Bb + Bx};
 
-    double Cv[3] = {(double)p.cx - p.ox, (double)p.cy - p.oy, (double)p.cz - p.oz};
-    double Up[3] = {p.ux, p.uy, p.uz};
-    double Rt[3] = {p.rx, p.ry, p.rz};
-    double ps = p.spacing;
-    double cv = ps * (0.5 - cp.height / 2.0);
-    double cu = ps * (0.5 - cp.width / 2.0);
+    const double* Cv = cp.cvec;
+    const double* Up = cp.up;
+    const double* Rt = cp.rt;
+    const double ps = cp.ps, cv = cp.cv, cu = cp.cu;
 
     float ea[3], eb[3], ec[3];
     double c_edge[3] = {0.0, 0.0, 0.0};   // the constants before the tile half-width (the box below)

@@ -340,6 +340,14 @@ CullParams make_cull_params(const xrt_camera& c)
     cp.height = c.height;
     cp.dir_grid = direction_grid(c, cp.dmax);
     cp.pad = 0;
+    for (int k = 0; k < 3; ++k) {
+        cp.cvec[k] = (double)c.detector[k] - (double)c.origin[k];
+        cp.up[k] = c.up[k];
+        cp.rt[k] = c.right[k];
+    }
+    cp.ps = c.pixel_spacing;
+    cp.cv = cp.ps * (0.5 - cp.height / 2.0);
+    cp.cu = cp.ps * (0.5 - cp.width / 2.0);
     return cp;
 }
 

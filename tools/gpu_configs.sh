@@ -1,8 +1,9 @@
 #!/bin/bash
 # Every BASELINE.json config on one GPU, plus the LDS staging batch sweep
-# (XRT_STAGE candidates staged per round: 64 / 128 (default) / 256, variant
-# builds from tools/build_variants.sh) on dragon 2048^2 and the 1.12M-triangle
-# tiled mesh at 8192^2.  Each GPU step has its own limit; a summary table at the end.
+# (XRT_STAGE candidates staged per round, variant builds from
+# tools/build_variants.sh named in $VARIANTS, e.g. "stage128 stage256") on dragon
+# 2048^2 and the 1.12M-triangle tiled mesh at 8192^2.  Each GPU step has its own
+# limit; a summary table at the end.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/configs
@@ -16,7 +17,7 @@ timeout -k 10 120 $B --size 1024 1024 > $OUT/binned_1024.json 2> $OUT/binned_102
  && timeout -k 10 120 $B --size 8192 8192 --steps 20 --warmup 3 > $OUT/binned_8192.json 2> $OUT/binned_8192.err \
  && timeout -k 10 200 $B --size 8192 8192 --tile-mesh 7 --steps 5 --warmup 2 > $OUT/binned_1m_8192.json 2> $OUT/binned_1m_8192.err \
  || exit 1
-for v in stage64 stage256; do
+for v in ${VARIANTS:-}; do
   L=simpleraytracing_amd/lib/ab/libxrt_$v.so
   XRT_LIB=$L timeout -k 10 120 $B --size 2048 2048 > $OUT/${v}_2048.json 2> $OUT/${v}_2048.err \
    && XRT_LIB=$L timeout -k 10 200 $B --size 8192 8192 --tile-mesh 7 --steps 5 --warmup 2 > $OUT/${v}_1m_8192.json 2> $OUT/${v}_1m_8192.err \
