@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--mesh", default=os.path.join(ROOT, "data", "dragon.ply"))
     ap.add_argument("--tile-mesh", type=int, default=1,
                     help="n x n tiled copies of the mesh (7 = the 1M-triangle config)")
+    ap.add_argument("--orbit", type=float, default=0.0, metavar="DEG",
+                    help="frames mode: frame k's camera is the default one turned k*DEG degrees about the "
+                         "detector's up axis through the mesh centre (a projection sweep: every frame a "
+                         "new geometry for the region lists); 0 = one camera")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
@@ -187,7 +191,7 @@ def main():
     import torch.distributed as dist
 
     import simpleraytracing_amd as xrt
-    from simpleraytracing_amd.scenes import tiled_mesh
+    from simpleraytracing_amd.scenes import orbit_camera, tiled_mesh
     from simpleraytracing_amd.strips import root_share, strip_bounds, unpack_descriptors, weighted_bounds
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,6 +224,13 @@ def main():
     T = len(tris)
     cam = xrt.camera_for_mesh(tris, W, H)
     strips = mode == "strips"
+    if args.orbit and (strips or args.model != "attenuation"):
+        raise SystemExit("--orbit is for frames mode, attenuation model")
+    orbit_cams = None
+    if args.orbit:
+        lo, hi = xrt.mesh_bbox(tris)
+        orbit_cams = [orbit_camera(cam, 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64)),
+                                   k * args.orbit) for k in range(args.warmup + args.steps)]
     gathering = strips and world > 1
     # Row strips.  The root's own rows need no transfer: by default it renders a
     # larger first strip (strips.root_share), the others split the rest.
@@ -337,7 +348,7 @@ def main():
         elif root:
             o = r0 * W
             works = post_recvs() if gathering else None
-            ctx.render_rows_device(cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
+            ctx.render_rows_device(orbit_cams[k] if orbit_cams else cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
                                    u8.data_ptr() + o, stream.cuda_stream)
             if gathering:
                 finish_recvs(works)
@@ -410,7 +421,8 @@ def main():
         result_kernel = {1: "brute", 2: "tiled", 3: "binned"}[stats.kernel]
         workload = f"{os.path.basename(args.mesh)}" + (f" tiled {args.tile_mesh}x{args.tile_mesh}"
                                                          if args.tile_mesh > 1 else "") + f" {W}x{H}" + \
-            (" signed L-buffer + hole fill" if signed else "")
+            (" signed L-buffer + hole fill" if signed else "") + \
+            (f", orbit {args.orbit:g} deg per frame" if args.orbit else "")
         roofline = make_roofline(args, result_kernel, workload, stats, T, rays_per_launch, avg_kernel_s,
                                  launches)
         result = {

@@ -1152,9 +1152,10 @@ struct BinBuffers {
     // Slots [0, tile_slots) render as tiles (16 waves a region); the rest are
     // the fill plan's empty regions (one workgroup each).  = regions: no plan.
     uint32_t tile_slots;
-    // Fill plan: k_prep stores 1 here (host-mapped memory, read by the host
-    // before it launches the render) when it bins a pair past tile_slots or a
-    // triangle into the global list.  Null: no plan to check.
+    // k_prep's flags (host-mapped memory, read by the host before it launches
+    // the render): [0] = 1 when it bins a pair past tile_slots (the fill plan)
+    // or a triangle into the global list, [1] = 1 when a region's count passes
+    // its list's capacity.  Null: nothing to check.
     uint32_t* plan_miss;
 };
 
@@ -1468,6 +1469,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     if (__ballot(over) && lane == 0) {
         atomicMax(&bs->max_count, my_max);
         atomicOr(&bs->overflow, 1u);
+        if (bins.plan_miss) bins.plan_miss[1] = 1u;  // the host re-sizes for the next frame
     }
     XRT_STAMP(kStampPrep + 8 * blockIdx.x + 4);
 }

@@ -80,8 +80,9 @@ struct FrameSet {
     hipEvent_t done = nullptr;         // render end (unsampled frames of a timed region)
     hipEvent_t done_ev = nullptr;      // the event that marks the set's last render complete
     bool done_valid = false;
-    // Fill plan check (BinBuffers::plan_miss): host-mapped, cleared by the host
-    // before k_prep, read after the host has waited for k_prep's completion.
+    // k_prep's flags (BinBuffers::plan_miss): [0] the fill plan did not hold,
+    // [1] a list overflowed.  Host-mapped, cleared by the host before k_prep,
+    // read after the host has waited for k_prep's completion.
     volatile uint32_t* plan_flag = nullptr;
 };
 
@@ -154,9 +155,19 @@ struct xrt_context {
             return std::memcmp(&cam, &o.cam, sizeof cam) == 0 && row_begin == o.row_begin &&
                    row_end == o.row_end && T == o.T && gen == o.gen;
         }
+        // the same region grid and mesh: only the camera's pose differs
+        bool same_layout(const BinKey& o) const
+        {
+            return cam.width == o.cam.width && cam.height == o.cam.height && row_begin == o.row_begin &&
+                   row_end == o.row_end && T == o.T && gen == o.gen;
+        }
     } bin_key = {};
     static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
+    // A camera that moved under the same region grid keeps the lists' layout
+    // and fill plan (DESIGN.md "Moving camera"); once one has, the sizing
+    // plans for motion (a dilated fill plan, roomier lists).
+    bool moving = false;
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     uint32_t model = kModelAttenuation;   // xrt_set_model
     float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
@@ -169,6 +180,7 @@ struct xrt_context {
     bool host_profile = false;
     double hp_total = 0, hp_done = 0, hp_prep = 0, hp_lprep = 0, hp_lrender = 0, hp_gap = 0;
     uint64_t hp_calls = 0;
+    uint64_t hp_sizings = 0, hp_reused = 0, hp_plan_miss = 0, hp_overflow = 0;   // frames by geometry path
     HostClock::time_point hp_last_end{};
 };
 
@@ -498,11 +510,12 @@ void use_plan(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fill)
 }
 
 // Arms the k_prep check of a frame that uses the fill plan.
-void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins)
+void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool moving)
 {
     bins.plan_miss = nullptr;
-    if (bins.tile_slots < n_regions) {
-        *fs.plan_flag = 0u;
+    if (fs.plan_flag && (bins.tile_slots < n_regions || moving)) {
+        fs.plan_flag[0] = 0u;
+        fs.plan_flag[1] = 0u;
         bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
     }
 }
@@ -523,6 +536,7 @@ struct PendingFrame {
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
     HostClock::time_point t_call;
+    bool resized = false;              // prepared again after k_prep overflowed a list
 };
 
 int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
@@ -623,6 +637,21 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     key.row_end = row_end;
     key.T = T;
     key.gen = ctx->mesh_gen;
+    // A new camera over the same region grid (a projection sweep) reuses the
+    // current lists and plan instead of the synchronous sizing: k_prep flags a
+    // pair binned into a planned-empty region, into the global list or past a
+    // list's capacity (BinBuffers::plan_miss), and that frame renders every
+    // region as tiles (exact) while the next one re-sizes.
+    static const bool camera_reuse = [] {
+        const char* e = std::getenv("XRT_CAMERA_REUSE");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (camera_reuse && binned && rows > 0 && fill_ok && ctx->bin_key_valid && ctx->compact &&
+        !ctx->bin_force_cap && !ctx->packed_cap && !key.same(ctx->bin_key) && key.same_layout(ctx->bin_key)) {
+        ctx->bin_key = key;
+        ctx->moving = true;
+        ++ctx->hp_reused;
+    }
     const bool new_geometry = binned && rows > 0 && (!ctx->bin_key_valid || !key.same(ctx->bin_key));
     if (new_geometry) ctx->compact = false;
     if (binned) {
@@ -634,7 +663,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
         bins.tile_slots = n_regions;
         if (!new_geometry && ctx->compact && ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
-        arm_plan_check(fs, n_regions, bins);
+        arm_plan_check(fs, n_regions, bins, ctx->moving && fill_ok);
     }
 
     hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
@@ -643,6 +672,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // Size the compact region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of every region's count, slot offsets
         // from them, and a re-run of k_prep into the compact lists.
+        ++ctx->hp_sizings;
         std::vector<uint32_t> counts((size_t)n_regions * kCounterStride);
         BinState st = {};
         XRT_HIP(ctx, hipMemcpyAsync(counts.data(), bins.counts, counts.size() * sizeof(uint32_t),
@@ -658,10 +688,29 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         const int plan = ctx->fill_plan;
         if (plan != 0 && st.global_count == 0u && bins.order) {
             std::vector<uint32_t> full, empty, full_count;
+            // A moving camera fills only regions whose 8 neighbours are empty too
+            // (the silhouette moves less than a region per small step).
+            std::vector<uint8_t> busy(n_regions, 0);
+            for (uint32_t s = 0; s < n_regions; ++s)
+                if (counts[(size_t)s * kCounterStride] != 0u) busy[slot_region[s]] = 1;
+            if (ctx->moving) {
+                std::vector<uint8_t> grown(busy);
+                for (uint32_t r = 0; r < n_regions; ++r) {
+                    if (!busy[r]) continue;
+                    const int x = (int)(r % rx), y = (int)(r / rx);
+                    for (int dy = -1; dy <= 1; ++dy)
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int u = x + dx, v = y + dy;
+                            if (u >= 0 && v >= 0 && u < (int)rx && v < (int)ry) grown[(size_t)v * rx + u] = 1;
+                        }
+                }
+                busy.swap(grown);
+            }
             for (uint32_t s = 0; s < n_regions; ++s) {
                 const uint32_t c = counts[(size_t)s * kCounterStride];
-                (c == 0u || plan == 2 ? empty : full).push_back(slot_region[s]);
-                if (c != 0u && plan != 2) full_count.push_back(c);
+                const bool fill = !busy[slot_region[s]] || plan == 2;
+                (fill ? empty : full).push_back(slot_region[s]);
+                if (!fill) full_count.push_back(c);
             }
             // tile regions by candidate count, heaviest first (their long tiles start
             // first instead of setting the tail: render 2048^2 -6 %, 1024^2 -10 %;
@@ -691,7 +740,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         for (uint32_t s = 0; s < n_regions; ++s) {
             off[s] = (uint32_t)run;
             const uint64_t c = count_of[slot_region[s]];
-            run += c + c / 8u + 4u;
+            // a moving camera: room for the counts of the next poses (2c + 64)
+            run += ctx->moving ? 2u * c + 64u : c + c / 8u + 4u;
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
         off[n_regions] = (uint32_t)run;
@@ -724,7 +774,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
         bins.tile_slots = n_regions;
         if (ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
-        arm_plan_check(fs, n_regions, bins);
+        arm_plan_check(fs, n_regions, bins, ctx->moving && fill_ok);
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
     }
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
@@ -777,12 +827,30 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     }
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;
-    if (binned && bins.plan_miss && *fs.plan_flag != 0u) {
-        // k_prep binned a pair into a region the plan fills (or into the global
-        // list): this frame renders every region as tiles, the next re-plans.
+    if (binned && bins.plan_miss && (fs.plan_flag[0] | fs.plan_flag[1]) != 0u) {
+        // k_prep binned a pair into a region the plan fills, into the global
+        // list or past a list's capacity: this frame renders every region as
+        // tiles (exact).  The next frame re-sizes -- except after a plan miss of
+        // a moving camera, whose lists still hold (the next camera would miss
+        // a fresh plan as likely: edge-on slivers turn into wide wedges).
+        const bool overflow = fs.plan_flag[1] != 0u;
+        ++(overflow ? ctx->hp_overflow : ctx->hp_plan_miss);
+        if (overflow && !pf.resized && ctx->bin_key_valid) {
+            // A region whose list overflowed would render from the whole mesh:
+            // size this frame's lists now (k_prep's counts are this camera's)
+            // and prepare it again.  The set is this frame's (not yet rotated).
+            ctx->bin_key_valid = false;
+            const xrt_camera cam = ctx->bin_key.cam;
+            PendingFrame again;
+            int rc = prepare_frame(ctx, &cam, ctx->bin_key.row_begin, ctx->bin_key.row_end, pf.out.image,
+                                   pf.out.lbuffer, pf.out.image_u8, stream, again);
+            if (rc) return rc;
+            again.resized = true;
+            return launch_frame(ctx, again);
+        }
         bins.tile_slots = rx * ry;
         grid = dim3(kWavesPerRegion / kTileWaves * bins.tile_slots);
-        ctx->bin_key_valid = false;
+        if (overflow || !ctx->moving) ctx->bin_key_valid = false;
     }
     ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
     if (pf.out.packed && rows > 0 &&
@@ -913,7 +981,7 @@ int xrt_create(int device, xrt_context** out)
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
              hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
-             hipHostMalloc((void**)&fs.plan_flag, sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
+             hipHostMalloc((void**)&fs.plan_flag, 2 * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
         return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
@@ -932,6 +1000,11 @@ void xrt_destroy(xrt_context* ctx)
                      ctx->hp_done / ctx->hp_calls * 1e6, ctx->hp_prep / ctx->hp_calls * 1e6,
                      ctx->hp_lprep / ctx->hp_calls * 1e6, ctx->hp_lrender / ctx->hp_calls * 1e6,
                      ctx->hp_gap / ctx->hp_calls * 1e6);
+    if (ctx->host_profile && ctx->hp_calls)
+        std::fprintf(stderr, "xrt geometry: %llu sizings, %llu camera reuses; frames flagged by k_prep: %llu plan "
+                     "misses, %llu list overflows\n", (unsigned long long)ctx->hp_sizings,
+                     (unsigned long long)ctx->hp_reused, (unsigned long long)ctx->hp_plan_miss,
+                     (unsigned long long)ctx->hp_overflow);
     (void)hipSetDevice(ctx->device);
     if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
     (void)hipDeviceSynchronize();

@@ -8,8 +8,13 @@ copy-major (j outer, k inner).  For dragon.ply and n = 7 that is
 22,866 * 49 = 1,120,434 triangles; tiling across the detector keeps the hit
 count per ray at the single dragon's (<= 12), as tiling along the ray would not.
 Deterministic: no randomness.
+
+``orbit_camera`` turns a camera about its up axis through a centre: a
+projection sweep (bench.py --orbit, the moving-camera parity test).
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
@@ -29,3 +34,24 @@ def tiled_mesh(tris: np.ndarray, n: int = 7) -> np.ndarray:
             off = np.array([0.0, np.float32(j) * dy, np.float32(k) * dz], np.float32)
             out.append((tris.reshape(-1, 3, 3) + off[None, None, :]).astype(np.float32).reshape(-1, 9))
     return np.ascontiguousarray(np.concatenate(out), np.float32)
+
+
+def orbit_camera(cam, centre, deg):
+    """cam turned deg degrees about its up axis through centre (Rodrigues in
+    f64, stored as float32): origin, detector and the right axis turn; up,
+    spacing and size stay."""
+    out = type(cam)()
+    ctypes.pointer(out)[0] = cam
+    up = np.array(cam.up[:], np.float64)
+    k = up / np.linalg.norm(up)
+    th = np.radians(deg)
+    c, s = np.cos(th), np.sin(th)
+
+    def rot(v):
+        return v * c + np.cross(k, v) * s + k * np.dot(k, v) * (1.0 - c)
+
+    for name, is_point in (("origin", True), ("detector", True), ("right", False)):
+        v = np.array(getattr(cam, name)[:], np.float64)
+        r = rot(v - centre) + centre if is_point else rot(v)
+        getattr(out, name)[:] = [float(np.float32(x)) for x in r]
+    return out

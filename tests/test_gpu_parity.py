@@ -11,7 +11,7 @@ import pytest
 
 import simpleraytracing_amd as xrt
 from simpleraytracing_amd import _abi
-from simpleraytracing_amd.scenes import tiled_mesh
+from simpleraytracing_amd.scenes import orbit_camera, tiled_mesh
 from oracle import oracle
 from conftest import DRAGON, GOLDEN, ROOT, bits
 from kat import kat_vectors
@@ -431,6 +431,40 @@ def test_fill_plan_changes_nothing(ctx, dragon, W, H, r0, r1):
         for x, y in zip(on[:3], off[:3]):
             assert np.array_equal(bits(x), bits(y)), frame
         assert _stats(on[3]) == _stats(off[3]), frame
+
+
+@pytest.mark.parametrize("W,H,r0,r1,degs", [
+    (512, 512, 0, None, [0, 1, 2, 3, 3.5, 10, 10, 45, 46, 90, 91, 0]),
+    (1000, 700, 0, None, [0, 0.5, 1, 1.5, 30, 30.5, 180, 181]),
+    (1024, 1024, 256, 700, [0, 1, 2, 20, 21, 22]),
+])
+def test_moving_camera_reuses_lists_exactly(dragon, W, H, r0, r1, degs):
+    """A projection sweep: each frame a new camera over the same region grid, so
+    the context keeps the previous sizing's lists and fill plan (no synchronous
+    re-sizing) and k_prep flags the frames the plan or a list capacity does not
+    hold (tiles, then a re-size).  Every frame is bit-identical, image, L-buffer,
+    u8 and hit statistics, to a fresh context's render of that camera."""
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    seq = xrt.Context(0)
+    seq.set_kernel(xrt.XRT_KERNEL_BINNED)
+    seq.upload_mesh(dragon)
+    fills = []
+    for i, d in enumerate(degs):
+        cam = orbit_camera(base, centre, d)
+        got = seq.render_rows(cam, r0, r1)
+        fills.append(seq.fill_regions())
+        with xrt.Context(0) as fresh:
+            fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
+            fresh.upload_mesh(dragon)
+            ref = fresh.render_rows(cam, r0, r1)
+        for x, y in zip(got[:3], ref[:3]):
+            assert np.array_equal(bits(x), bits(y)), (i, d)
+        for f in ("rays", "hit_rays", "odd_rays", "max_hits"):
+            assert getattr(got[3], f) == getattr(ref[3], f), (i, d, f)
+    seq.close()
+    assert any(fills[1:]), fills          # some frames of the sweep ran on a carried-over plan
 
 
 def test_global_list_and_fill_plan(ctx, dragon):
