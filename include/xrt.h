@@ -365,7 +365,9 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
  * the geometry's sizing frame counted empty render as one miss-filling
  * workgroup each instead of 16 tile waves.  mode 1 (default) on, 0 off;
  * test hook 2 plans every region as empty, so every workgroup takes the
- * exact fallback of a region that is not.  The next frame re-sizes.
+ * exact fallback of a region that is not.  The next frame re-sizes (after a
+ * camera change under the same image size and strip the context keeps its
+ * lists and plan instead: DESIGN.md "Moving camera"; XRT_CAMERA_REUSE=0 off).
  */
 int xrt_set_fill_plan(xrt_context* ctx, int mode);
 
