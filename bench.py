@@ -81,16 +81,18 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(tris, W, H, budget_s, gpu_rows):
+def cpu_baseline(tris, cam, W, H, budget_s, gpu_rows):
     """The oracle (a restatement of main.cxx's serial loop, threaded over pixel
     blocks like main-pthreads-redo.cxx) timed on a bounded row sample of the same
-    frame; also checks those rows against the GPU frame."""
+    frame; also checks those rows against the planes the timed loop's last frame
+    left on the GPU."""
     import numpy as np
 
     from oracle import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
-    cam = oracle.camera_for_mesh(tris, W, H)
+    cam = np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) + [cam.pixel_spacing],
+                   np.float32)                         # the oracle's 13-float camera
     # serial rate on a span of one row (the reference main.cxx is single-threaded),
     # sized to about 1 s
     mid = H // 2
@@ -121,7 +123,33 @@ def cpu_baseline(tris, W, H, budget_s, gpu_rows):
         "serial_value": serial_rate / 1e6,
         "serial_sample": f"{span} rays of row {mid}, 1 thread ({serial_s:.2f} s)",
         "sample_bit_exact_vs_gpu": parity,
+        "gpu_planes": "the timed loop's last frame (device planes copied back after timing)",
     }
+
+
+def end_to_end(args, W, H, device_index, kernel):
+    """The reference's only published numbers are whole-process runs
+    (submit-serial.sh:18 /usr/bin/time; main.cxx:206-216 times the load): a fresh
+    context's load + upload + first render (list sizing included) + D2H of the
+    three planes, each part timed on the host (HIP already initialised)."""
+    import simpleraytracing_amd as xrt
+    from simpleraytracing_amd.scenes import tiled_mesh
+    t0 = time.perf_counter()
+    tris = xrt.load_ply(args.mesh)
+    if args.tile_mesh > 1:
+        tris = tiled_mesh(tris, args.tile_mesh)
+    t1 = time.perf_counter()
+    with xrt.Context(device_index) as c:
+        c.set_kernel(kernel)
+        t2 = time.perf_counter()
+        c.upload_mesh(tris)
+        t3 = time.perf_counter()
+        c.render_rows(xrt.camera_for_mesh(tris, W, H))    # host planes: render + D2H, synchronous
+        t4 = time.perf_counter()
+    return {"end_to_end_ms": (t1 - t0 + t4 - t2) * 1e3, "load_ms": (t1 - t0) * 1e3,
+            "upload_ms": (t3 - t2) * 1e3, "render_and_d2h_ms": (t4 - t3) * 1e3,
+            "what": "load PLY + upload + first render of a fresh context (list sizing included) + D2H of "
+                    "image, L-buffer and u8 (context creation excluded)"}
 
 
 def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_s, launches):
@@ -230,7 +258,7 @@ def main():
     if args.orbit:
         lo, hi = xrt.mesh_bbox(tris)
         orbit_cams = [orbit_camera(cam, 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64)),
-                                   k * args.orbit) for k in range(args.warmup + args.steps)]
+                                   k * args.orbit) for k in range(max(args.warmup, 1) + args.steps)]
     gathering = strips and world > 1
     # Row strips.  The root's own rows need no transfer: by default it renders a
     # larger first strip (strips.root_share), the others split the rest.
@@ -370,7 +398,13 @@ def main():
                 ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
                 pending[b] = send_strip(tbufs[b])
 
-    for _ in range(args.warmup):
+    # the first frame of this context (list sizing included), then the warm-up
+    torch.cuda.synchronize(dev)
+    t_first = time.perf_counter()
+    step()
+    torch.cuda.synchronize(dev)
+    first_frame_ms = (time.perf_counter() - t_first) * 1e3
+    for _ in range(max(args.warmup - 1, 0)):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -425,6 +459,13 @@ def main():
             (f", orbit {args.orbit:g} deg per frame" if args.orbit else "")
         roofline = make_roofline(args, result_kernel, workload, stats, T, rays_per_launch, avg_kernel_s,
                                  launches)
+        ms_per_step = elapsed_max / args.steps * 1e3
+        if not strips and roofline["avg_kernel_ms"] > ms_per_step:
+            # the renders of one stream are serial: their mean duration cannot
+            # exceed the step time -- an event sample that says so is not the
+            # kernel's duration
+            raise SystemExit(f"bench.py: avg_kernel_ms {roofline['avg_kernel_ms']:.4f} > ms_per_step "
+                             f"{ms_per_step:.4f} ({launches} sampled launches): inconsistent timing")
         result = {
             "metric": "Mrays/s (dragon.ply render, whole job)",
             "value": value,
@@ -432,7 +473,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong" if strips else "weak",
             "vs_baseline": None,
@@ -459,14 +500,23 @@ def main():
                 "wave_tile_tests": stats.tile_tests,
                 "ray_triangle_tests_per_ray": stats.tile_tests * 64 / max(stats.rays, 1),
             },
+            "latency": {"first_frame_ms": first_frame_ms,
+                        "first_frame": "this context's first frame: k_prep, the synchronous list sizing, "
+                                       "k_prep again and the render (device planes, synchronised)"},
             "cpu_baseline": None,
             "gather_check": gather,
             "dist_backend": args.dist_backend if world > 1 else None,
         }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not signed:
-        full = ctx.render_rows(cam)     # the same frame, fetched to the host for the parity check
-        result["cpu_baseline"] = cpu_baseline(tris, W, H, args.cpu_seconds, full[:3])
+    if rank == 0 and world == 1 and not signed:
+        # the timed loop's own planes (its last frame), checked against the oracle's rows
+        last_cam = orbit_cams[frame_no[0] - 1] if orbit_cams else cam
+        planes = (img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy())
+        result["latency"].update(end_to_end(args, W, H, device_index, {"auto": xrt.XRT_KERNEL_AUTO,
+                                 "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
+                                 "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]))
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
 
     if world > 1:
         dist.barrier()

@@ -418,6 +418,15 @@ int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks
 int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
 
 /*
+ * Diagnostics: BINNED frames by geometry path since the context was created --
+ * counters[0] frames whose lists were sized synchronously (a new frame
+ * geometry), [1] frames rendered over lists sized for another camera of the
+ * same region grid (a moving camera), [2] frames k_prep flagged for a fill-plan
+ * miss, [3] frames k_prep flagged for a list overflow.
+ */
+int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4]);
+
+/*
  * Diagnostics: copies the last render's statistics records (32 bytes each, one
  * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
  * overflow rays, hits, wave-level triangle tests, candidates, max hits; builds

@@ -47,7 +47,7 @@ void xrt_host_intersect_batch(const float* rays, const float* triangles, uint64_
  *                   (applyLUT's intended mapping, include/Image.inl:189-216,
  *                   without its [i] / [i*3] indexing bug)
  *   XRT_IMAGE_PGM   the same LUT as binary 8-bit PGM
- *   XRT_IMAGE_JPEG  saveJPEGFile: XRT_ERR_IO (no libjpeg headers in this build)
+ *   XRT_IMAGE_JPEG  saveJPEGFile: baseline JPEG of the LUT, quality 100 (src/Image.cxx:85-144)
  */
 enum { XRT_IMAGE_TEXT = 0, XRT_IMAGE_TGA = 1, XRT_IMAGE_PGM = 2, XRT_IMAGE_JPEG = 3 };
 int xrt_host_save_image(const float* pixels, uint32_t width, uint32_t height, const char* path, int format,

@@ -32,7 +32,8 @@ def _fp(a):
 def lib():
     global _orc
     if _orc is None:
-        path = os.path.join(HERE, "liboracle.so")
+        # XRT_ORACLE_LIB: a sanitizer build (make -C oracle SAN=1, tools/san_check.sh)
+        path = os.environ.get("XRT_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run `make -C oracle`")
         L = ctypes.CDLL(path)

@@ -217,6 +217,12 @@ class Context:
         self._check(self._lib.xrt_debug_fill_regions(self._ctx, ctypes.byref(n)), "xrt_debug_fill_regions")
         return n.value
 
+    def geometry_counters(self) -> dict:
+        """BINNED frames by geometry path: sized, reused (moving camera), plan misses, list overflows."""
+        c = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.xrt_debug_geometry_counters(self._ctx, c), "xrt_debug_geometry_counters")
+        return dict(zip(("sizings", "reused", "plan_misses", "overflows"), (int(v) for v in c)))
+
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
                     image=True, lbuffer=True, u8=True):
         """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats)."""

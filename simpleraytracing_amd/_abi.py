@@ -131,6 +131,7 @@ XRT_SYMBOLS = {
     "xrt_set_bin_capacity": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_set_fill_plan": (ctypes.c_int, [_CtxP, ctypes.c_int]),
     "xrt_debug_fill_regions": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint32)]),
+    "xrt_debug_geometry_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
@@ -210,7 +211,8 @@ def load_host():
     global _host
     if _host is None:
         load()
-        path = lib_path("libxrt_host.so")
+        # XRT_HOST_LIB: a sanitizer build (make -C simpleraytracing_amd/csrc SAN=1, tools/san_check.sh)
+        path = os.environ.get("XRT_HOST_LIB") or lib_path("libxrt_host.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: build simpleraytracing_amd/csrc first")
         _host = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL), XRT_HOST_SYMBOLS)

@@ -156,12 +156,6 @@ void Image::saveTGAFile(const std::string& file_name, float vmin, float vmax) co
     std::fclose(f);
 }
 
-void Image::saveJPEGFile(const std::string& file_name, float, float) const
-{
-    throw std::runtime_error("JPEG output is not available in this build (no libjpeg headers); "
-                             "use saveTGAFile or savePGMFile for " + file_name);
-}
-
 void Image::savePGMFile(const std::string& file_name, float vmin, float vmax) const
 {
     std::FILE* f = std::fopen(file_name.c_str(), "wb");

@@ -6,8 +6,9 @@
 // writing what the reference writes (src/Image.cxx:210-235).  applyLUT is the
 // reference's intended 8-bit mapping with its indexing bug fixed
 // (include/Image.inl:189-216 reads [i*3] and writes [i]); saveTGAFile writes
-// that LUT as an uncompressed 24-bit TGA (src/Image.cxx:148-206).  JPEG output
-// needs libjpeg headers, which this image lacks: saveJPEGFile throws.
+// that LUT as an uncompressed 24-bit TGA (src/Image.cxx:148-206) and
+// saveJPEGFile as a baseline JPEG, quality 100 (src/Image.cxx:85-144; host/Jpeg.cpp,
+// an encoder of its own: this image has no libjpeg headers).
 #pragma once
 
 #include <string>

@@ -130,9 +130,14 @@ RayTracerInfo initialiseRayTracing(std::vector<TriangleMesh>&, const Vec3& upper
     info.origin = Vec3(cam.origin[0], cam.origin[1], cam.origin[2]);
     info.up = Vec3(cam.up[0], cam.up[1], cam.up[2]);
     info.right = Vec3(cam.right[0], cam.right[1], cam.right[2]);
+    // main.cxx:598-601: a white light at the source, pointing at the box centre
+    const Vec3 range = upper - lower;
+    Vec3 light_direction = (lower + range / 2.0) - info.origin;
+    light_direction.normalise();
+    info.light = Light(Vec3(1.0f, 1.0f, 1.0f), light_direction, info.origin);
     info.upper_bbox_corner = upper;
     info.lower_bbox_corner = lower;
-    info.range = upper - lower;
+    info.range = range;
     return info;
 }
 
@@ -204,13 +209,19 @@ void renderLoopRows(Image& image, const std::vector<TriangleMesh>& meshes, const
                  image.getData() + (size_t)row_begin * image.getWidth(), lbuffer_strip, u8_strip, stats);
 }
 
-unsigned long long renderLoop(Image& image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info)
+namespace {
+thread_local unsigned long long t_last_odd_rays = 0;
+}
+
+void renderLoop(Image& image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info)
 {
     xrt_stats stats;
     renderLoopRows(image, meshes, info, 0, image.getHeight(), nullptr, nullptr, &stats);
     report_odd(stats.odd_rays);
-    return stats.odd_rays;
+    t_last_odd_rays = stats.odd_rays;
 }
+
+unsigned long long renderLoopOddRays() { return t_last_odd_rays; }
 
 unsigned long long renderLoopLBuffer(Image& image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info,
                                      std::vector<float>* lbuffer)

@@ -14,17 +14,20 @@
 #include <vector>
 
 #include "Image.h"
+#include "Light.h"
+#include "Material.h"
 #include "TriangleMesh.h"
 #include "Vec3.h"
 
 struct xrt_stats;
 
-// RayTracerInfo (main.cxx:111-121) without the Phong renderer's Light.
+// RayTracerInfo (main.cxx:111-121), member for member.
 struct RayTracerInfo {
     Vec3 detector_position;
     Vec3 origin;
     Vec3 up;
     Vec3 right;
+    Light light;              // initialiseRayTracing's light (main.cxx:598-601); unused by the X-ray path
     Vec3 upper_bbox_corner;
     Vec3 lower_bbox_corner;
     Vec3 range;
@@ -48,10 +51,13 @@ RayTracerInfo initialiseRayTracing(std::vector<TriangleMesh>& meshes, const Vec3
                                    const Vec3& lower, unsigned int image_height,
                                    unsigned int image_width, Image& output_image, float lut);
 
-// Whole image; prints one "Only one intersect on this ray" line per odd ray
-// (main.cxx:710) and returns the number of such rays.
-unsigned long long renderLoop(Image& output_image, const std::vector<TriangleMesh>& meshes,
-                              RayTracerInfo& info);
+// Whole image (main.cxx:159-161, the reference's declaration); prints one
+// "Only one intersect on this ray" line per odd ray (main.cxx:710).
+void renderLoop(Image& output_image, const std::vector<TriangleMesh>& meshes, RayTracerInfo& info);
+
+// The number of odd rays of this thread's last renderLoop call (the lines it
+// printed).
+unsigned long long renderLoopOddRays();
 
 // Rows [row_begin, row_end) of output_image only; optional L-buffer / 8-bit
 // outputs of the same strip size.  Does not print.

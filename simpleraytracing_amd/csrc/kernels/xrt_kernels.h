@@ -1135,20 +1135,34 @@ struct alignas(16) RegionEntry {
 };
 static_assert(sizeof(RegionEntry) == 128, "RegionEntry must be 128 bytes");
 
+// Read-only data of a launch (written by the host or an earlier kernel) read
+// through the constant address space: scalar loads, issued together.
+template <typename T>
+using const_ptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ const_ptr<T> as_const(const T* p)
+{
+    return (const_ptr<T>)p;
+}
+
+// One launch slot's static description (host-built per region grid / frame
+// geometry): its list is list[base .. base + cap), it renders region
+// (x, y) = (xy & 0xFFFF, xy >> 16).  A tile wave reads it with ONE
+// s_load_dwordx4 beside its count -- no dependent reads before its DMA.
+struct SlotDesc {
+    uint32_t base, cap, xy, pad;
+};
+static_assert(sizeof(SlotDesc) == 16, "SlotDesc must be 16 bytes");
+
 struct BinBuffers {
     uint32_t* counts;        // [n_regions * kCounterStride] by slot; cleared before every binned frame
-    RegionEntry* list;       // [n_regions * cap] entries by slot
+    RegionEntry* list;       // the slots' lists (SlotDesc::base / cap)
     RegionEntry* global_list;   // [T] entries of the footprints over > kGlobalRegions regions
-    const uint32_t* order;   // [n_regions] slot -> region (x | y << 16), the render launch order (null: raster)
-    const uint32_t* rank;    // [n_regions] region -> slot (order's inverse; null with order)
-    uint32_t cap;            // list capacity per region
+    const SlotDesc* desc;    // [n_regions] slot -> list and region, in the render's launch order
+    const uint32_t* rank;    // [n_regions] region -> slot (desc's inverse)
     uint32_t regions_x, regions_y;
     uint32_t* clear;         // the other half's counters (its BinState line precedes them), cleared by k_prep
     uint32_t clear_regions;  // counters to clear there
-    // Compact lists: slot s's list is list[offsets[s] .. offsets[s+1]) -- sized
-    // from the counts of the first frame of the geometry (identical for every
-    // frame of it).  Null: fixed capacity `cap` per slot (that first frame).
-    const uint32_t* offsets;
     // Slots [0, tile_slots) render as tiles (16 waves a region); the rest are
     // the fill plan's empty regions (one workgroup each).  = regions: no plan.
     uint32_t tile_slots;
@@ -1159,20 +1173,30 @@ struct BinBuffers {
     uint32_t* plan_miss;
 };
 
-__device__ __forceinline__ uint32_t list_base(const BinBuffers& b, uint32_t slot)
-{
-    return b.offsets ? b.offsets[slot] : slot * b.cap;
-}
-__device__ __forceinline__ uint32_t list_cap(const BinBuffers& b, uint32_t slot)
-{
-    return b.offsets ? b.offsets[slot + 1u] - b.offsets[slot] : b.cap;
-}
-
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t slot_of(const BinBuffers& bins, uint32_t region)
+// A render wave's first reads: its slot's count (k_prep's atomics) and its
+// SlotDesc, issued back to back as scalar loads and awaited once.  One asm
+// statement, so the compiler cannot put the count load behind a branch that
+// consumes the description (two serial round trips).  slot is wave-uniform.
+__device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot, uint32_t& count, uint32_t& base,
+                                          uint32_t& cap, uint32_t& xy)
 {
-    return bins.rank ? bins.rank[region] : region;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t* count_addr = bins.counts + (size_t)slot * kCounterStride;
+    const SlotDesc* desc_addr = bins.desc + slot;
+    u32x4 d;
+    uint32_t c;
+    asm volatile("s_load_dword %0, %2, 0x0\n\t"
+                 "s_load_dwordx4 %1, %3, 0x0\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(c), "=&s"(d)
+                 : "s"(count_addr), "s"(desc_addr)
+                 : "memory");
+    count = c;
+    base = d.x;
+    cap = d.y;
+    xy = d.z;
 }
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
@@ -1369,7 +1393,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
                 reg[b] = kEmpty;
                 own[b] = 0u;
                 if (q < queued) {
-                    reg[b] = slot_of(bins, s_qreg[wave][q]);
+                    reg[b] = bins.rank[s_qreg[wave][q]];
                     own[b] = s_qown[wave][q];
                 }
             }
@@ -1382,8 +1406,10 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
-                lbase[b] = reg[b] != kEmpty ? list_base(bins, reg[b]) : 0u;
-                lcap[b] = reg[b] != kEmpty ? list_cap(bins, reg[b]) : 0u;
+                const uint2 bc = reg[b] != kEmpty ? *reinterpret_cast<const uint2*>(bins.desc + reg[b])
+                                                  : make_uint2(0u, 0u);
+                lbase[b] = bc.x;
+                lcap[b] = bc.y;
             }
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
@@ -1598,20 +1624,14 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
                                             uint64_t& t_staged)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n_local = wave_uniform(bins.counts[(size_t)slot * kCounterStride]);
-    uint32_t reg_x, reg_y;
-    if (bins.order) {
-        const uint32_t xy = wave_uniform(bins.order[slot]);
-        reg_x = xy & 0xFFFFu;
-        reg_y = xy >> 16;
-    } else {
-        reg_x = slot % bins.regions_x;
-        reg_y = slot / bins.regions_x;
-    }
-    const RegionEntry* __restrict__ local = bins.list + list_base(bins, slot);
+    // the slot's count (k_prep) and description (host): two scalar loads in flight together
+    uint32_t n_local, d_base, d_cap, d_xy;
+    load_slot(bins, slot, n_local, d_base, d_cap, d_xy);
+    const uint32_t reg_x = d_xy & 0xFFFFu, reg_y = d_xy >> 16;
+    const RegionEntry* __restrict__ local = bins.list + d_base;
     const RegionEntry* __restrict__ glob = bins.global_list;
     const uint32_t T = p.num_triangles;
-    const bool whole = n_local > list_cap(bins, slot);   // the list overflowed: whole mesh (exact, slower)
+    const bool whole = n_local > d_cap;   // the list overflowed: whole mesh (exact, slower)
     const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole ? T : n_local + n_glob;
     cand = n_cand;
 
@@ -1716,15 +1736,8 @@ __device__ __forceinline__ void fill_region_rows(const RenderParams& p, const Ou
                                                  const BinBuffers& bins, uint32_t slot, uint32_t wave,
                                                  WaveStats& ws)
 {
-    uint32_t reg_x, reg_y;
-    if (bins.order) {
-        const uint32_t xy = wave_uniform(bins.order[slot]);
-        reg_x = xy & 0xFFFFu;
-        reg_y = xy >> 16;
-    } else {
-        reg_x = slot % bins.regions_x;
-        reg_y = slot / bins.regions_x;
-    }
+    const uint32_t xy = as_const(bins.desc)[slot].xy;
+    const uint32_t reg_x = xy & 0xFFFFu, reg_y = xy >> 16;
     constexpr uint32_t kRows = kRegion / kTileWaves;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t col = reg_x * kRegion + (lane % kRegion);
@@ -1771,7 +1784,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint64_t t_start = block_start_stamp();
     const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
     const uint32_t wave = wave_in_block();
-    const uint32_t n_glob = wave_uniform(bs->global_count);
+    const uint32_t n_glob = as_const(bs)->global_count;
     uint64_t t_staged = t_start;                   // XRT_STAMPS diagnostics
     WaveStats ws = {};
     uint32_t cand = 0;

@@ -30,6 +30,9 @@ constexpr uint64_t kTimingStride = 4;
 // Buffer sets in rotation: frame N's preparation reuses the set of frame
 // N - kFrameSets, whose render the host has seen complete by then.
 constexpr int kFrameSets = 4;
+// A camera that stays put this many frames over lists sized for another
+// camera is sized for itself.
+constexpr uint32_t kStillFrames = 2;
 
 
 // Everything one frame's preparation writes and its render reads or writes.
@@ -88,6 +91,18 @@ struct FrameSet {
 
 using HostClock = std::chrono::steady_clock;
 
+// A launch layout of a region grid: launch slot -> region and list
+// (SlotDesc, device), region -> slot (k_prep's binning), and the host copy of
+// slot -> region (row-major over the strip).
+struct SlotLayout {
+    SlotDesc* d_desc = nullptr;
+    size_t desc_cap = 0;
+    uint32_t* d_rank = nullptr;
+    size_t rank_cap = 0;
+    std::vector<uint32_t> slot_region;
+    uint32_t rx = 0, ry = 0, cap = 0;  // the fixed-capacity layout's key
+};
+
 struct xrt_context {
     int device = 0;
     std::string error;
@@ -101,29 +116,25 @@ struct xrt_context {
     FrameSet* last_set = nullptr;      // set of the last enqueued frame
     hipStream_t prep_stream = nullptr;
 
-    // compact region lists of the current geometry (bin_key): slot offsets
-    uint32_t* d_slot_off = nullptr;
-    size_t slot_off_cap = 0;
+    // Launch layouts of the region grid (SlotLayout): the fixed-capacity one
+    // the first frame of a geometry bins into (centre-first order), and the
+    // compact one sized from its counts (the fill plan's order when there is
+    // a plan).
+    SlotLayout fixed;
+    SlotLayout compact_layout;
     uint64_t slot_pool = 0;            // entries of the compact lists
-    bool compact = false;              // d_slot_off is valid for bin_key
+    bool compact = false;              // compact_layout is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
-    uint32_t* d_order = nullptr;       // render launch order of the regions (launch_order)
-    size_t order_cap = 0;
-    uint32_t order_rx = 0, order_ry = 0;
-    std::vector<uint32_t> h_order;     // slot -> region (x | y << 16) of d_order
-    // Fill plan of the current geometry (bin_key): launch order with the
-    // regions its sizing frame counted empty last, one workgroup each
-    // (DESIGN.md "Fill plan").  fill_plan: 1 on (XRT_FILL=0 / xrt_set_fill_plan
-    // turn it off); 2 plans EVERY region as empty (tests of the exact fallback).
+    // Fill plan of the current geometry (bin_key): the compact layout's
+    // slots [plan_tile_slots, regions) are the regions its sizing frame
+    // counted empty, one workgroup each (DESIGN.md "Fill plan").  fill_plan:
+    // 1 on (xrt_set_fill_plan 0 turns it off); 2 plans EVERY region as empty
+    // (tests of the exact fallback).
     int fill_plan = 1;
-    uint32_t* d_plan = nullptr;        // [slot -> region | region -> slot]
-    size_t plan_cap = 0;
     uint32_t plan_tile_slots = 0;
     bool plan_valid = false;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
     uint64_t packed_cap = 0;           // xrt_set_transit_layout: the packed L-buffer's floats (0: row-major)
-    std::vector<uint32_t> h_plan_region;   // the plan's slot -> region (row-major over the strip)
-    uint32_t plan_rx = 0, plan_ry = 0;
 
     // staging for the host-pointer entry point
     float* d_image = nullptr;
@@ -164,10 +175,13 @@ struct xrt_context {
     } bin_key = {};
     static_assert(sizeof(xrt_camera) == 15 * 4, "xrt_camera has no padding (compared bytewise)");
     bool bin_key_valid = false;
-    // A camera that moved under the same region grid keeps the lists' layout
-    // and fill plan (DESIGN.md "Moving camera"); once one has, the sizing
-    // plans for motion (a dilated fill plan, roomier lists).
+    // The last frame rendered over lists sized for another camera (DESIGN.md
+    // "Moving camera"): a sizing then plans for motion (roomier lists, no
+    // fill plan).
     bool moving = false;
+    bool reuse_cameras = true;         // false for xrt_render_rows_multi's contexts
+    BinKey last_key = {};              // the last frame's geometry
+    uint32_t still_frames = 0;         // frames in a row on one camera over reused lists
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     uint32_t model = kModelAttenuation;   // xrt_set_model
     float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
@@ -380,8 +394,7 @@ int check_camera(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, ui
 // k_prep: one thread per triangle, and at least one per image row and column
 // (the pixel-offset tables).
 int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const CullParams& cp, bool culled,
-                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done,
-                unsigned flags)
+                const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
 {
     const uint64_t T = ctx->num_tris;
     // kPrepTris triangles per wave; every thread covers a pixel-offset entry / counter
@@ -390,7 +403,7 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                                                (threads + kPrepThreads - 1) / kPrepThreads);
     const auto t_launch = HostClock::now();
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(kPrepThreads),
-                          0, stream, nullptr, done, flags,
+                          0, stream, nullptr, done, 0u,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
@@ -401,9 +414,10 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
 // Region buffers of a binned frame.  The frame counts into one half of the
 // set's counters (FrameSet::bin_counts); k_prep clears the other half.  A half
 // is cleared here, on the prep stream, only when it is not known clean for
-// this many regions (the first frames, a larger region grid, a re-run).
-int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& bins, BinState*& ctl,
-                hipStream_t stream, bool& cleared, bool rerun = false)
+// this many regions (the first frames, a larger region grid, a re-run).  The
+// caller sets the launch layout (bins.desc / bins.rank).
+int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, uint64_t list_entries, BinBuffers& bins,
+                BinState*& ctl, hipStream_t stream, bool& cleared, bool rerun = false)
 {
     cleared = false;
     const uint64_t T = ctx->num_tris;
@@ -416,11 +430,7 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
         fs.bin_half_words = half_words;
         fs.dirty[0] = fs.dirty[1] = kDirtyAll;
     }
-    const bool compact = ctx->compact && !ctx->bin_force_cap;
-    const uint32_t cap = ctx->bin_force_cap ? (uint32_t)std::min<size_t>(kInitialRegionCap, ctx->bin_force_cap)
-                                            : kInitialRegionCap;
-    if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, compact ? ctx->slot_pool : (size_t)n_regions * cap)))
-        return rc;
+    if ((rc = ensure(ctx, fs.bin_list, fs.bin_list_cap, (size_t)list_entries))) return rc;
     if ((rc = ensure(ctx, fs.global_list, fs.global_list_cap, T))) return rc;
     const uint32_t q = rerun ? fs.half : fs.half ^ 1u;     // a re-run recounts into the same half
     uint32_t* mine = fs.bin_counts + (size_t)q * fs.bin_half_words;
@@ -441,79 +451,85 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, BinBuffers& 
     bins.counts = mine + kCounterStride;
     bins.list = fs.bin_list;
     bins.global_list = fs.global_list;
-    bins.cap = cap;
-    bins.offsets = compact ? ctx->d_slot_off : nullptr;
     return XRT_OK;
 }
 
-// Render launch order of the regions (XRT_ORDER): 0 raster; 1 centre
-// first (regions by distance of their centre from the image centre), so the
-// dense middle of a centred object does not start last and set the tail.
-// A function of the region grid only, uploaded when the grid changes.
-int launch_order(xrt_context* ctx, uint32_t rx, uint32_t ry, BinBuffers& bins)
+// The base launch order of a region grid: centre first (regions by the
+// distance of their centre from the image centre), so the dense middle of a
+// centred object does not start last and set the tail.
+std::vector<uint32_t> centre_first_order(uint32_t rx, uint32_t ry)
 {
-    static const int mode = [] {
-        const char* e = std::getenv("XRT_ORDER");
-        return e ? std::atoi(e) : XRT_DEFAULT_ORDER;
-    }();
-    bins.order = nullptr;
-    bins.rank = nullptr;
-    if (mode == 0 || rx > 0xFFFFu || ry > 0xFFFFu) return XRT_OK;   // raster order
-    if (ctx->order_rx != rx || ctx->order_ry != ry || !ctx->d_order) {
-        const size_t n = (size_t)rx * ry;
-        std::vector<uint32_t> order(n);
-        for (size_t r = 0; r < n; ++r) order[r] = (uint32_t)r;
-        const double cx = 0.5 * (rx - 1), cy = 0.5 * (ry - 1);
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-            const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
-            return ax * ax + ay * ay < bx * bx + by * by;
-        });
-        // [slot -> region as (x | y << 16) | region -> slot]: the render takes its
-        // region's coordinates without an integer division
-        order.resize(2 * n);
-        for (size_t k = 0; k < n; ++k) {
-            const uint32_t r = order[k];
-            order[n + r] = (uint32_t)k;
-            order[k] = (r % rx) | ((r / rx) << 16);
-        }
-        XRT_HIP(ctx, hipDeviceSynchronize());   // the previous order may be in use
-        int rc = ensure(ctx, ctx->d_order, ctx->order_cap, 2 * n);
-        if (rc) return rc;
-        XRT_HIP(ctx, hipMemcpy(ctx->d_order, order.data(), 2 * n * sizeof(uint32_t), hipMemcpyHostToDevice));
-        order.resize(n);
-        ctx->h_order.swap(order);
-        ctx->order_rx = rx;
-        ctx->order_ry = ry;
+    const size_t n = (size_t)rx * ry;
+    std::vector<uint32_t> order(n);
+    for (size_t r = 0; r < n; ++r) order[r] = (uint32_t)r;
+    const double cx = 0.5 * (rx - 1), cy = 0.5 * (ry - 1);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
+        return ax * ax + ay * ay < bx * bx + by * by;
+    });
+    return order;
+}
+
+// Uploads a launch layout: slot s renders region slot_region[s] from
+// list[base[s] .. base[s] + cap[s]).  Frames in flight may read the previous
+// one, so the device is synchronised first.
+int upload_layout(xrt_context* ctx, SlotLayout& L, uint32_t rx, uint32_t ry, std::vector<uint32_t> slot_region,
+                  const std::vector<uint32_t>& base, const std::vector<uint32_t>& cap)
+{
+    const size_t n = slot_region.size();
+    std::vector<SlotDesc> desc(n);
+    std::vector<uint32_t> rank(n);
+    for (size_t s = 0; s < n; ++s) {
+        const uint32_t r = slot_region[s];
+        desc[s] = SlotDesc{base[s], cap[s], (r % rx) | ((r / rx) << 16), 0u};
+        rank[r] = (uint32_t)s;
     }
-    bins.order = ctx->d_order;
-    bins.rank = ctx->d_order + (size_t)rx * ry;
+    XRT_HIP(ctx, hipDeviceSynchronize());
+    int rc;
+    if ((rc = ensure(ctx, L.d_desc, L.desc_cap, n))) return rc;
+    if ((rc = ensure(ctx, L.d_rank, L.rank_cap, n))) return rc;
+    XRT_HIP(ctx, hipMemcpy(L.d_desc, desc.data(), n * sizeof(SlotDesc), hipMemcpyHostToDevice));
+    XRT_HIP(ctx, hipMemcpy(L.d_rank, rank.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    L.slot_region = std::move(slot_region);
+    L.rx = rx;
+    L.ry = ry;
     return XRT_OK;
 }
 
-// Region (row-major index) of a launch slot under the base launch order
-// (launch_order's host copy; raster without one).
-inline uint32_t slot_to_region(const xrt_context* ctx, const BinBuffers& bins, uint32_t slot)
+// The fixed-capacity layout (centre-first order, `cap` entries per slot) of a
+// region grid: the first frame of a geometry bins into it.
+int fixed_layout(xrt_context* ctx, uint32_t rx, uint32_t ry, uint32_t cap, BinBuffers& bins)
 {
-    if (!bins.order) return slot;
-    const uint32_t xy = ctx->h_order[slot];
-    return (xy & 0xFFFFu) + (xy >> 16) * ctx->order_rx;
+    SlotLayout& L = ctx->fixed;
+    if (L.rx != rx || L.ry != ry || L.cap != cap || !L.d_desc) {
+        const size_t n = (size_t)rx * ry;
+        std::vector<uint32_t> base(n), caps(n, cap);
+        for (size_t s = 0; s < n; ++s) base[s] = (uint32_t)(s * cap);
+        int rc = upload_layout(ctx, L, rx, ry, centre_first_order(rx, ry), base, caps);
+        if (rc) return rc;
+        L.cap = cap;
+    }
+    bins.desc = L.d_desc;
+    bins.rank = L.d_rank;
+    return XRT_OK;
 }
 
-// The current geometry's fill plan as the launch order (DESIGN.md "Fill plan").
-// The signed model keeps the plan's order (the compact lists are sized by its
-// slots) but renders every region as tiles.
-void use_plan(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fill)
+// The current geometry's compact layout (its fill plan's order when there is
+// a plan, DESIGN.md "Fill plan").  The signed model keeps the plan's order (the
+// compact lists are sized by its slots) but renders every region as tiles.
+void use_compact(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fill)
 {
-    bins.order = ctx->d_plan;
-    bins.rank = ctx->d_plan + n_regions;
-    bins.tile_slots = fill ? ctx->plan_tile_slots : n_regions;
+    bins.desc = ctx->compact_layout.d_desc;
+    bins.rank = ctx->compact_layout.d_rank;
+    bins.tile_slots = fill && ctx->plan_valid ? ctx->plan_tile_slots : n_regions;
 }
 
-// Arms the k_prep check of a frame that uses the fill plan.
-void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool moving)
+// Arms the k_prep check of a frame that uses the fill plan or lists sized for
+// another camera.
+void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool reused)
 {
     bins.plan_miss = nullptr;
-    if (fs.plan_flag && (bins.tile_slots < n_regions || moving)) {
+    if (fs.plan_flag && (bins.tile_slots < n_regions || reused)) {
         fs.plan_flag[0] = 0u;
         fs.plan_flag[1] = 0u;
         bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
@@ -536,7 +552,6 @@ struct PendingFrame {
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
     HostClock::time_point t_call;
-    bool resized = false;              // prepared again after k_prep overflowed a list
 };
 
 int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
@@ -574,24 +589,13 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     // This frame's buffer set.  The render that last used it (kFrameSets
     // frames ago) must be complete before the set is prepared again.
     FrameSet& fs = ctx->sets[ctx->next_set];
-    // Where the preparation runs (DESIGN.md "Pipelining"; XRT_PIPELINE selects
-    // the others for A/B):
-    //   1 (default) on the context's prep stream, beside the previous frame's
-    //     render; the host waits for its completion before it launches the
-    //     render (no cross-queue event on the render queue);
-    //   2 on the caller's stream as an any-order dispatch (no barrier bit in
-    //     its AQL packet).  Measured: it did not overlap the previous render
-    //     on ROCm 7.2 -- the same per-frame time as serial;
-    //   0 serial on the caller's stream.
-    static const int pipeline = [] {
-        const char* e = std::getenv("XRT_PIPELINE");
-        return e ? std::atoi(e) : 1;
-    }();
-    hipStream_t ps = pipeline == 1 ? ctx->prep_stream : stream;
-    unsigned prep_flags = pipeline == 2 ? hipExtAnyOrderLaunch : 0u;
-    // The fill plan needs the host between k_prep and the render (the plan
-    // check) and the attenuation model (the signed render fills nothing).
-    const bool fill_ok = ps != stream && !signed_model;
+    // The preparation runs on the context's prep stream, beside the previous
+    // frame's render; the host waits for its completion before it launches
+    // the render (DESIGN.md "Pipelining": no cross-queue event on the render
+    // queue).  The fill plan needs the attenuation model (the signed render
+    // fills nothing).
+    hipStream_t ps = ctx->prep_stream;
+    const bool fill_ok = !signed_model;
     const auto t_call = HostClock::now();
     if (fs.done_valid) {
         const auto t = HostClock::now();
@@ -638,36 +642,48 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     key.T = T;
     key.gen = ctx->mesh_gen;
     // A new camera over the same region grid (a projection sweep) reuses the
-    // current lists and plan instead of the synchronous sizing: k_prep flags a
-    // pair binned into a planned-empty region, into the global list or past a
-    // list's capacity (BinBuffers::plan_miss), and that frame renders every
-    // region as tiles (exact) while the next one re-sizes.
-    static const bool camera_reuse = [] {
-        const char* e = std::getenv("XRT_CAMERA_REUSE");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    if (camera_reuse && binned && rows > 0 && fill_ok && ctx->bin_key_valid && ctx->compact &&
-        !ctx->bin_force_cap && !ctx->packed_cap && !key.same(ctx->bin_key) && key.same_layout(ctx->bin_key)) {
-        ctx->bin_key = key;
-        ctx->moving = true;
-        ++ctx->hp_reused;
+    // lists sized for an earlier camera instead of the synchronous sizing
+    // (DESIGN.md "Moving camera"), without a fill plan: k_prep flags a region
+    // count past its list's capacity, that region renders from the whole mesh
+    // (exact) and the next frame re-sizes.  A camera that then stays put for
+    // kStillFrames frames is sized for itself (tight lists and a fill plan).
+    // Contexts of xrt_render_rows_multi size every camera (reuse_cameras).
+    ctx->still_frames = key.same(ctx->last_key) ? ctx->still_frames + 1u : 0u;
+    ctx->last_key = key;
+    bool reuse = false;
+    if (binned && rows > 0 && fill_ok && ctx->bin_key_valid && ctx->compact && !ctx->bin_force_cap &&
+        !ctx->packed_cap) {
+        if (ctx->reuse_cameras && !key.same(ctx->bin_key) && key.same_layout(ctx->bin_key) &&
+            ctx->still_frames < kStillFrames) {
+            reuse = true;
+            ctx->moving = true;
+            ++ctx->hp_reused;
+        } else if (ctx->moving && ctx->still_frames >= kStillFrames) {
+            ctx->moving = false;           // the camera stopped: sized for it below
+            ctx->bin_key_valid = false;
+        }
     }
-    const bool new_geometry = binned && rows > 0 && (!ctx->bin_key_valid || !key.same(ctx->bin_key));
+    if (!key.same_layout(ctx->bin_key)) ctx->moving = false;
+    const bool new_geometry = binned && rows > 0 && !reuse && (!ctx->bin_key_valid || !key.same(ctx->bin_key));
     if (new_geometry) ctx->compact = false;
+    const uint32_t fixed_cap = ctx->bin_force_cap ? (uint32_t)std::min<size_t>(kInitialRegionCap, ctx->bin_force_cap)
+                                                  : kInitialRegionCap;
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
+        const bool compact = ctx->compact && !ctx->bin_force_cap;
         bool cleared = false;
-        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared))) return rc;
-        if (cleared) prep_flags = 0u;              // an any-order k_prep could start before the memset
-        if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
+        if ((rc = bin_buffers(ctx, fs, n_regions, compact ? ctx->slot_pool : (uint64_t)n_regions * fixed_cap, bins,
+                              bin_ctl, ps, cleared)))
+            return rc;
         bins.tile_slots = n_regions;
-        if (!new_geometry && ctx->compact && ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
-        arm_plan_check(fs, n_regions, bins, ctx->moving && fill_ok);
+        if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
+        else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+        arm_plan_check(fs, n_regions, bins, reuse);
     }
 
-    hipEvent_t prep_done = ps != stream ? fs.ready : nullptr;
-    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, prep_flags))) return rc;
+    hipEvent_t prep_done = fs.ready;
+    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     if (new_geometry && !ctx->bin_force_cap) {
         // Size the compact region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of every region's count, slot offsets
@@ -679,103 +695,49 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
                                     hipMemcpyDeviceToHost, ps));
         XRT_HIP(ctx, hipMemcpyAsync(&st, bin_ctl, sizeof st, hipMemcpyDeviceToHost, ps));
         XRT_HIP(ctx, hipStreamSynchronize(ps));
-        // The fill plan: the regions this frame counted empty (with an empty
-        // global list) go to the end of the launch order, one workgroup each.
-        // The slots are renumbered; the counts above are by the old slots.
-        std::vector<uint32_t> slot_region(n_regions);   // new slot -> region
-        for (uint32_t s = 0; s < n_regions; ++s) slot_region[s] = slot_to_region(ctx, bins, s);
+        const std::vector<uint32_t>& fixed_region = ctx->fixed.slot_region;   // the counts' slots
+        std::vector<uint32_t> count_of(n_regions);     // by region
+        for (uint32_t s = 0; s < n_regions; ++s) count_of[fixed_region[s]] = counts[(size_t)s * kCounterStride];
+        // The fill plan (not for a moving camera, whose next pose would miss it):
+        // the regions this frame counted empty (with an empty global list) go to
+        // the end of the launch order, one workgroup each; the tile regions by
+        // candidate count, heaviest first (their long tiles start first instead
+        // of setting the tail: render 2048^2 -6 %, 1024^2 -10 %).
+        std::vector<uint32_t> slot_region = fixed_region;
         uint32_t tile_slots = n_regions;
         const int plan = ctx->fill_plan;
-        if (plan != 0 && st.global_count == 0u && bins.order) {
-            std::vector<uint32_t> full, empty, full_count;
-            // A moving camera fills only regions whose 8 neighbours are empty too
-            // (the silhouette moves less than a region per small step).
-            std::vector<uint8_t> busy(n_regions, 0);
-            for (uint32_t s = 0; s < n_regions; ++s)
-                if (counts[(size_t)s * kCounterStride] != 0u) busy[slot_region[s]] = 1;
-            if (ctx->moving) {
-                std::vector<uint8_t> grown(busy);
-                for (uint32_t r = 0; r < n_regions; ++r) {
-                    if (!busy[r]) continue;
-                    const int x = (int)(r % rx), y = (int)(r / rx);
-                    for (int dy = -1; dy <= 1; ++dy)
-                        for (int dx = -1; dx <= 1; ++dx) {
-                            const int u = x + dx, v = y + dy;
-                            if (u >= 0 && v >= 0 && u < (int)rx && v < (int)ry) grown[(size_t)v * rx + u] = 1;
-                        }
-                }
-                busy.swap(grown);
-            }
-            for (uint32_t s = 0; s < n_regions; ++s) {
-                const uint32_t c = counts[(size_t)s * kCounterStride];
-                const bool fill = !busy[slot_region[s]] || plan == 2;
-                (fill ? empty : full).push_back(slot_region[s]);
-                if (!fill) full_count.push_back(c);
-            }
-            // tile regions by candidate count, heaviest first (their long tiles start
-            // first instead of setting the tail: render 2048^2 -6 %, 1024^2 -10 %;
-            // XRT_PLAN_HEAVY_FIRST=0 keeps the base order for A/B)
-            static const int heavy_first = [] {
-                const char* e = std::getenv("XRT_PLAN_HEAVY_FIRST");
-                return e ? std::atoi(e) : 1;
-            }();
-            if (heavy_first) {
-                std::vector<uint32_t> idx(full.size());
-                for (size_t k = 0; k < idx.size(); ++k) idx[k] = (uint32_t)k;
-                std::stable_sort(idx.begin(), idx.end(),
-                                 [&](uint32_t a, uint32_t b) { return full_count[a] > full_count[b]; });
-                std::vector<uint32_t> sorted(full.size());
-                for (size_t k = 0; k < idx.size(); ++k) sorted[k] = full[idx[k]];
-                full.swap(sorted);
-            }
+        if (plan != 0 && st.global_count == 0u && !ctx->moving) {
+            std::vector<uint32_t> full, empty;
+            for (uint32_t r : fixed_region) (count_of[r] != 0u && plan != 2 ? full : empty).push_back(r);
+            std::stable_sort(full.begin(), full.end(), [&](uint32_t a, uint32_t b) { return count_of[a] > count_of[b]; });
             tile_slots = (uint32_t)full.size();
             full.insert(full.end(), empty.begin(), empty.end());
             slot_region.swap(full);
         }
-        std::vector<uint32_t> count_of(n_regions);     // by region
-        for (uint32_t s = 0; s < n_regions; ++s)
-            count_of[slot_to_region(ctx, bins, s)] = counts[(size_t)s * kCounterStride];
-        std::vector<uint32_t> off(n_regions + 1u);
+        std::vector<uint32_t> base(n_regions), cap(n_regions);
         uint64_t run = 0;
         for (uint32_t s = 0; s < n_regions; ++s) {
-            off[s] = (uint32_t)run;
             const uint64_t c = count_of[slot_region[s]];
             // a moving camera: room for the counts of the next poses (2c + 64)
-            run += ctx->moving ? 2u * c + 64u : c + c / 8u + 4u;
+            const uint64_t room = ctx->moving ? 2u * c + 64u : c + c / 8u + 4u;
+            base[s] = (uint32_t)run;
+            cap[s] = (uint32_t)std::min<uint64_t>(room, 0xFFFFFFFFull);
+            run += room;
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
-        off[n_regions] = (uint32_t)run;
-        XRT_HIP(ctx, hipDeviceSynchronize());      // frames in flight may read the previous offsets
-        if ((rc = ensure(ctx, ctx->d_slot_off, ctx->slot_off_cap, off.size()))) return rc;
-        XRT_HIP(ctx, hipMemcpy(ctx->d_slot_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        ctx->plan_valid = false;
-        if (tile_slots < n_regions) {
-            // [slot -> region as (x | y << 16) | region -> slot], as launch_order's
-            std::vector<uint32_t> ord(2 * (size_t)n_regions);
-            for (uint32_t s = 0; s < n_regions; ++s) {
-                const uint32_t r = slot_region[s];
-                ord[s] = (r % rx) | ((r / rx) << 16);
-                ord[(size_t)n_regions + r] = s;
-            }
-            if ((rc = ensure(ctx, ctx->d_plan, ctx->plan_cap, ord.size()))) return rc;
-            XRT_HIP(ctx, hipMemcpy(ctx->d_plan, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-            ctx->plan_tile_slots = tile_slots;
-            ctx->plan_valid = true;
-            ctx->h_plan_region = slot_region;
-            ctx->plan_rx = rx;
-            ctx->plan_ry = ry;
-        }
+        if ((rc = upload_layout(ctx, ctx->compact_layout, rx, ry, std::move(slot_region), base, cap))) return rc;
+        ctx->plan_tile_slots = tile_slots;
+        ctx->plan_valid = tile_slots < n_regions;
         ctx->slot_pool = run;
         ctx->compact = true;
         ctx->bin_key = key;
         ctx->bin_key_valid = true;
         bool cleared = false;
-        if ((rc = bin_buffers(ctx, fs, n_regions, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
-        if ((rc = launch_order(ctx, rx, ry, bins))) return rc;
+        if ((rc = bin_buffers(ctx, fs, n_regions, run, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
         bins.tile_slots = n_regions;
-        if (ctx->plan_valid) use_plan(ctx, n_regions, bins, fill_ok);
-        arm_plan_check(fs, n_regions, bins, ctx->moving && fill_ok);
-        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done, 0u))) return rc;
+        use_compact(ctx, n_regions, bins, fill_ok);
+        arm_plan_check(fs, n_regions, bins, false);
+        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     }
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
     // one workgroup per region of the fill plan
@@ -830,27 +792,12 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     if (binned && bins.plan_miss && (fs.plan_flag[0] | fs.plan_flag[1]) != 0u) {
         // k_prep binned a pair into a region the plan fills, into the global
         // list or past a list's capacity: this frame renders every region as
-        // tiles (exact).  The next frame re-sizes -- except after a plan miss of
-        // a moving camera, whose lists still hold (the next camera would miss
-        // a fresh plan as likely: edge-on slivers turn into wide wedges).
-        const bool overflow = fs.plan_flag[1] != 0u;
-        ++(overflow ? ctx->hp_overflow : ctx->hp_plan_miss);
-        if (overflow && !pf.resized && ctx->bin_key_valid) {
-            // A region whose list overflowed would render from the whole mesh:
-            // size this frame's lists now (k_prep's counts are this camera's)
-            // and prepare it again.  The set is this frame's (not yet rotated).
-            ctx->bin_key_valid = false;
-            const xrt_camera cam = ctx->bin_key.cam;
-            PendingFrame again;
-            int rc = prepare_frame(ctx, &cam, ctx->bin_key.row_begin, ctx->bin_key.row_end, pf.out.image,
-                                   pf.out.lbuffer, pf.out.image_u8, stream, again);
-            if (rc) return rc;
-            again.resized = true;
-            return launch_frame(ctx, again);
-        }
+        // tiles (an overflowed region from the whole mesh -- exact, slower), and
+        // the next frame re-sizes its lists.
+        ++(fs.plan_flag[1] != 0u ? ctx->hp_overflow : ctx->hp_plan_miss);
         bins.tile_slots = rx * ry;
         grid = dim3(kWavesPerRegion / kTileWaves * bins.tile_slots);
-        if (overflow || !ctx->moving) ctx->bin_key_valid = false;
+        ctx->bin_key_valid = false;
     }
     ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
     if (pf.out.packed && rows > 0 &&
@@ -883,15 +830,6 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         ctx->tev_used += 2;
     }
     ctx->last_t0 = ctx->last_t1 = nullptr;
-    static const bool no_events = [] {      // A/B of the event cost only
-        const char* e = std::getenv("XRT_NO_EVENTS");
-        return e && std::atoi(e) != 0;
-    }();
-    if (no_events) {
-        if (sampled) ctx->tev_used -= 2;
-        t0 = nullptr;
-        t1 = fs.done;
-    }
     if (rows > 0) {
         const bool sgn = p.model == kModelSigned;
         const auto t_launch = HostClock::now();
@@ -912,7 +850,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         }
         fs.done_ev = t1;
         fs.done_valid = true;
-    } else if (sampled && !no_events) {
+    } else if (sampled) {
         ctx->tev_used -= 2;         // nothing launched, nothing to time
     }
     if (ctx->host_profile) {
@@ -967,14 +905,10 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
-    const char* fp = std::getenv("XRT_FILL");       // A/B: "0" = no fill plan
-    if (fp) ctx->fill_plan = std::atoi(fp);
     // The prep stream gets the highest queue priority: its small workgroups
     // must find CU slots while the previous frame's render fills the chip.
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-    const char* pp = std::getenv("XRT_PREP_PRIORITY");   // A/B only: "0" = default priority
-    if (pp && std::atoi(pp) == 0) prio_greatest = prio_least;
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess &&
               hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
@@ -1023,9 +957,10 @@ void xrt_destroy(xrt_context* ctx)
             if (e) (void)hipEventDestroy(e);
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
-    (void)hipFree(ctx->d_order);
-    (void)hipFree(ctx->d_plan);
-    (void)hipFree(ctx->d_slot_off);
+    for (SlotLayout* L : {&ctx->fixed, &ctx->compact_layout}) {
+        (void)hipFree(L->d_desc);
+        (void)hipFree(L->d_rank);
+    }
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
@@ -1262,15 +1197,16 @@ int xrt_plan_region_map(xrt_context* ctx, uint32_t width, uint32_t rows, uint32_
     const uint32_t rx = (width + kRegion - 1) / kRegion, ry = (rows + kRegion - 1) / kRegion;
     if (n_regions != (uint64_t)rx * ry)
         return fail(ctx, XRT_ERR_ARGUMENT, "map must hold ceil(width/32) x ceil(rows/32) regions");
-    const bool planned = ctx->last_fill_regions > 0 && ctx->plan_valid && ctx->plan_rx == rx &&
-                         ctx->plan_ry == ry && ctx->h_plan_region.size() == n_regions;
+    const SlotLayout& L = ctx->compact_layout;
+    const bool planned = ctx->last_fill_regions > 0 && ctx->plan_valid && L.rx == rx && L.ry == ry &&
+                         L.slot_region.size() == n_regions;
     if (!planned) {                                 // every region travels
         for (uint64_t r = 0; r < n_regions; ++r) map[r] = (uint32_t)r;
         *n_packed = (uint32_t)n_regions;
         return XRT_OK;
     }
     for (uint64_t s = 0; s < n_regions; ++s)
-        map[ctx->h_plan_region[s]] = s < ctx->plan_tile_slots ? (uint32_t)s : kEmpty;
+        map[L.slot_region[s]] = s < ctx->plan_tile_slots ? (uint32_t)s : kEmpty;
     *n_packed = ctx->plan_tile_slots;
     return XRT_OK;
 }
@@ -1332,6 +1268,16 @@ int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions)
 {
     if (!ctx || !regions) return XRT_ERR_ARGUMENT;
     *regions = ctx->last_fill_regions;
+    return XRT_OK;
+}
+
+int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
+{
+    if (!ctx || !counters) return XRT_ERR_ARGUMENT;
+    counters[0] = ctx->hp_sizings;
+    counters[1] = ctx->hp_reused;
+    counters[2] = ctx->hp_plan_miss;
+    counters[3] = ctx->hp_overflow;
     return XRT_OK;
 }
 

@@ -434,26 +434,32 @@ def test_fill_plan_changes_nothing(ctx, dragon, W, H, r0, r1):
 
 
 @pytest.mark.parametrize("W,H,r0,r1,degs", [
-    (512, 512, 0, None, [0, 1, 2, 3, 3.5, 10, 10, 45, 46, 90, 91, 0]),
-    (1000, 700, 0, None, [0, 0.5, 1, 1.5, 30, 30.5, 180, 181]),
-    (1024, 1024, 256, 700, [0, 1, 2, 20, 21, 22]),
+    (512, 512, 0, None, [0, 1, 2, 3, 3.5, 10, 10, 10, 45, 46, 90, 91, 0]),
+    (1000, 700, 0, None, [0, 0.5, 1, 1.5, 30, 30.5, 30.5, 30.5, 180, 181]),
+    (1024, 1024, 256, 700, [0, 1, 2, 20, 21, 22, 22, 22]),
 ])
 def test_moving_camera_reuses_lists_exactly(dragon, W, H, r0, r1, degs):
     """A projection sweep: each frame a new camera over the same region grid, so
-    the context keeps the previous sizing's lists and fill plan (no synchronous
-    re-sizing) and k_prep flags the frames the plan or a list capacity does not
-    hold (tiles, then a re-size).  Every frame is bit-identical, image, L-buffer,
-    u8 and hit statistics, to a fresh context's render of that camera."""
+    the context renders over the lists sized for an earlier camera (no
+    synchronous re-sizing, no fill plan), k_prep flags a list that overflows
+    (that region renders from the whole mesh, the next frame re-sizes), and a
+    camera that stays put for two frames more is sized for itself again (fill
+    plan back).  Every frame is bit-identical, image, L-buffer, u8 and hit
+    statistics, to a fresh context's brute-force render of that camera; the
+    geometry counters show which path each frame took."""
     lo, hi = xrt.mesh_bbox(dragon)
     centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
     base = xrt.camera_for_mesh(dragon, W, H)
     seq = xrt.Context(0)
     seq.set_kernel(xrt.XRT_KERNEL_BINNED)
     seq.upload_mesh(dragon)
-    fills = []
+    fills, paths = [], []
     for i, d in enumerate(degs):
         cam = orbit_camera(base, centre, d)
+        before = seq.geometry_counters()
         got = seq.render_rows(cam, r0, r1)
+        after = seq.geometry_counters()
+        paths.append({k: after[k] - before[k] for k in after})
         fills.append(seq.fill_regions())
         with xrt.Context(0) as fresh:
             fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
@@ -463,8 +469,40 @@ def test_moving_camera_reuses_lists_exactly(dragon, W, H, r0, r1, degs):
             assert np.array_equal(bits(x), bits(y)), (i, d)
         for f in ("rays", "hit_rays", "odd_rays", "max_hits"):
             assert getattr(got[3], f) == getattr(ref[3], f), (i, d, f)
+    total = seq.geometry_counters()
     seq.close()
-    assert any(fills[1:]), fills          # some frames of the sweep ran on a carried-over plan
+    assert paths[0]["sizings"] == 1 and fills[0] > 0, (paths[0], fills[0])
+    assert total["reused"] > 0 and total["sizings"] < len(degs), total
+    # reused frames run without a fill plan; the third frame in a row on one
+    # camera is sized for it (a fill plan again)
+    for i, p in enumerate(paths):
+        if p["reused"]:
+            assert fills[i] == 0 and p["sizings"] == 0, (i, p, fills[i])
+    still = max(i for i in range(2, len(degs)) if degs[i] == degs[i - 1] == degs[i - 2])
+    assert paths[still]["sizings"] == 1 and fills[still] > 0, (paths[still], fills[still])
+
+
+@pytest.mark.parametrize("devices", [[0, 0]])
+def test_multi_strips_orbit_exact(dragon, devices):
+    """xrt_render_rows_multi under a moving camera: its contexts size
+    every camera for itself; each gathered frame of a sweep equals a fresh
+    single-device brute-force render bit for bit."""
+    W, H = 1000, 777
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.MultiContext(devices) as multi:
+        multi.set_kernel(xrt.XRT_KERNEL_BINNED)
+        multi.upload_mesh(dragon)
+        for d in (0, 0.5, 1.0, 30, 30, 31):
+            cam = orbit_camera(base, centre, d)
+            got = multi.render(cam)
+            with xrt.Context(0) as fresh:
+                fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
+                fresh.upload_mesh(dragon)
+                ref = fresh.render_rows(cam)
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y)), d
 
 
 def test_global_list_and_fill_plan(ctx, dragon):
