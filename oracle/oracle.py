@@ -82,7 +82,9 @@ def ref_lib():
     global _ref
     if _ref is None:
         path = os.path.join(HERE, "_ref", "libxrt_ref.so")
-        if not os.path.exists(path):
+        # sanitizer runs (tools/san_check.sh): RTLD_DEEPBIND is incompatible with
+        # the sanitizer runtimes, and the reference's classes are not this repo's code
+        if not os.path.exists(path) or os.environ.get("XRT_ORACLE_NO_REF"):
             return None
         # RTLD_DEEPBIND: the reference's classes (TriangleMesh, Vec3, ...) bind
         # to their own definitions, not to the same-named drop-in classes of
