@@ -300,6 +300,20 @@ int xrt_multi_set_model(xrt_multi* m, int model, float mu);
 /* Waits for the last frame's gathers; the devices' statistics, summed. */
 int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
 
+/*
+ * How the strips reach device 0.  XRT_GATHER_AUTO (the default): RCCL when
+ * every listed device is distinct, device copies when one is listed twice.
+ * XRT_GATHER_RCCL on a list that names ONE device n times (a one-GPU
+ * rehearsal) gathers through a one-rank RCCL communicator on that device --
+ * grouped ncclSend / ncclRecv from the rank to itself, the same calls and
+ * stream order as the distinct-device gather.  XRT_GATHER_COPY forces copies.
+ * A list that mixes repeated and distinct devices gathers with copies.
+ */
+#define XRT_GATHER_AUTO 0
+#define XRT_GATHER_COPY 1
+#define XRT_GATHER_RCCL 2
+int xrt_multi_set_gather(xrt_multi* m, int mode);
+
 /* --- diagnostics (device probes of the exact device code paths) ----------- */
 
 /*

@@ -20,13 +20,13 @@ import numpy as np
 from . import _abi
 from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
                    XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT, XRT_MODEL_ATTENUATION,
-                   XRT_MODEL_SIGNED)
+                   XRT_MODEL_SIGNED, XRT_GATHER_AUTO, XRT_GATHER_COPY, XRT_GATHER_RCCL)
 
 __all__ = [
     "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
     "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT", "load_meshes", "scene_bbox", "camera_for_scene",
-    "XRT_MODEL_ATTENUATION", "XRT_MODEL_SIGNED",
+    "XRT_MODEL_ATTENUATION", "XRT_MODEL_SIGNED", "XRT_GATHER_AUTO", "XRT_GATHER_COPY", "XRT_GATHER_RCCL",
 ]
 
 
@@ -376,6 +376,11 @@ class MultiContext:
 
     def set_kernel(self, kernel: int):
         self._check(self._lib.xrt_multi_set_kernel(self._m, int(kernel)), "xrt_multi_set_kernel")
+
+    def set_gather(self, mode: int):
+        """XRT_GATHER_AUTO / _COPY / _RCCL (a one-rank RCCL communicator when one
+        device is listed n times)."""
+        self._check(self._lib.xrt_multi_set_gather(self._m, int(mode)), "xrt_multi_set_gather")
 
     def set_model(self, model: int, mu: float = 0.1037):
         self._check(self._lib.xrt_multi_set_model(self._m, int(model), float(np.float32(mu))), "xrt_multi_set_model")

@@ -36,6 +36,10 @@ XRT_PROBE_SIGNED_L = 5
 XRT_MODEL_ATTENUATION = 0
 XRT_MODEL_SIGNED = 1
 
+XRT_GATHER_AUTO = 0
+XRT_GATHER_COPY = 1
+XRT_GATHER_RCCL = 2
+
 XRT_IMAGE_TEXT = 0
 XRT_IMAGE_TGA = 1
 XRT_IMAGE_PGM = 2
@@ -154,6 +158,7 @@ XRT_SYMBOLS = {
                                              ctypes.POINTER(Stats)]),
     "xrt_render_rows_multi_device": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _vp, _vp, _vp, _vp]),
     "xrt_multi_read_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(Stats)]),
+    "xrt_multi_set_gather": (ctypes.c_int, [_MultiP, ctypes.c_int]),
 }
 
 # every C symbol declared in include/xrt_host.h

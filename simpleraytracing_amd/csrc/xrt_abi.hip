@@ -524,12 +524,18 @@ void use_compact(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fi
     bins.tile_slots = fill && ctx->plan_valid ? ctx->plan_tile_slots : n_regions;
 }
 
-// Arms the k_prep check of a frame that uses the fill plan or lists sized for
-// another camera.
-void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool reused)
+// Arms the k_prep check of a frame whose region lists or fill plan k_prep's
+// binning has not yet been seen to match: the first frame over a new plan
+// (`validate`) and frames over lists sized for another camera (`reused`).
+// The binning of a frame geometry (mesh, camera, strip) is deterministic --
+// the same footprints join the same regions, only the order of a list's
+// entries varies with the atomics -- so later frames of a validated geometry
+// cannot miss it and are launched without the host reading the check
+// (DESIGN.md "Pipelining").
+void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool reused, bool validate)
 {
     bins.plan_miss = nullptr;
-    if (fs.plan_flag && (bins.tile_slots < n_regions || reused)) {
+    if (fs.plan_flag && ((validate && bins.tile_slots < n_regions) || reused)) {
         fs.plan_flag[0] = 0u;
         fs.plan_flag[1] = 0u;
         bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
@@ -542,7 +548,11 @@ void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool reu
 struct PendingFrame {
     FrameSet* fs = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t prep_done = nullptr;    // host waits for it before the launch (prep stream)
+    hipEvent_t prep_done = nullptr;    // k_prep complete (prep stream)
+    // The host waits for prep_done and reads k_prep's check before the launch
+    // (a sizing frame, a frame with the check armed); otherwise the render's
+    // queue waits for prep_done on the device and the host runs ahead.
+    bool host_wait = false;
     int kernel = XRT_KERNEL_AUTO;
     bool binned = false;
     uint32_t rows = 0, rx = 0, ry = 0;
@@ -679,7 +689,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.tile_slots = n_regions;
         if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
-        arm_plan_check(fs, n_regions, bins, reuse);
+        // the fill plan's test hook (every region planned empty) is checked every frame
+        arm_plan_check(fs, n_regions, bins, reuse, ctx->fill_plan == 2);
     }
 
     hipEvent_t prep_done = fs.ready;
@@ -736,7 +747,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = bin_buffers(ctx, fs, n_regions, run, bins, bin_ctl, ps, cleared, true))) return rc;   // clears
         bins.tile_slots = n_regions;
         use_compact(ctx, n_regions, bins, fill_ok);
-        arm_plan_check(fs, n_regions, bins, false);
+        arm_plan_check(fs, n_regions, bins, false, true);
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     }
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
@@ -753,6 +764,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     pf.fs = &fs;
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
+    pf.host_wait = bins.plan_miss != nullptr;
     pf.kernel = kernel;
     pf.binned = binned;
     pf.rows = rows;
@@ -779,13 +791,16 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     BinState* bin_ctl = pf.bin_ctl;
     const auto t_call = pf.t_call;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
-    // The render is launched once the preparation is complete (host-side
-    // order; the caller's queue never waits on the prep queue).
-    if (pf.prep_done) {
-        hipEvent_t prep_done = pf.prep_done;
+    // The render runs once its preparation is complete: the caller's queue
+    // waits for it on the device (a barrier packet, ~2.4 us per frame), or --
+    // when the host must read k_prep's check to choose the grid -- the host
+    // waits for it before the launch.
+    if (pf.prep_done && pf.host_wait) {
         const auto t = HostClock::now();
-        XRT_HIP(ctx, hipEventSynchronize(prep_done));
+        XRT_HIP(ctx, hipEventSynchronize(pf.prep_done));
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
+    } else if (pf.prep_done) {
+        XRT_HIP(ctx, hipStreamWaitEvent(stream, pf.prep_done, 0));
     }
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;

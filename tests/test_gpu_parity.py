@@ -718,6 +718,29 @@ def test_multi_strips_equal_single_frame(dragon, devices, W, H):
         assert np.array_equal(bits(got[0]), bits(o[0]))
 
 
+@pytest.mark.parametrize("devices,W,H", [([0, 0], 160, 131), ([0, 0, 0], 1000, 777)])
+def test_multi_rccl_gather_one_rank(dragon, devices, W, H):
+    """The RCCL gather itself on one GPU: XRT_GATHER_RCCL over one device listed
+    n times builds a one-rank communicator (ncclCommInitAll) and moves every
+    strip with the grouped ncclSend / ncclRecv of the distinct-device gather
+    (the rank sends to itself).  Packed regions at 1000 x 777; bit-equal to one
+    device's frame, frames in rotation, then back to the copy gather."""
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        ref = one.render_rows(cam)
+    with xrt.MultiContext(devices) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        for mode in (xrt.XRT_GATHER_RCCL, xrt.XRT_GATHER_COPY, xrt.XRT_GATHER_RCCL):
+            m.set_gather(mode)
+            for _ in range(3):                          # the strip buffers rotate
+                got = m.render(cam)
+                for x, y in zip(got[:3], ref[:3]):
+                    assert np.array_equal(bits(x), bits(y))
+
+
 def test_multi_device_pipelined(dragon):
     """xrt_render_rows_multi_device: frames enqueued back to back into torch
     device planes (the next frame's strips render while the last one's gather is
