@@ -441,6 +441,16 @@ int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
 int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4]);
 
 /*
+ * Diagnostics: the frame pipeline since the context was created --
+ * counters[0] frames rendered from a preparation made ahead of their call
+ * (xrt_render_rows_device repeating its frame geometry), [1] preparations made
+ * ahead and dropped (the next call's geometry or settings differed), [2]
+ * renders launched with their preparation already complete (no wait), [3]
+ * renders launched after the host read k_prep's check (sizing / validation).
+ */
+int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4]);
+
+/*
  * Diagnostics: copies the last render's statistics records (32 bytes each, one
  * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
  * overflow rays, hits, wave-level triangle tests, candidates, max hits; builds

@@ -223,6 +223,13 @@ class Context:
         self._check(self._lib.xrt_debug_geometry_counters(self._ctx, c), "xrt_debug_geometry_counters")
         return dict(zip(("sizings", "reused", "plan_misses", "overflows"), (int(v) for v in c)))
 
+    def pipeline_counters(self) -> dict:
+        """Frames rendered from a preparation made ahead, preparations dropped, renders
+        launched with no wait, renders launched after a host wait (xrt_debug_pipeline_counters)."""
+        c = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.xrt_debug_pipeline_counters(self._ctx, c), "xrt_debug_pipeline_counters")
+        return dict(zip(("ahead_used", "ahead_dropped", "no_wait", "host_waits"), (int(v) for v in c)))
+
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
                     image=True, lbuffer=True, u8=True):
         """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats)."""

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <string>
 #include <vector>
@@ -33,6 +34,11 @@ constexpr int kFrameSets = 4;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
+// Frames prepared ahead of their call when a device-pointer render repeats
+// its geometry (xrt_context::ahead); with kFrameSets sets, two renders can be
+// in flight beside them.
+constexpr size_t kAheadFrames = 2;
+static_assert(kAheadFrames + 2 <= (size_t)kFrameSets, "sets for the renders in flight and the frames ahead");
 
 
 // Everything one frame's preparation writes and its render reads or writes.
@@ -101,6 +107,29 @@ struct SlotLayout {
     size_t rank_cap = 0;
     std::vector<uint32_t> slot_region;
     uint32_t rx = 0, ry = 0, cap = 0;  // the fixed-capacity layout's key
+};
+
+// A frame between its preparation (enqueued) and its render launch.  Split so
+// that a multi-device render can enqueue every device's preparation before it
+// waits for any (xrt_render_rows_multi).
+struct PendingFrame {
+    FrameSet* fs = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t prep_done = nullptr;    // k_prep complete (prep stream)
+    // The host waits for prep_done and reads k_prep's check before the launch
+    // (a sizing frame, a frame with the check armed); otherwise the render's
+    // queue waits for prep_done on the device and the host runs ahead.
+    bool host_wait = false;
+    bool ahead = false;                // prepared ahead of its call (xrt_context::ahead)
+    int kernel = XRT_KERNEL_AUTO;
+    bool binned = false;
+    uint32_t rows = 0, rx = 0, ry = 0;
+    dim3 grid;
+    RenderParams p;
+    Outputs out;
+    BinBuffers bins = {};
+    BinState* bin_ctl = nullptr;
+    HostClock::time_point t_call;
 };
 
 struct xrt_context {
@@ -182,6 +211,25 @@ struct xrt_context {
     bool reuse_cameras = true;         // false for xrt_render_rows_multi's contexts
     BinKey last_key = {};              // the last frame's geometry
     uint32_t still_frames = 0;         // frames in a row on one camera over reused lists
+    // Prepare-ahead (DESIGN.md "Pipelining"): when a device-pointer render
+    // repeats the previous call's frame geometry, the preparations of the next
+    // kAheadFrames frames of that geometry are enqueued at once on the prep
+    // stream; a later call whose geometry and settings match takes the oldest
+    // (its k_prep then ran beside earlier renders and is complete: the render
+    // is launched with no wait at all).  Any mismatch drops them (their k_prep
+    // runs, on the prep stream, before any newer one).  state_gen counts the
+    // setting changes a prepared frame depends on.
+    struct AheadFrame {
+        PendingFrame pf;
+        BinKey key;
+        uint64_t state_gen;
+        uint32_t outs;                 // which output planes (image 1, L-buffer 2, u8 4)
+    };
+    std::deque<AheadFrame> ahead;
+    uint64_t state_gen = 0;
+    BinKey call_key = {};              // the last device-pointer call's geometry
+    uint64_t call_state_gen = ~0ull;
+    uint64_t hp_ahead_used = 0, hp_ahead_dropped = 0, hp_launch_nowait = 0, hp_host_waits = 0;
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     uint32_t model = kModelAttenuation;   // xrt_set_model
     float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
@@ -542,30 +590,9 @@ void arm_plan_check(FrameSet& fs, uint32_t n_regions, BinBuffers& bins, bool reu
     }
 }
 
-// A frame between its preparation (enqueued) and its render launch.  Split so
-// that a multi-device render can enqueue every device's preparation before it
-// waits for any (xrt_render_rows_multi).
-struct PendingFrame {
-    FrameSet* fs = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t prep_done = nullptr;    // k_prep complete (prep stream)
-    // The host waits for prep_done and reads k_prep's check before the launch
-    // (a sizing frame, a frame with the check armed); otherwise the render's
-    // queue waits for prep_done on the device and the host runs ahead.
-    bool host_wait = false;
-    int kernel = XRT_KERNEL_AUTO;
-    bool binned = false;
-    uint32_t rows = 0, rx = 0, ry = 0;
-    dim3 grid;
-    RenderParams p;
-    Outputs out;
-    BinBuffers bins = {};
-    BinState* bin_ctl = nullptr;
-    HostClock::time_point t_call;
-};
-
 int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
-                  float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream, PendingFrame& pf)
+                  float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream, PendingFrame& pf,
+                  int set_index = -1)
 {
     int rc = check_camera(ctx, cam, row_begin, row_end);
     if (rc) return rc;
@@ -598,7 +625,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
 
     // This frame's buffer set.  The render that last used it (kFrameSets
     // frames ago) must be complete before the set is prepared again.
-    FrameSet& fs = ctx->sets[ctx->next_set];
+    FrameSet& fs = ctx->sets[set_index < 0 ? ctx->next_set : set_index];
     // The preparation runs on the context's prep stream, beside the previous
     // frame's render; the host waits for its completion before it launches
     // the render (DESIGN.md "Pipelining": no cross-queue event on the render
@@ -798,9 +825,15 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     if (pf.prep_done && pf.host_wait) {
         const auto t = HostClock::now();
         XRT_HIP(ctx, hipEventSynchronize(pf.prep_done));
+        ++ctx->hp_host_waits;
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
     } else if (pf.prep_done) {
-        XRT_HIP(ctx, hipStreamWaitEvent(stream, pf.prep_done, 0));
+        // a preparation already complete needs no wait packet (a frame prepared
+        // ahead usually is); hipErrorNotReady otherwise
+        const hipError_t q = hipEventQuery(pf.prep_done);
+        if (q == hipSuccess) ++ctx->hp_launch_nowait;
+        else if (q == hipErrorNotReady) XRT_HIP(ctx, hipStreamWaitEvent(stream, pf.prep_done, 0));
+        else XRT_HIP(ctx, q);
     }
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;
@@ -875,19 +908,78 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         ++ctx->hp_calls;
     }
     ctx->last_set = &fs;
-    ctx->next_set = (ctx->next_set + 1) % kFrameSets;
+    ctx->next_set = (int)((&fs - ctx->sets) + 1) % kFrameSets;
     ctx->last_stream = stream;
     ctx->pending = true;
     ctx->last_kernel = kernel;
     return XRT_OK;
 }
 
-int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
-                   float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream)
+xrt_context::BinKey geometry_key(const xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin,
+                                 uint32_t row_end)
 {
+    xrt_context::BinKey key = {};
+    key.cam = *cam;
+    key.row_begin = row_begin;
+    key.row_end = row_end;
+    key.T = ctx->num_tris;
+    key.gen = ctx->mesh_gen;
+    return key;
+}
+
+// One frame: its preparation (or the one prepared ahead for it) and its
+// render; `ahead` (the pipelined device-pointer entry) prepares the next
+// frames of a repeated geometry ahead of their calls (xrt_context::ahead).
+int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, uint32_t row_end,
+                   float* d_image, float* d_lbuffer, uint8_t* d_u8, hipStream_t stream, bool ahead = false)
+{
+    int rc = check_camera(ctx, cam, row_begin, row_end);
+    if (rc) return rc;
+    const xrt_context::BinKey key = geometry_key(ctx, cam, row_begin, row_end);
+    const uint32_t outs = (d_image ? 1u : 0u) | (d_lbuffer ? 2u : 0u) | (d_u8 ? 4u : 0u);
     PendingFrame pf;
-    int rc = prepare_frame(ctx, cam, row_begin, row_end, d_image, d_lbuffer, d_u8, stream, pf);
-    return rc ? rc : launch_frame(ctx, pf);
+    bool taken = false;
+    if (!ctx->ahead.empty()) {
+        xrt_context::AheadFrame& a = ctx->ahead.front();
+        if (ahead && a.key.same(key) && a.state_gen == ctx->state_gen && a.outs == outs) {
+            pf = a.pf;
+            ctx->ahead.pop_front();
+            pf.stream = stream;
+            pf.out.image = d_image;
+            pf.out.lbuffer = d_lbuffer;
+            pf.out.image_u8 = d_u8;
+            pf.t_call = HostClock::now();
+            taken = true;
+            ++ctx->hp_ahead_used;
+        } else {                       // their k_prep runs before any newer one (prep stream)
+            ctx->hp_ahead_dropped += ctx->ahead.size();
+            ctx->ahead.clear();
+        }
+    }
+    if (!taken && (rc = prepare_frame(ctx, cam, row_begin, row_end, d_image, d_lbuffer, d_u8, stream, pf)))
+        return rc;
+    const bool repeated = ahead && key.same(ctx->call_key) && ctx->call_state_gen == ctx->state_gen;
+    ctx->call_key = key;
+    ctx->call_state_gen = ahead ? ctx->state_gen : ~0ull;
+    if ((rc = launch_frame(ctx, pf))) return rc;
+    // the next frames of a repeated geometry, prepared now (a steady frame:
+    // no sizing, no check to read on the host)
+    if (repeated && !pf.host_wait && pf.rows > 0) {
+        while (ctx->ahead.size() < kAheadFrames) {
+            xrt_context::AheadFrame a;
+            a.key = key;
+            a.state_gen = ctx->state_gen;
+            a.outs = outs;
+            const int set = (int)((ctx->next_set + ctx->ahead.size()) % kFrameSets);
+            if ((rc = prepare_frame(ctx, cam, row_begin, row_end, d_image, d_lbuffer, d_u8, stream, a.pf, set))) {
+                ctx->ahead.clear();
+                return rc;
+            }
+            a.pf.ahead = true;
+            ctx->ahead.push_back(a);
+        }
+    }
+    return XRT_OK;
 }
 
 }  // namespace
@@ -951,9 +1043,11 @@ void xrt_destroy(xrt_context* ctx)
                      ctx->hp_gap / ctx->hp_calls * 1e6);
     if (ctx->host_profile && ctx->hp_calls)
         std::fprintf(stderr, "xrt geometry: %llu sizings, %llu camera reuses; frames flagged by k_prep: %llu plan "
-                     "misses, %llu list overflows\n", (unsigned long long)ctx->hp_sizings,
+                     "misses, %llu list overflows; prepared ahead: %llu used, %llu dropped; renders launched "
+                     "without a wait: %llu\n", (unsigned long long)ctx->hp_sizings,
                      (unsigned long long)ctx->hp_reused, (unsigned long long)ctx->hp_plan_miss,
-                     (unsigned long long)ctx->hp_overflow);
+                     (unsigned long long)ctx->hp_overflow, (unsigned long long)ctx->hp_ahead_used,
+                     (unsigned long long)ctx->hp_ahead_dropped, (unsigned long long)ctx->hp_launch_nowait);
     (void)hipSetDevice(ctx->device);
     if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
     (void)hipDeviceSynchronize();
@@ -1004,6 +1098,7 @@ int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_trian
                                hipMemcpyHostToDevice));
     ctx->num_tris = num_triangles;
     ++ctx->mesh_gen;
+    ++ctx->state_gen;
     return XRT_OK;
 }
 
@@ -1089,6 +1184,7 @@ int xrt_set_kernel(xrt_context* ctx, int kernel)
     if (kernel < XRT_KERNEL_AUTO || kernel > XRT_KERNEL_BINNED)
         return fail(ctx, XRT_ERR_ARGUMENT, "unknown kernel");
     ctx->kernel = kernel;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1099,6 +1195,7 @@ int xrt_set_model(xrt_context* ctx, int model, float mu)
         return fail(ctx, XRT_ERR_ARGUMENT, "unknown model");
     ctx->model = (uint32_t)model;
     ctx->mu = mu;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1172,6 +1269,7 @@ int xrt_set_miss_code(xrt_context* ctx, uint32_t bits)
     if (!ctx) return XRT_ERR_ARGUMENT;
     if (bits && bits != kMissTransit) return fail(ctx, XRT_ERR_ARGUMENT, "miss code must be 0 or XRT_MISS_TRANSIT");
     ctx->miss_code = bits;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1195,6 +1293,7 @@ int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity)
     if (capacity > (uint32_t)kMaxHits)
         return fail(ctx, XRT_ERR_ARGUMENT, "capacity > " + std::to_string(kMaxHits));
     ctx->hit_capacity = capacity ? capacity : (uint32_t)kMaxHits;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1202,6 +1301,7 @@ int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->bin_force_cap = (size_t)entries;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1276,6 +1376,7 @@ int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->packed_cap = packed_floats;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1296,6 +1397,16 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     return XRT_OK;
 }
 
+int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4])
+{
+    if (!ctx || !counters) return XRT_ERR_ARGUMENT;
+    counters[0] = ctx->hp_ahead_used;
+    counters[1] = ctx->hp_ahead_dropped;
+    counters[2] = ctx->hp_launch_nowait;
+    counters[3] = ctx->hp_host_waits;
+    return XRT_OK;
+}
+
 int xrt_set_fill_plan(xrt_context* ctx, int mode)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
@@ -1303,6 +1414,7 @@ int xrt_set_fill_plan(xrt_context* ctx, int mode)
     ctx->fill_plan = mode;
     ctx->bin_key_valid = false;         // the next frame re-sizes and re-plans
     ctx->plan_valid = false;
+    ++ctx->state_gen;                   // frames prepared ahead are stale
     return XRT_OK;
 }
 
@@ -1341,7 +1453,7 @@ int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t 
 {
     if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
     return enqueue_render(ctx, camera, row_begin, row_end, d_image, d_lbuffer, d_u8,
-                          (hipStream_t)stream);
+                          (hipStream_t)stream, true);
 }
 
 int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
@@ -1379,8 +1491,10 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
         BinState bs = {};
         XRT_HIP(ctx, hipMemcpy(&bs, fs->last_state, sizeof bs, hipMemcpyDeviceToHost));
         stats->global_triangles = bs.global_count;
-        if (bs.overflow && !ctx->bin_force_cap)   // the next frame re-sizes its lists
+        if (bs.overflow && !ctx->bin_force_cap) {  // the next frame re-sizes its lists
             ctx->bin_key_valid = false;
+            ++ctx->state_gen;
+        }
     }
     return XRT_OK;
 }

@@ -608,6 +608,62 @@ def test_device_buffers_and_timing(ctx, dragon):
     assert st.rays == W * H
 
 
+@pytest.mark.parametrize("W,H,r0,r1,kernel", [(512, 512, 0, 512, xrt.XRT_KERNEL_BINNED),
+                                               (1000, 777, 100, 700, xrt.XRT_KERNEL_BINNED),
+                                               (192, 192, 0, 192, xrt.XRT_KERNEL_TILED)])
+def test_prepared_ahead_frames_exact(dragon, W, H, r0, r1, kernel):
+    """Prepare-ahead (DESIGN.md "Pipelining"): device-pointer frames that repeat
+    their geometry are rendered from preparations enqueued during earlier calls;
+    a change of camera, of a setting (hit capacity, miss code) or a host-buffer
+    call in between drops them.  Every frame of the sequence -- each into its
+    own planes, no host sync until the end -- is bit-identical to a fresh
+    brute-force render of its camera, and the pipeline counters show frames
+    taken from ahead, dropped preparations and renders launched with no wait."""
+    import torch
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    cams = {"A": base, "B": orbit_camera(base, centre, 40.0)}
+    refs = {}
+    for name, cam in cams.items():
+        with xrt.Context(0) as fresh:
+            fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
+            fresh.upload_mesh(dragon)
+            refs[name] = fresh.render_rows(cam, r0, r1)
+    seq = "AAAAAA" + "BBBBB" + "h" + "BBBB" + "x" + "BBBB" + "AAAAAAAA"
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    n = (r1 - r0) * W
+    outs = []
+    with xrt.Context(0) as ctx:
+        ctx.set_kernel(kernel)
+        ctx.upload_mesh(dragon)
+        with torch.cuda.stream(stream):
+            for step in seq:
+                if step == "h":                       # a setting change between device frames
+                    ctx.set_hit_capacity(5)
+                    continue
+                if step == "x":                       # a host-buffer render in between
+                    got = ctx.render_rows(cams["B"], r0, r1)
+                    assert np.array_equal(bits(got[1]), bits(refs["B"][1]))
+                    continue
+                planes = (torch.empty(n, dtype=torch.float32, device=dev),
+                          torch.empty(n, dtype=torch.float32, device=dev),
+                          torch.empty(n, dtype=torch.uint8, device=dev))
+                ctx.render_rows_device(cams[step], r0, r1, planes[0].data_ptr(), planes[1].data_ptr(),
+                                       planes[2].data_ptr(), stream.cuda_stream)
+                outs.append((step, planes))
+        stream.synchronize()
+        pc = ctx.pipeline_counters()
+        st = ctx.read_stats()
+    for i, (step, planes) in enumerate(outs):
+        ref = refs[step]
+        for x, y in zip(planes, ref[:3]):
+            assert np.array_equal(bits(x.cpu().numpy()), bits(y)), (i, step)
+    assert st.hit_rays == refs["A"][3].hit_rays and st.odd_rays == refs["A"][3].odd_rays
+    assert pc["ahead_used"] >= 8 and pc["ahead_dropped"] >= 4 and pc["no_wait"] > 0, pc
+
+
 def test_pipelined_frames_without_sync(ctx, dragon):
     """Many frames enqueued back to back on one stream with no host sync --
     different cameras, image sizes, strips, kernels and output buffers, so the

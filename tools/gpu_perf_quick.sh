@@ -17,7 +17,7 @@ fi
 i=0
 CFGS=("$@")
 if [ ${#CFGS[@]} -eq 0 ]; then
-  CFGS=("--size 1024 1024" "--size 2048 2048" "--size 4096 4096" "--size 8192 8192 --tile-mesh 7 --steps 20 --warmup 3")
+  CFGS=("--size 1024 1024" "--size 2048 2048" "--size 4096 4096" "--size 8192 8192 --tile-mesh 7 --steps 100 --warmup 10")
 fi
 for cfg in "${CFGS[@]}"; do
   i=$((i+1))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-kernel VGPR/SGPR/LDS/occupancy of libxrt's kernels (compiler remarks).
 cd "$(dirname "$0")/../simpleraytracing_amd/csrc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -fno-fast-math \
     -I../../include "$@" --cuda-device-only -c -o /dev/null xrt_abi.hip -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys
