@@ -91,7 +91,7 @@ typedef struct xrt_stats {
     uint64_t hits;          /* total recorded intersections */
     uint32_t max_hits;      /* largest per-ray hit count */
     uint32_t kernel;        /* xrt_kernel actually used */
-    double kernel_ms;       /* device time of the main render kernel (HIP events) */
+    double kernel_ms;       /* the last render kernel's span (its waves' s_memrealtime records) */
     uint64_t candidates;    /* TILED: triangles kept by the region footprint test, summed over regions */
     uint64_t tile_tests;    /* triangle tests issued per 8x8 wave tile (64 ray-triangle tests each) */
     uint64_t global_triangles; /* BINNED: footprints too large for the region lists (every region's candidates) */
@@ -160,13 +160,18 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
 
 /*
  * Same with DEVICE buffers on HIP stream `stream` (hipStream_t, NULL = default
- * stream).  Asynchronous with respect to the render: returns once the render
- * is enqueued.  The frame's preparation (k_prep, on the context's own prep
- * stream, overlapping earlier renders) has completed by then -- the call waits
- * for it, typically tens of microseconds -- and when four frames are already
- * in flight the call first waits for the oldest of them.  Call
- * xrt_read_stats() (which synchronises the stream) for counters and kernel
- * time.
+ * stream).  Asynchronous: returns once the render is enqueued.  The frame's
+ * preparation (k_prep) runs on the context's own prep stream, beside earlier
+ * renders; the render waits for it on the device.  The host waits only when
+ * the frame geometry is new (its region lists are sized from a synchronous
+ * count, and the first frame over them is checked), when the frame reuses
+ * lists sized for another camera (k_prep's check decides its launch), and
+ * when four frames are already in flight (for the oldest).  When a call
+ * repeats the previous call's frame geometry (mesh, camera, rows) and
+ * settings, the preparations of the next two frames of that geometry are
+ * enqueued at once; a later call that matches takes one (rendered with no
+ * wait), any other call drops them.  Call xrt_read_stats() (which
+ * synchronises the stream) for counters and kernel time.
  */
 int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
                            uint32_t row_end, float* d_image, float* d_lbuffer,
@@ -175,13 +180,19 @@ int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t 
 int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
 
 /*
- * Kernel timing over a region of many renders without host synchronisation:
- * after xrt_timing_begin, every render records a HIP event pair around its
- * main render kernel on the render's stream; xrt_timing_end synchronises on the
- * last event and returns the summed kernel time and the number of launches.
+ * Kernel timing over a region of many renders without host synchronisation.
+ * Every render's waves store their s_memrealtime start and end beside their
+ * statistics records (xrt_stats::kernel_ms is the last frame's span: last end -
+ * first start).  After xrt_timing_begin, every render keeps its records apart
+ * (up to 2^27 records, 1 GiB, per region); xrt_timing_end synchronises the
+ * device and returns the summed spans of those renders and their number.  Every 16th render of the region also
+ * carries a HIP start/stop event pair on its dispatch: xrt_timing_events
+ * returns their summed durations and number (a cross-check; a start event
+ * costs its frame a few microseconds).
  */
 int xrt_timing_begin(xrt_context* ctx);
 int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches);
+int xrt_timing_events(xrt_context* ctx, double* total_ms, uint64_t* launches);
 
 /* --- strips in transit ---------------------------------------------------- */
 
@@ -453,19 +464,21 @@ int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4]);
 /*
  * Diagnostics: copies the last render's statistics records (32 bytes each, one
  * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
- * overflow rays, hits, wave-level triangle tests, candidates, max hits; builds
- * with XRT_STAMPS put u64 start/end timestamps and hardware ids there instead)
+ * overflow rays, hits, wave-level triangle tests, candidates, max hits)
  * into `dst`, at most `capacity` bytes; `*n_records` receives the number of
  * records.
  */
 int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint64_t* n_records);
 
 /*
- * Diagnostics: copies up to `n` u64 phase timestamps (s_memrealtime, 100 MHz)
- * of the last frame's binning kernels into `dst` (layout in xrt_kernels.h,
- * XRT_STAMP_*).  Builds without XRT_STAMPS return zeros.
+ * Diagnostics: the timing records of the render `frames_back` frames before
+ * the last (0 = the last; up to 3, outside timed regions), one per statistics
+ * record (u32 s_memrealtime start, u32 end; 100 MHz, low 32 bits), into `dst`,
+ * at most `capacity` records; `*n_records` receives their number.
  */
-int xrt_debug_stamps(xrt_context* ctx, uint64_t* dst, uint64_t n);
+int xrt_debug_wave_times(xrt_context* ctx, uint32_t frames_back, uint32_t* dst, uint64_t capacity,
+                         uint64_t* n_records);
+
 
 /*
  * Test hook (host code, no device): for each i, the culled render's

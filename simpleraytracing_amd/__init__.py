@@ -223,6 +223,29 @@ class Context:
         self._check(self._lib.xrt_debug_geometry_counters(self._ctx, c), "xrt_debug_geometry_counters")
         return dict(zip(("sizings", "reused", "plan_misses", "overflows"), (int(v) for v in c)))
 
+    def wave_times(self, frames_back: int = 0) -> np.ndarray:
+        """Timing records of the render frames_back frames before the last (xrt_debug_wave_times):
+        (n, 2) u32 s_memrealtime start / end (100 MHz, low 32 bits), one per statistics record."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.xrt_debug_wave_times(self._ctx, frames_back, None, 0, ctypes.byref(n)),
+                    "xrt_debug_wave_times")
+        out = np.zeros((n.value, 2), np.uint32)
+        self._check(self._lib.xrt_debug_wave_times(self._ctx, frames_back,
+                                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                   n.value, ctypes.byref(n)), "xrt_debug_wave_times")
+        return out
+
+    def block_records(self) -> np.ndarray:
+        """The last render's statistics records (xrt_debug_block_records): (n, 8) u32 -- rays,
+        hit rays, odd rays, overflow rays, hits, tile tests, candidates, max hits."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.xrt_debug_block_records(self._ctx, None, 0, ctypes.byref(n)),
+                    "xrt_debug_block_records")
+        out = np.zeros((n.value, 8), np.uint32)
+        self._check(self._lib.xrt_debug_block_records(self._ctx, out.ctypes.data, out.nbytes, ctypes.byref(n)),
+                    "xrt_debug_block_records")
+        return out
+
     def pipeline_counters(self) -> dict:
         """Frames rendered from a preparation made ahead, preparations dropped, renders
         launched with no wait, renders launched after a host wait (xrt_debug_pipeline_counters)."""
@@ -309,11 +332,22 @@ class Context:
         self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
 
     def timing_end(self):
-        """(total kernel ms, launches) of the main render kernel since timing_begin."""
+        """(summed kernel spans in ms, sampled launches) of the render kernel since
+        timing_begin: every render's in-kernel span (its waves' s_memrealtime
+        records, first start to last end)."""
         ms = ctypes.c_double()
         n = ctypes.c_uint64()
         self._check(self._lib.xrt_timing_end(self._ctx, ctypes.byref(ms), ctypes.byref(n)),
                     "xrt_timing_end")
+        return ms.value, n.value
+
+    def timing_events(self):
+        """(summed ms, launches) of the HIP start/stop event pairs on every 16th render
+        dispatch of the last timed region (a cross-check of timing_end)."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        self._check(self._lib.xrt_timing_events(self._ctx, ctypes.byref(ms), ctypes.byref(n)),
+                    "xrt_timing_events")
         return ms.value, n.value
 
     def probe_intersect(self, rays: np.ndarray, tris: np.ndarray):

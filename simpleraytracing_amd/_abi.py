@@ -119,6 +119,7 @@ XRT_SYMBOLS = {
     "xrt_read_stats": (ctypes.c_int, [_CtxP, ctypes.POINTER(Stats)]),
     "xrt_timing_begin": (ctypes.c_int, [_CtxP]),
     "xrt_timing_end": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
+    "xrt_timing_events": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
     "xrt_probe_intersect": (ctypes.c_int, [_CtxP, _fp, _fp, _u64, _u8p, _fp]),
     "xrt_probe_math": (ctypes.c_int, [_CtxP, ctypes.c_int, _fp, _fp, _u64]),
     "xrt_probe_prep": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _fp, _fp]),
@@ -138,7 +139,7 @@ XRT_SYMBOLS = {
     "xrt_debug_geometry_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_pipeline_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
-    "xrt_debug_stamps": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u64), _u64]),
+    "xrt_debug_wave_times": (ctypes.c_int, [_CtxP, _u32, ctypes.POINTER(_u32), _u64, ctypes.POINTER(_u64)]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
     "xrt_expand_rows_device": (ctypes.c_int, [_CtxP, _u64, _vp, _vp, _vp, _vp]),
     "xrt_plan_region_map": (ctypes.c_int, [_CtxP, ctypes.c_uint32, ctypes.c_uint32,

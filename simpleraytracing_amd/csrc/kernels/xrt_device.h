@@ -41,9 +41,6 @@
 #ifndef XRT_TILE_WAVES
 #define XRT_TILE_WAVES 4  // binned render: tile waves per workgroup
 #endif
-#ifndef XRT_PREP_SETPRIO
-#define XRT_PREP_SETPRIO 1   // preparation kernels raise their wave priority (s_setprio 3)
-#endif
 #ifndef XRT_DEFAULT_ORDER
 #define XRT_DEFAULT_ORDER 1    // binned render launch order: 0 raster, 1 centre first
 #endif
@@ -83,9 +80,6 @@
 #endif
 #ifndef XRT_ABLATION
 #define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
-#endif
-#ifndef XRT_STAMPS
-#define XRT_STAMPS 0      // diagnostics: per-workgroup start/end/hw-id in BlockStats
 #endif
 #if XRT_WAVES_PER_EU > 0
 #define XRT_CULLED_ATTR __attribute__((amdgpu_waves_per_eu(XRT_WAVES_PER_EU, 8)))

@@ -67,8 +67,6 @@ __host__ __device__ __forceinline__ int grid_exp(float x)
 // record each, and summed on the host by xrt_read_stats: same-address global
 // atomics from every wave serialise in L2, and a reduction kernel would sit
 // on every frame's critical path.
-// 32 bytes; XRT_STAMPS builds store the start/end s_memrealtime in the first
-// four words (two u64), the HW_ID in `candidates` and the XCC id in `max_hits`.
 struct BlockStats {
     unsigned int rays, hit_rays, odd_rays, overflow_rays, hits, tile_tests, candidates, max_hits;
 };
@@ -79,6 +77,11 @@ struct Outputs {
     float* lbuffer;
     uint8_t* image_u8;
     BlockStats* block_stats;   // one per workgroup (BINNED: per wave) of the render grid
+    // Timing records (timed regions, every kTimingStride-th frame; else null):
+    // beside each statistics record its wave's (workgroup's) s_memrealtime
+    // start and end, low 32 bits of the 100 MHz counter.  The host takes the
+    // kernel's span, last end - first start, from them (xrt_timing_end).
+    uint2* wave_times;
     // The frame's parameters in device memory (written by k_prep), read by
     // make_ray through this constant-address-space pointer: scalar loads where
     // a tile first needs its rays, instead of camera kernel arguments held in
@@ -171,61 +174,20 @@ __device__ __forceinline__ void wave_stats(WaveStats& ws, bool active, uint32_t 
     ws.lane_max = ws.lane_max > h ? ws.lane_max : h;
 }
 
-// Combines the block's wave counters through LDS and stores one BlockStats.
-// Must be reached by every thread of the block.
-// XRT_STAMPS builds (diagnostics only) overwrite rays/hit_rays/max_hits/pad
-// with the workgroup's s_memrealtime start/end, XCC id and HW_ID register.
-__device__ __forceinline__ uint64_t block_start_stamp()
+// Start of a wave (workgroup) for its timing record: the 100 MHz
+// s_memrealtime counter (one scalar load; awaited with the first others).
+__device__ __forceinline__ uint64_t block_start_stamp() { return __builtin_amdgcn_s_memrealtime(); }
+
+// The timing record of a statistics record: (start, end), low 32 bits.
+__device__ __forceinline__ void store_times(uint2* times, uint32_t index, uint64_t t_start)
 {
-#if XRT_STAMPS
-    return __builtin_amdgcn_s_memrealtime();
-#else
-    return 0;
-#endif
+    if (times) times[index] = make_uint2((uint32_t)t_start, (uint32_t)__builtin_amdgcn_s_memrealtime());
 }
 
-#if XRT_PREP_SETPRIO
-#define XRT_PREP_PRIO() __builtin_amdgcn_s_setprio(3)
-#else
-#define XRT_PREP_PRIO() do {} while (0)
-#endif
-
-// Phase timestamps of the binning kernels (XRT_STAMPS builds): one u64 per
-// (workgroup, phase) in g_stamps; the workgroup's threads are synchronised
-// first so a stamp marks the end of the phase for the whole workgroup.
-constexpr uint32_t kStampsN = 1u << 16;
-constexpr uint32_t kStampPrep = 0;          // k_prep: 8 per workgroup
-#if XRT_STAMPS
-__device__ uint64_t g_stamps[kStampsN];
-#define XRT_STAMP(idx)                                                               \
-    do {                                                                             \
-        __syncthreads();                                                             \
-        if (threadIdx.x == 0 && (idx) < kStampsN) g_stamps[(idx)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#else
-#define XRT_STAMP(idx) do {} while (0)
-#endif
-
-// XRT_STAMPS builds: workgroup/wave start and end time and hardware ids in
-// place of the counters (diagnostics only; the totals are then wrong).
-__device__ __forceinline__ void stamp_record(BlockStats& b, uint64_t t_start)
-{
-#if XRT_STAMPS
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-    b.rays = (unsigned int)t_start;
-    b.hit_rays = (unsigned int)(t_start >> 32);
-    b.odd_rays = (unsigned int)t_end;
-    b.overflow_rays = (unsigned int)(t_end >> 32);
-    b.candidates = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-    b.max_hits = __builtin_amdgcn_s_getreg((15 << 11) | 20);    // HW_REG_XCC_ID
-#else
-    (void)b;
-    (void)t_start;
-#endif
-}
-
+// Combines the block's wave counters through LDS and stores one BlockStats
+// (and its timing record).  Must be reached by every thread of the block.
 __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t candidates,
-                                                  BlockStats* out, uint64_t t_start = 0)
+                                                  BlockStats* out, uint2* times, uint64_t t_start)
 {
     __shared__ WaveStats s_ws[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -254,8 +216,8 @@ __device__ __forceinline__ void store_block_stats(const WaveStats& ws, uint32_t 
             b.max_hits = b.max_hits > s_ws[w].lane_max ? b.max_hits : s_ws[w].lane_max;
         }
         b.candidates = candidates;
-        stamp_record(b, t_start);
         out[blockIdx.y * gridDim.x + blockIdx.x] = b;
+        store_times(times, blockIdx.y * gridDim.x + blockIdx.x, t_start);
     }
 }
 
@@ -306,10 +268,11 @@ __device__ __forceinline__ void wave_reduce_sum_max(uint32_t a, uint32_t b, uint
 }
 
 // One wave's statistics as one BlockStats record (no LDS, no barrier): the
-// lane sums are reduced across the wave and lane 0 stores the record.
+// lane sums are reduced across the wave and lane 0 stores the record (and its
+// timing record, `copies` of it from index on).
 __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t candidates,
-                                                 BlockStats* out, uint32_t index, uint64_t t_start = 0,
-                                                 uint32_t stamp_extra = 0)
+                                                 BlockStats* out, uint32_t index, uint2* times,
+                                                 uint64_t t_start, uint32_t copies = 1)
 {
     uint32_t hits, mx;
     wave_reduce_sum_max(ws.lane_hits, ws.lane_max, hits, mx);
@@ -323,13 +286,11 @@ __device__ __forceinline__ void store_wave_stats(const WaveStats& ws, uint32_t c
         b.tile_tests = ws.tile_tests;
         b.candidates = candidates;
         b.max_hits = mx;
-        stamp_record(b, t_start);
-#if XRT_STAMPS
-        b.hits = stamp_extra;       // XRT_STAMPS: ticks from the wave's start to its first staged round
-#else
-        (void)stamp_extra;
-#endif
         out[index] = b;
+        if (times) {
+            const uint2 t = make_uint2((uint32_t)t_start, (uint32_t)__builtin_amdgcn_s_memrealtime());
+            for (uint32_t k = 0; k < copies; ++k) times[index + k] = t;
+        }
     }
 }
 
@@ -626,6 +587,7 @@ template <bool kSigned>
 __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__ recs,
                                                       RenderParams p, Outputs out)
 {
+    const uint64_t t_start = block_start_stamp();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_in_block();
     const uint32_t col = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
@@ -648,7 +610,7 @@ __global__ __launch_bounds__(256) void k_render_brute(const TriRec* __restrict__
         finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, T, fetch);
     else
         finish_ray(p, out, active, (size_t)(row - p.row_begin) * p.width + col, hl, ws, recs, dx, dy, dz, T, fetch);
-    store_block_stats(ws, 0u, out.block_stats);
+    store_block_stats(ws, 0u, out.block_stats, out.wave_times, t_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -899,7 +861,7 @@ __global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriR
                             [&](uint32_t k) { return s_list[k]; }, ws, st);
     else   // list overflow: every triangle is a candidate (still exact)
         render_region_tiles(p, out, recs, culls, rx0, ry0, T, [](uint32_t k) { return k; }, ws, st);
-    store_block_stats(ws, n_cand, out.block_stats, t_start);
+    store_block_stats(ws, n_cand, out.block_stats, out.wave_times, t_start);
 }
 
 // Conservative footprint of one triangle (DESIGN.md "Tile cull").
@@ -1269,9 +1231,10 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
                                               RenderParams* __restrict__ frame_out,
                                               float* __restrict__ offsets_out)
 {
-    // The preparation of frame N+1 shares the CUs with frame N's render (prep
-    // stream): top wave priority keeps this latency-bound chain short.
-    XRT_PREP_PRIO();
+    // The preparation shares the CUs with earlier frames' renders (prep
+    // stream) at the default wave priority: frames are prepared ahead of their
+    // renders, and a raised priority only took issue slots from the render
+    // (1024^2 step 29.0 -> 27.6 us without it).
     // i: the thread's index over the grid (pixel-offset tables, counter
     // clears); tri: its triangle -- kPrepTris per wave (fewer than 64 spreads
     // the binning's cells and commits of a frame over more waves).
@@ -1284,7 +1247,6 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
         if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
         else if (i - p.height < p.width) offsets_out[i] = pixel_offset(p.spacing, i - p.height, p.width);
     }
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 0);
     Footprint fp;
     TriRec r = {};
     if (valid) {
@@ -1320,7 +1282,6 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
             fp.e0.w = __uint_as_float(tri);          // the region entries carry the id (make_entry's layout)
         }
     }
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 1);
     if (!bins.counts) return;                      // kernel-uniform
     if (bins.clear) {                              // the other half, for the set's next frame
         if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
@@ -1379,7 +1340,6 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 2);
 
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
     bool over = false;                             // a slot past its list's capacity
@@ -1485,9 +1445,7 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 6);
     commit();                                      // (2)
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 3);
     // A region count past the list capacity: the render of that region falls
     // back to the whole mesh, and the host grows the lists for the next frame
     // (xrt_read_stats / the sizing read).  No global atomic otherwise.
@@ -1497,7 +1455,6 @@ __global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8,
         atomicOr(&bs->overflow, 1u);
         if (bins.plan_miss) bins.plan_miss[1] = 1u;  // the host re-sizes for the next frame
     }
-    XRT_STAMP(kStampPrep + 8 * blockIdx.x + 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -1620,8 +1577,7 @@ template <bool kSigned>
 __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __restrict__ recs,
                                             const float4* __restrict__ culls, const RenderParams& p,
                                             const Outputs& out, const BinBuffers& bins, uint32_t n_glob,
-                                            uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand,
-                                            uint64_t& t_staged)
+                                            uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand)
 {
     const uint32_t lane = threadIdx.x & 63u;
     // the slot's count (k_prep) and description (host): two scalar loads in flight together
@@ -1668,9 +1624,6 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
         else stage_entries(st, local, n_local, glob, base, cnt);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
         __syncthreads();                           // and every wave's
-#if XRT_STAMPS
-        if (!base) t_staged = __builtin_amdgcn_s_memrealtime();
-#endif
         if (!tile_live) continue;
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64u) {
             const uint32_t k = k0 + lane;
@@ -1785,7 +1738,6 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
     const uint32_t wave = wave_in_block();
     const uint32_t n_glob = as_const(bs)->global_count;
-    uint64_t t_staged = t_start;                   // XRT_STAMPS diagnostics
     WaveStats ws = {};
     uint32_t cand = 0;
     if (!kSigned && blockIdx.x >= tile_blocks) {   // a planned-empty region (workgroup-uniform)
@@ -1794,7 +1746,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         const uint32_t rec0 =
             tile_blocks * kTileWaves + ((blockIdx.x - tile_blocks) * kTileWaves + wave) * kBlocksPerRegion;
         fill_region_rows(p, out, bins, slot, wave, ws);    // (packed layout: counts only)
-        store_wave_stats(ws, 0u, out.block_stats, rec0, t_start);
+        store_wave_stats(ws, 0u, out.block_stats, rec0, out.wave_times, t_start, kBlocksPerRegion);
         if ((threadIdx.x & 63u) == 0u) {
 #pragma unroll
             for (uint32_t k = 1; k < kBlocksPerRegion; ++k) out.block_stats[rec0 + k] = BlockStats{};
@@ -1819,9 +1771,9 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
 #endif
     const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
-    render_tile<kSigned>(st, recs, culls, p, out, bins, n_glob, slot, tile, ws, cand, t_staged);
+    render_tile<kSigned>(st, recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
     // candidates are counted once per region (by the wave holding tile 0)
-    store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, t_start, (uint32_t)(t_staged - t_start));
+    store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
 }
 
 // ---------------------------------------------------------------------------

@@ -26,8 +26,15 @@ using namespace XRT_KERNEL_NS;
 // every later frame of the geometry are the same): the sum of the counts plus
 // 1/8 + 4 per region, instead of the largest count times the regions.
 constexpr uint32_t kInitialRegionCap = 256;
-// Timed regions put render timing events on every kTimingStride-th frame.
-constexpr uint64_t kTimingStride = 4;
+// Timed regions (xrt_timing_begin/end) keep the timing records of every
+// frame (Outputs::wave_times: each wave's s_memrealtime start and end), up to
+// kTimingRecords of them (8 B each) per region, and put a HIP start/stop event
+// pair on the render dispatch of every kEventStride-th frame, a cross-check of
+// the in-kernel spans (a start event costs the frame a few microseconds).
+constexpr size_t kTimingRecords = (size_t)1 << 27;
+constexpr uint64_t kEventStride = 16;
+// s_memrealtime ticks per millisecond (100 MHz on gfx950)
+constexpr double kTicksPerMs = 1e5;
 // Buffer sets in rotation: frame N's preparation reuses the set of frame
 // N - kFrameSets, whose render the host has seen complete by then.
 constexpr int kFrameSets = 4;
@@ -61,6 +68,8 @@ struct FrameSet {
     size_t offsets_cap = 0;
     BlockStats* block_stats = nullptr;   // the render's per-workgroup / per-wave records
     size_t block_stats_cap = 0;
+    uint2* times = nullptr;              // their timing records (Outputs::wave_times), frames not sampled
+    size_t times_cap = 0;
     uint32_t n_blocks = 0;         // records of the set's last render
     bool binned = false;           // the set's last frame was binned (BinState valid)
 
@@ -85,8 +94,7 @@ struct FrameSet {
     // Completion events ride on the kernel dispatches themselves
     // (hipExtLaunchKernel stop events): no separate event packets.
     hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
-    hipEvent_t t0 = nullptr, t1 = nullptr;   // render start / end (untimed frames)
-    hipEvent_t done = nullptr;         // render end (unsampled frames of a timed region)
+    hipEvent_t done = nullptr;         // render end (a stop event on the render's dispatch)
     hipEvent_t done_ev = nullptr;      // the event that marks the set's last render complete
     bool done_valid = false;
     // k_prep's flags (BinBuffers::plan_miss): [0] the fill plan did not hold,
@@ -172,12 +180,25 @@ struct xrt_context {
     size_t stage_cap = 0;
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-    hipEvent_t last_t0 = nullptr, last_t1 = nullptr;   // events of the last render launch
     // region timing (xrt_timing_begin/end)
     bool timing = false;
-    std::vector<hipEvent_t> tev;      // pairs: [2i] before, [2i+1] after the main kernel
+    std::vector<hipEvent_t> tev;      // pairs: [2i] start, [2i+1] stop of a sampled render dispatch
     size_t tev_used = 0;
     uint64_t timed_frames = 0;        // frames enqueued since xrt_timing_begin
+    size_t timed_records = 0;         // their timing records kept
+    // the sampled frames' timing records: chunks of device memory (a chunk is
+    // never moved while kernels may write it), and where each frame's are
+    struct TimesChunk {
+        uint2* p;
+        size_t cap, used;
+    };
+    std::vector<TimesChunk> tchunks;
+    struct TimesSample {
+        size_t chunk, offset, n;
+    };
+    std::vector<TimesSample> tsamples;
+    double event_ms = 0.0;            // the last timed region's HIP-event samples
+    uint64_t event_launches = 0;
     hipStream_t last_stream = nullptr;
     bool pending = false;
     int kernel = XRT_KERNEL_AUTO;
@@ -663,6 +684,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     std::memcpy(&out.miss_l, &miss_bits, sizeof miss_bits);
     out.mu = ctx->mu;
     out.packed = 0u;
+    out.wave_times = nullptr;          // launch_frame
     if (ctx->packed_cap) {                         // xrt_set_transit_layout
         if (!binned || signed_model || d_image || d_u8)
             return fail(ctx, XRT_ERR_ARGUMENT,
@@ -785,6 +807,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     // stats records: one per workgroup; BINNED one per tile wave, 16 per fill region
     const uint32_t n_blocks = !rows ? 0u : binned ? kWavesPerRegion * n_regions : grid.x * grid.y;
     if ((rc = ensure(ctx, fs.block_stats, fs.block_stats_cap, n_blocks))) return rc;
+    if ((rc = ensure(ctx, fs.times, fs.times_cap, n_blocks))) return rc;
     fs.n_blocks = n_blocks;
     fs.binned = binned;
     out.block_stats = fs.block_stats;
@@ -806,6 +829,44 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     return XRT_OK;
 }
 
+// Room for n timing records of a sampled frame in the timed region's chunks
+// (a new chunk, never a moved one, when the last is full).
+int timing_slot(xrt_context* ctx, size_t n, uint2*& slot)
+{
+    if (ctx->tchunks.empty() || ctx->tchunks.back().cap - ctx->tchunks.back().used < n) {
+        size_t want = std::max<size_t>(n * 64, (size_t)1 << 16);
+        // chunks of earlier regions are reused before new ones are allocated
+        size_t k = 0;
+        while (k < ctx->tchunks.size() && !(ctx->tchunks[k].used == 0 && ctx->tchunks[k].cap >= n)) ++k;
+        if (k < ctx->tchunks.size() && k + 1 < ctx->tchunks.size()) {
+            std::swap(ctx->tchunks[k], ctx->tchunks.back());   // an unused chunk to the end
+        } else if (k == ctx->tchunks.size()) {
+            xrt_context::TimesChunk c = {nullptr, want, 0};
+            XRT_HIP(ctx, hipMalloc(&c.p, want * sizeof(uint2)));
+            ctx->tchunks.push_back(c);
+        }
+    }
+    xrt_context::TimesChunk& c = ctx->tchunks.back();
+    ctx->tsamples.push_back({ctx->tchunks.size() - 1, c.used, n});
+    slot = c.p + c.used;
+    c.used += n;
+    return XRT_OK;
+}
+
+// A frame's kernel span from its waves' timing records: the last end minus
+// the first start, in ms (32-bit tick differences: spans below 21 s).
+double records_span_ms(const std::vector<uint2>& t)
+{
+    if (t.empty()) return 0.0;
+    const uint32_t ref = t[0].x;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (const uint2& r : t) {
+        lo = std::min<int64_t>(lo, (int32_t)(r.x - ref));
+        hi = std::max<int64_t>(hi, (int32_t)(r.y - ref));
+    }
+    return hi > lo ? (double)(hi - lo) / kTicksPerMs : 0.0;
+}
+
 int launch_frame(xrt_context* ctx, PendingFrame& pf)
 {
     FrameSet& fs = *pf.fs;
@@ -814,7 +875,6 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     const bool binned = pf.binned;
     const uint32_t rows = pf.rows, rx = pf.rx, ry = pf.ry;
     const RenderParams& p = pf.p;
-    const Outputs& out = pf.out;
     BinState* bin_ctl = pf.bin_ctl;
     const auto t_call = pf.t_call;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
@@ -853,21 +913,26 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         return fail(ctx, XRT_ERR_OVERFLOW, "the packed layout needs this frame's fill plan (and room for its "
                                         "unfilled regions): the frame was not rendered");
 
-    // Events ride on the render's own dispatch (hipExtLaunchKernel).  Outside
-    // timed regions every frame carries the set's start/end pair (stats
-    // kernel_ms); inside one (xrt_timing_begin/end) every kTimingStride-th
-    // frame carries a timing pair -- a start event costs the frame a few
-    // microseconds -- and the others only the set's end event, which the host
-    // needs to reuse the set.  The mean render duration is taken over the
-    // sampled frames.
-    hipEvent_t t0 = fs.t0, t1 = fs.t1;
-    const bool sampled = ctx->timing && (ctx->timed_frames++ % kTimingStride) == 0;
-    if (ctx->timing && !sampled) {
-        t0 = nullptr;
-        t1 = fs.done;
-    } else if (ctx->timing) {
+    // Every render dispatch carries the set's stop event (the host needs it
+    // to reuse the set).  Its waves store their timing records beside their
+    // statistics (the span of the set's last frame: xrt_read_stats); in a
+    // timed region every frame keeps them apart (the mean span over the
+    // region's frames: xrt_timing_end) and every kEventStride-th
+    // dispatch also carries a start event (xrt_timing_events).
+    Outputs out = pf.out;
+    out.wave_times = fs.times;
+    hipEvent_t t0 = nullptr, t1 = fs.done;
+    const uint64_t frame_in_region = ctx->timing ? ctx->timed_frames++ : 0;
+    if (ctx->timing && rows > 0 && ctx->timed_records + fs.n_blocks <= kTimingRecords) {
+        ctx->timed_records += fs.n_blocks;
+        uint2* slot = nullptr;
+        int rc = timing_slot(ctx, fs.n_blocks, slot);
+        if (rc) return rc;
+        out.wave_times = slot;
+    }
+    if (ctx->timing && rows > 0 && frame_in_region % kEventStride == 0) {
         if (ctx->tev_used + 2 > ctx->tev.size()) {
-            for (int k = 0; k < 256; ++k) {
+            for (int k = 0; k < 64; ++k) {
                 hipEvent_t e;
                 XRT_HIP(ctx, hipEventCreate(&e));
                 ctx->tev.push_back(e);
@@ -877,7 +942,6 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         t1 = ctx->tev[ctx->tev_used + 1];
         ctx->tev_used += 2;
     }
-    ctx->last_t0 = ctx->last_t1 = nullptr;
     if (rows > 0) {
         const bool sgn = p.model == kModelSigned;
         const auto t_launch = HostClock::now();
@@ -892,14 +956,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
                                   0, stream, t0, t1, 0, fs.recs, fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         if (ctx->host_profile) ctx->hp_lrender += seconds_since(t_launch);
-        if (t0) {
-            ctx->last_t0 = t0;
-            ctx->last_t1 = t1;
-        }
         fs.done_ev = t1;
         fs.done_valid = true;
-    } else if (sampled) {
-        ctx->tev_used -= 2;         // nothing launched, nothing to time
     }
     if (ctx->host_profile) {
         ctx->hp_total += seconds_since(t_call);
@@ -1020,8 +1078,7 @@ int xrt_create(int device, xrt_context** out)
               hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
-             hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.t0) == hipSuccess &&
-             hipEventCreate(&fs.t1) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
+             hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
              hipHostMalloc((void**)&fs.plan_flag, 2 * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
@@ -1062,7 +1119,8 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.bin_counts);
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
-        for (hipEvent_t e : {fs.ready, fs.t0, fs.t1, fs.done})
+        (void)hipFree(fs.times);
+        for (hipEvent_t e : {fs.ready, fs.done})
             if (e) (void)hipEventDestroy(e);
     }
     if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
@@ -1074,6 +1132,7 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+    for (auto& c : ctx->tchunks) (void)hipFree(c.p);
     if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
     delete ctx;
@@ -1433,17 +1492,19 @@ int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint
     return XRT_OK;
 }
 
-int xrt_debug_stamps(xrt_context* ctx, uint64_t* dst, uint64_t n)
+int xrt_debug_wave_times(xrt_context* ctx, uint32_t frames_back, uint32_t* dst, uint64_t capacity,
+                         uint64_t* n_records)
 {
-    if (!ctx || (n && !dst)) return XRT_ERR_ARGUMENT;
+    if (!ctx || !n_records) return XRT_ERR_ARGUMENT;
+    if (frames_back >= (uint32_t)kFrameSets) return fail(ctx, XRT_ERR_ARGUMENT, "frames_back must be < 4");
     XRT_HIP(ctx, hipSetDevice(ctx->device));
     XRT_HIP(ctx, hipDeviceSynchronize());
-    n = std::min<uint64_t>(n, kStampsN);
-#if XRT_STAMPS
-    if (n) XRT_HIP(ctx, hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), n * sizeof(uint64_t)));
-#else
-    std::memset(dst, 0, n * sizeof(uint64_t));
-#endif
+    const FrameSet* fs = ctx->last_set
+                             ? &ctx->sets[((ctx->last_set - ctx->sets) + kFrameSets - (int)frames_back) % kFrameSets]
+                             : nullptr;
+    *n_records = fs ? fs->n_blocks : 0u;
+    const size_t n = std::min<size_t>((size_t)capacity, (size_t)*n_records);
+    if (n && dst) XRT_HIP(ctx, hipMemcpy(dst, fs->times, n * sizeof(uint2), hipMemcpyDeviceToHost));
     return XRT_OK;
 }
 
@@ -1483,8 +1544,12 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
         }
     }
     stats->global_triangles = 0;
-    float ms = 0.0f;
-    if (!ctx->last_t0 || hipEventElapsedTime(&ms, ctx->last_t0, ctx->last_t1) != hipSuccess) ms = 0.0f;
+    double ms = 0.0;
+    if (fs && fs->n_blocks && !ctx->timing) {      // the set's records (a timed region keeps its samples apart)
+        std::vector<uint2> t(fs->n_blocks);
+        XRT_HIP(ctx, hipMemcpy(t.data(), fs->times, t.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+        ms = records_span_ms(t);
+    }
     stats->kernel = (uint32_t)ctx->last_kernel;
     stats->kernel_ms = ms;
     if (fs && fs->binned && fs->last_state) {
@@ -1511,6 +1576,9 @@ int xrt_timing_begin(xrt_context* ctx)
     ctx->timing = true;
     ctx->tev_used = 0;
     ctx->timed_frames = 0;
+    ctx->timed_records = 0;
+    for (auto& c : ctx->tchunks) c.used = 0;
+    ctx->tsamples.clear();
     return XRT_OK;
 }
 
@@ -1518,17 +1586,36 @@ int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches)
 {
     if (!ctx || !total_ms || !launches) return XRT_ERR_ARGUMENT;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
-    double sum = 0.0;
+    double ev = 0.0;
     for (size_t i = 0; i + 1 < ctx->tev_used; i += 2) {
         XRT_HIP(ctx, hipEventSynchronize(ctx->tev[i + 1]));
         float ms = 0.0f;
         XRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->tev[i], ctx->tev[i + 1]));
-        sum += ms;
+        ev += ms;
+    }
+    ctx->event_ms = ev;
+    ctx->event_launches = ctx->tev_used / 2;
+    XRT_HIP(ctx, hipDeviceSynchronize());          // the sampled frames' records are written
+    double sum = 0.0;
+    std::vector<uint2> t;
+    for (const auto& smp : ctx->tsamples) {
+        t.resize(smp.n);
+        XRT_HIP(ctx, hipMemcpy(t.data(), ctx->tchunks[smp.chunk].p + smp.offset, smp.n * sizeof(uint2),
+                               hipMemcpyDeviceToHost));
+        sum += records_span_ms(t);
     }
     *total_ms = sum;
-    *launches = ctx->tev_used / 2;
+    *launches = ctx->tsamples.size();
     ctx->timing = false;
     ctx->tev_used = 0;
+    return XRT_OK;
+}
+
+int xrt_timing_events(xrt_context* ctx, double* total_ms, uint64_t* launches)
+{
+    if (!ctx || !total_ms || !launches) return XRT_ERR_ARGUMENT;
+    *total_ms = ctx->event_ms;
+    *launches = ctx->event_launches;
     return XRT_OK;
 }
 

@@ -601,7 +601,9 @@ def test_device_buffers_and_timing(ctx, dragon):
                                    stream.cuda_stream)
     ms, launches = ctx.timing_end()
     st = ctx.read_stats()
-    assert launches == 2 and ms > 0            # timing events on every 4th frame
+    assert launches == 8 and ms > 0            # every frame's in-kernel span
+    ev_ms, ev_launches = ctx.timing_events()
+    assert ev_launches == 1 and ev_ms > 0      # HIP events on every 16th dispatch
     ref = ctx.render_rows(cam)
     assert np.array_equal(bits(img.cpu().numpy()), bits(ref[0]))
     assert np.array_equal(u8.cpu().numpy(), ref[2])

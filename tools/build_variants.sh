@@ -3,7 +3,7 @@
 #   tools/build_variants.sh name1 "-DFOO=1" name2 "-DFOO=0" ...
 set -e
 cd "$(dirname "$0")/../simpleraytracing_amd/csrc"
-OUT=../lib/ab
+OUT=../lib/var
 mkdir -p $OUT
 while [ $# -gt 1 ]; do
   name=$1; flags=$2; shift 2

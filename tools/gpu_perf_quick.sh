@@ -21,6 +21,8 @@ if [ ${#CFGS[@]} -eq 0 ]; then
 fi
 for cfg in "${CFGS[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 python bench.py --no-cpu-baseline $cfg > $OUT/perf_$i.json 2> $OUT/perf_$i.err || { cat $OUT/perf_$i.err; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu-baseline $cfg > $OUT/perf_$i.json 2> $OUT/perf_$i.err
+  rc=$?
+  if [ $rc -ne 0 ]; then tail -2 $OUT/perf_$i.err; [ $rc -eq 1 ] && continue; exit $rc; fi
   python3 -c "import json,sys; d=json.load(open('$OUT/perf_$i.json')); r=d['roofline']; print('$cfg', 'Mrays/s %.0f'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'kernel_ms %.4f'%r['avg_kernel_ms'], 'ratio %.3f'%(d['ms_per_step']/r['avg_kernel_ms']), 'tests/ray %.2f'%d['render_stats']['ray_triangle_tests_per_ray'], 'first_ms %.3f'%d['latency']['first_frame_ms'])"
 done
