@@ -19,6 +19,7 @@ CFGS=("$@")
 if [ ${#CFGS[@]} -eq 0 ]; then
   CFGS=("--size 1024 1024" "--size 2048 2048" "--size 4096 4096" "--size 8192 8192 --tile-mesh 7 --steps 100 --warmup 10")
 fi
+[ "${CFGS[0]}" = none ] && exit 0
 for cfg in "${CFGS[@]}"; do
   i=$((i+1))
   timeout -k 10 300 python bench.py --no-cpu-baseline $cfg > $OUT/perf_$i.json 2> $OUT/perf_$i.err
