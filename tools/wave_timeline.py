@@ -78,4 +78,12 @@ for lo, hi in ((0, 1), (1, 5), (5, 20), (20, 60), (60, 10**9)):
         groups[f"tests {lo}-{hi}"] = {"waves": int(m.sum()), "dur_us_median": float(np.median(dur[m])),
                                       "dur_us_max": float(dur[m].max())}
 out["by_tests"] = groups
+slow = np.argsort(-np.where(live, dur, -1.0))[:12]
+out["slowest"] = [{"record": int(k), "start_us": round(float(s[k]), 2), "dur_us": round(float(dur[k]), 2),
+                   "rays": int(rec[k, 0]), "hit_rays": int(rec[k, 1]), "overflow_rays": int(rec[k, 3]),
+                   "hits": int(rec[k, 4]), "tile_tests": int(rec[k, 5]), "candidates": int(rec[k, 6]),
+                   "max_hits": int(rec[k, 7])} for k in slow]
+ov = live & (rec[:, 3] > 0)
+out["overflow_waves"] = {"n": int(ov.sum()), "dur_us_median": float(np.median(dur[ov])) if ov.any() else None,
+                         "dur_us_sum": float(dur[ov].sum()) if ov.any() else 0.0}
 print(json.dumps(out))
