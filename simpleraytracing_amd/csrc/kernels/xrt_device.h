@@ -24,32 +24,10 @@
 #define XRT_KERNEL_NS xrt
 #endif
 
-// Compile-time variants for A/B timing (tools/build_variants.sh, tools/ab.py);
-// the defaults are the measured-faster choices.
-#ifndef XRT_MED3
-#define XRT_MED3 1        // med3 insertion (else the compare-exchange chain)
-#endif
-#ifndef XRT_PAIR
-#define XRT_PAIR 1        // culled kernels test survivors two at a time
-#endif
-#ifndef XRT_WAVES_PER_EU
-#define XRT_WAVES_PER_EU 0   // >0: occupancy hint for the culled render kernels
-#endif
-#ifndef XRT_XCD_REMAP
-#define XRT_XCD_REMAP 1  // binned render: >0 = regions per XCD per run of 8 XCDs, all of a region on one XCD (A/B: render 55.1 -> 53.8 us); 0 off
-#endif
+// Tuning constants (overridable with -D for A/B builds, tools/build_variants.sh);
+// the defaults are the measured-faster choices (DESIGN.md).
 #ifndef XRT_TILE_WAVES
 #define XRT_TILE_WAVES 4  // binned render: tile waves per workgroup
-#endif
-#ifndef XRT_DEFAULT_ORDER
-#define XRT_DEFAULT_ORDER 1    // binned render launch order: 0 raster, 1 centre first
-#endif
-#ifndef XRT_PRE_REJECT
-#define XRT_PRE_REJECT 0     // culled tests: wave-wide division-free reject before the exact test (A/B: slower, off)
-#endif
-#ifndef XRT_FAST_RCP
-#define XRT_FAST_RCP 2    // culled tests' 1/det: 0 IEEE division; 1 rcp + Newton per test (slower);
-                          // 2 rcp + Newton with one range check per survivor pair (fastest)
 #endif
 #ifndef XRT_RENDER_WAVES
 #define XRT_RENDER_WAVES 8   // binned render: minimum waves per SIMD (8 = 64 VGPRs)
@@ -57,34 +35,8 @@
 #ifndef XRT_STAGE
 #define XRT_STAGE 64      // binned render: candidates staged in LDS per round (8 KB; 128: 16 KB, 4 % slower at 2048^2 with the heavy-first plan)
 #endif
-#ifndef XRT_FOLD_CMP
-#define XRT_FOLD_CMP 1       // Ray::intersect's four range tests folded into two (min / max)
-#endif
-#ifndef XRT_DESC_MED3
-#define XRT_DESC_MED3 1      // hit-list insertion from the top slot down (in place, no copies)
-#endif
-#ifndef XRT_RCP_FALLTHROUGH
-#define XRT_RCP_FALLTHROUGH 1  // binned survivors: short reciprocal always, IEEE division behind one rare branch (render -1.5..2.6 %)
-#endif
-#ifndef XRT_PREFETCH_OFFSETS
-#define XRT_PREFETCH_OFFSETS 1  // binned render: the tile's pixel offsets loaded at the wave's start
-#endif
-#ifndef XRT_BRANCHLESS_EXPF
-#define XRT_BRANCHLESS_EXPF 1   // expf's special cases as selects (no divergent branches)
-#endif
-#ifndef XRT_BRANCHLESS_LUT
-#define XRT_BRANCHLESS_LUT 1    // the 8-bit LUT as selects
-#endif
 #ifndef XRT_PREP_THREADS
 #define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)
-#endif
-#ifndef XRT_ABLATION
-#define XRT_ABLATION 0    // diagnostics: honour RenderParams::ablate ($XRT_ABLATE)
-#endif
-#if XRT_WAVES_PER_EU > 0
-#define XRT_CULLED_ATTR __attribute__((amdgpu_waves_per_eu(XRT_WAVES_PER_EU, 8)))
-#else
-#define XRT_CULLED_ATTR
 #endif
 
 namespace XRT_KERNEL_NS {
@@ -121,34 +73,13 @@ struct RenderParams {
     uint32_t row_begin, row_end;
     uint32_t num_triangles;
     uint32_t hit_capacity;  // <= XRT_MAX_HITS
-    uint32_t ablate;        // diagnostics only ($XRT_ABLATE bits, kAblate*); 0 in production
+    uint32_t pad_;
     uint32_t model;         // kModelAttenuation (main.cxx) or kModelSigned (the L-buffer fork)
 };
 
 // What a render computes per ray.
 constexpr uint32_t kModelAttenuation = 0;   // renderLoop, src/main.cxx:626-743
 constexpr uint32_t kModelSigned = 1;        // renderLoopCallBack, src/main-pthreads-lbuffer.cxx:733-813
-
-// Ablation bits (timing studies; outputs are wrong when any is set).  Only
-// XRT_ABLATION builds (tools/gpu_ablate.sh) read them: the production kernels
-// carry neither the field nor its branches.
-constexpr uint32_t kAblateCandidates = 1;   // phase 2 sees no candidates
-constexpr uint32_t kAblateSweep = 2;        // tiled: no phase-1 footprint sweep
-constexpr uint32_t kAblateRayGen = 4;       // constant ray direction
-constexpr uint32_t kAblateStores = 8;       // no output stores
-constexpr uint32_t kAblateShade = 16;       // no expf / LUT
-constexpr uint32_t kAblateExact = 32;       // culled kernels: no Moller-Trumbore for survivors
-constexpr uint32_t kAblatePush = 64;        // culled kernels: exact test but no hit-list insert
-
-__device__ __forceinline__ uint32_t ablation(const RenderParams& p)
-{
-#if XRT_ABLATION
-    return p.ablate;
-#else
-    (void)p;
-    return 0u;
-#endif
-}
 
 // Register hit list per ray.  Each slot costs every exact test one
 // v_med3_f32; a ray with more hits is recomputed exactly by its wave
@@ -257,6 +188,7 @@ __device__ __forceinline__ void make_ray_from(const P& p, float v_off, float u_o
 // tests/test_abi.py); the f32 division sequence is about half the f64 one.
 __host__ __device__ __forceinline__ float inv_det_of(float det) { return 1.0f / det; }
 
+
 // v_rcp_f32 (within 1 ulp) and one FMA Newton step give the correctly rounded
 // 1.0f / d for every d with biased exponent in [1, 252], i.e. 2^-126 <= |d| <
 // 2^126: checked on all 2^32 inputs on the GPU (tools/probes/rcp_probe.hip,
@@ -272,15 +204,6 @@ __device__ __forceinline__ bool rcp_newton_exact_for(float d)
 {
     const float a = fabsf(d);
     return a >= 0x1p-126f && a < 0x1p126f;       // false for NaN
-}
-// The culled tests' 1/det: the short sequence, unless some lane of the wave
-// has a det outside its range (zero, denormal, |det| >= 2^126, inf, NaN) --
-// that wave takes the IEEE division on every lane.  Equal to inv_det_of(det)
-// on every lane either way.
-__device__ __forceinline__ float inv_det_fast(float det)
-{
-    if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) return inv_det_of(det);
-    return rcp_newton(det);
 }
 
 // Branch-free Ray::intersect for the culled kernels, whose survivors almost
@@ -389,7 +312,6 @@ __host__ __device__ __forceinline__ float mt_finish_inv(float det, float inv_det
     const float u = a * inv_det;                          // Ray.cxx:105
     const float v = b * inv_det;                          // Ray.cxx:115
     const float t = tnum * inv_det;                       // Ray.cxx:122
-#if XRT_FOLD_CMP
     // Ray.cxx:106 and :116 with two compares: !(u < 0) && !(v < 0) is
     // !(min(u, v) < 0), and !(u > 1) && !(u + v > 1) is !(max(u, u + v) > 1),
     // because IEEE minNum / maxNum return the other operand when one is a
@@ -397,9 +319,6 @@ __host__ __device__ __forceinline__ float mt_finish_inv(float det, float inv_det
     // when both are.
     // (bitwise &: evaluated without branches)
     hit = (det != 0.0f) & !(fminf(u, v) < 0.0f) & !(fmaxf(u, u + v) > 1.0f) & accept_t(t);
-#else
-    hit = det != 0.0f && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && accept_t(t);
-#endif
     return t;
 }
 
@@ -415,7 +334,7 @@ __device__ __forceinline__ float mt_exact(float dx, float dy, float dz, float e1
 {
     float det, a, b;
     mt_numerators(dx, dy, dz, e1x, e1y, e1z, e2x, e2y, e2z, tvx, tvy, tvz, qvx, qvy, qvz, det, a, b);
-    return mt_finish_inv(det, XRT_FAST_RCP == 1 ? inv_det_fast(det) : inv_det_of(det), a, b, tnum, hit);   // Ray.cxx:99
+    return mt_finish_inv(det, inv_det_of(det), a, b, tnum, hit);   // Ray.cxx:99
 }
 
 // ---------------------------------------------------------------------------
@@ -439,21 +358,7 @@ struct HitList {
     // A miss inserts +inf, which leaves h unchanged.  hit == false or x > 0.
     __device__ __forceinline__ void push_if(bool hit, float t)
     {
-#if !XRT_MED3
-        if (hit) {
-#pragma unroll
-            for (int k = 0; k < kMaxHits; ++k) {
-                const float cur = h[k];
-                const bool lt = t < cur;
-                h[k] = lt ? t : cur;
-                t = lt ? cur : t;
-            }
-            ++n;
-        }
-        return;
-#endif
         const float x = hit ? t : __builtin_inff();
-#if XRT_DESC_MED3
         // top slot first: each slot's new value is its last reader's, so the
         // list is updated in place
 #pragma unroll
@@ -461,16 +366,6 @@ struct HitList {
         // min(h[0], x): the values are never NaN, so one plain v_min_f32 (the
         // compiler's fminnum adds a canonicalising v_max of the loop-carried h[0])
         asm("v_min_f32 %0, %1, %2" : "=v"(h[0]) : "v"(h[0]), "v"(x));
-#else
-        float prev = h[0];
-        h[0] = fminf(prev, x);
-#pragma unroll
-        for (int k = 1; k < kMaxHits; ++k) {
-            const float cur = h[k];
-            h[k] = __builtin_amdgcn_fmed3f(prev, cur, x);
-            prev = cur;
-        }
-#endif
         n += hit ? 1u : 0u;
     }
 
@@ -600,14 +495,6 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     uint32_t ix;
     __builtin_memcpy(&ix, &x, 4);
     uint32_t abstop = (ix >> 20) & 0x7ff;
-#if !XRT_BRANCHLESS_EXPF
-    if (abstop >= 0x42b) {                  // |x| >= 88 or NaN
-        if (ix == 0xff800000u) return 0.0f; // -inf
-        if (abstop >= 0x7f8) return x + x;  // +inf or NaN
-        if (x > 0x1.62e42ep6f) return __builtin_inff();   // overflow
-        if (x < -0x1.9fe368p6f) return 0.0f;              // underflow
-    }
-#endif
     double xd = (double)x;
     double kd = __builtin_fma(kInvLn2N, xd, kShift);
     uint64_t ki = xrt_double_as_u64(kd);
@@ -620,7 +507,6 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
     double y = __builtin_fma(kC2, r, 1.0);
     y = __builtin_fma(z, r2, y);
     y = y * s;
-#if XRT_BRANCHLESS_EXPF
     // the special cases as selects over the main path's value (which is
     // computed, and discarded, for them too): no divergent branches
     float out = (float)y;
@@ -631,9 +517,6 @@ __host__ __device__ __forceinline__ float xrt_expf(float x)
         out = ix == 0xff800000u ? 0.0f : out;                    // -inf
     }
     return out;
-#else
-    return (float)y;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -819,23 +702,12 @@ __host__ __device__ __forceinline__ float signed_lbuffer(float distance, int sig
 __host__ __device__ __forceinline__ uint8_t lut_u8(float v)
 {
     const float vmin = 0.0f, vmax = 80.0f;
-#if XRT_BRANCHLESS_LUT
     // 255.0 * v / 80.0 == v * 3.1875 exactly (below); for x = v * 3.1875 >= 0
     // (at most 30 significant bits, < 256) x + 0.5 is exact, so round-half-
     // away-from-zero is floor(x + 0.5).  Selects instead of branches; the
     // product is computed, and discarded, for out-of-range v and NaN.
     const uint32_t r = (uint32_t)__builtin_floor((double)v * 3.1875 + 0.5);
     return v > vmax ? (uint8_t)255u : v >= vmin ? (uint8_t)r : (uint8_t)0u;
-#else
-    if (v < vmin) return 0;
-    if (v > vmax) return 255;
-    if (v != v) return 0;
-    // 255.0 * v / 80.0 == v * 3.1875 exactly: 255*v is exact in f64 and the
-    // quotient 51*v/16 has at most 30 significant bits, so the correctly
-    // rounded division returns it unchanged (checked for every f32 in
-    // [0, 80]: tools/check_fp_identities.c).
-    return (uint8_t)__builtin_round((double)(v - vmin) * 3.1875);
-#endif
 }
 
 }  // namespace XRT_KERNEL_NS

@@ -466,13 +466,6 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         distance = xrt_f32_from_bits(kX86DefaultNaN);
         lval = distance;
     }
-    if (ablation(p) & (kAblateStores | kAblateShade)) {
-        if (!(ablation(p) & kAblateStores)) {
-            if (out.image) out.image[o] = distance;
-            if (out.lbuffer) out.lbuffer[o] = lval;
-        }
-        return;
-    }
     // distance 0 (a miss or an odd count) shades to 80 * expf(-0) = 80 -> 255;
     // the wave skips expf and the LUT when none of its rays needs them.
     float photon = 80.0f;
@@ -715,8 +708,7 @@ __device__ __forceinline__ float test_lds(const StageLDS& st, uint32_t k, float 
 // scheduler to interleave), then pushed in ascending staged order.  The hit
 // set, and so the sorted list, does not depend on the pairing.
 __device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t count, float xc,
-                                                float yc, float dx, float dy, float dz, HitList& hl,
-                                                uint32_t ablate)
+                                                float yc, float dx, float dy, float dz, HitList& hl)
 {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t tests = 0;
@@ -725,24 +717,19 @@ __device__ __forceinline__ uint32_t test_staged(const StageLDS& st, uint32_t cou
         const bool pass = k < count && edges_pass_tile(st.e0[k], st.e1[k], st.e2[k], xc, yc);
         unsigned long long m = __ballot(pass);
         tests += (uint32_t)__popcll(m);
-        if (ablate & kAblateExact) m = 0ull;
         while (m) {
             const uint32_t k0 = base + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
             bool h0, h1 = false;
             const float t0 = test_lds(st, k0, dx, dy, dz, h0);
             float t1 = 0.0f;
-            if (XRT_PAIR && m) {                              // wave-uniform
+            if (m) {                                          // wave-uniform
                 const uint32_t k1 = base + (uint32_t)__builtin_ctzll(m);
                 m &= m - 1ull;
                 t1 = test_lds(st, k1, dx, dy, dz, h1);
             }
-            if (ablate & kAblatePush) {
-                hl.n += (h0 ? 1u : 0u) + (h1 ? 1u : 0u);
-            } else {
-                hl.push_if(h0, t0);
-                hl.push_if(h1, t1);
-            }
+            hl.push_if(h0, t0);
+            hl.push_if(h1, t1);
         }
     }
     return tests;
@@ -758,7 +745,6 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_in_block();
     const uint32_t T = p.num_triangles;
-    if (ablation(p) & kAblateCandidates) n_cand = 0;
     const bool once = n_cand <= kStage;
     if (once) {
         stage_candidates(st, recs, culls, T, 0u, n_cand, fetch);
@@ -774,20 +760,20 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
 
         float dx = 0.0f, dy = 0.0f, dz = 0.0f;
-        if (tile_live && !(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
+        if (tile_live) make_tile_ray(p, out, row, col, dx, dy, dz);
         else dx = 1.0f;
         HitList hl;
         hl.init();
         uint32_t tests = 0;
         if (once) {
-            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl, ablation(p));
+            if (tile_live) tests = test_staged(st, n_cand, xc, yc, dx, dy, dz, hl);
         } else {
             for (uint32_t first = 0; first < n_cand; first += kStage) {
                 const uint32_t count = min(kStage, n_cand - first);
                 __syncthreads();
                 stage_candidates(st, recs, culls, T, first, count, fetch);
                 __syncthreads();
-                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl, ablation(p));
+                if (tile_live) tests += test_staged(st, count, xc, yc, dx, dy, dz, hl);
             }
         }
         if (tile_live) {
@@ -801,7 +787,7 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
 // k_render_tiled: one 32x32 region per workgroup.  Phase 1: the 256 lanes
 // sweep the footprint boxes of the whole mesh (every region sees every
 // triangle) and compact the region's candidates into an LDS list.
-__global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriRec* __restrict__ recs,
+__global__ __launch_bounds__(256) void k_render_tiled(const TriRec* __restrict__ recs,
                                                       const float4* __restrict__ culls,
                                                       RenderParams p, Outputs out)
 {
@@ -825,7 +811,7 @@ __global__ __launch_bounds__(256) XRT_CULLED_ATTR void k_render_tiled(const TriR
     // workgroup starts at a different chunk so concurrent reads spread over
     // the L2 channels.
     const float fx0 = (float)rx0, fx1 = (float)rx1, fy0 = (float)ry0, fy1 = (float)ry1;
-    const uint32_t nchunks = (ablation(p) & kAblateSweep) ? 0u : (T + 1023u) / 1024u;
+    const uint32_t nchunks = (T + 1023u) / 1024u;
     uint32_t chunk =
         nchunks ? (uint32_t)(((uint64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 2654435761u) % nchunks) : 0u;
     for (uint32_t c = 0; c < nchunks; ++c, chunk = (chunk + 1u == nchunks) ? 0u : chunk + 1u) {
@@ -876,33 +862,73 @@ struct Footprint {
 // vertices are intersections of two of its seven boundary lines; candidate
 // vertices are accepted with a generous tolerance (so the box can only grow).
 // Leaves `box` unchanged (unbounded: never culled by the box) if none is found.
-__device__ void clipped_box(const double A[3], const double B[3], const double C[3], double W,
-                            double H, float4& box)
+// One of three doubles by a uniform index, as bit masks (a select chain the
+// optimiser would turn into an indexed table in scratch memory).
+__device__ __forceinline__ double pick3(uint32_t k, double x0, double x1, double x2)
 {
-    const double LA[7] = {A[0], A[1], A[2], 1.0, -1.0, 0.0, 0.0};
-    const double LB[7] = {B[0], B[1], B[2], 0.0, 0.0, 1.0, -1.0};
-    const double LC[7] = {C[0], C[1], C[2], 1.0, W, 1.0, H};
+    const uint64_t m0 = 0ull - (uint64_t)(k == 0u), m1 = 0ull - (uint64_t)(k == 1u), m2 = 0ull - (uint64_t)(k == 2u);
+    return __longlong_as_double((long long)(((uint64_t)__double_as_longlong(x0) & m0) |
+                                            ((uint64_t)__double_as_longlong(x1) & m1) |
+                                            ((uint64_t)__double_as_longlong(x2) & m2)));
+}
+
+struct ClipEdges {
+    double a0, a1, a2, b0, b1, b2, c0, c1, c2;
+};
+
+// Line k of the seven: k < 3 the edge (A_k x + B_k y + C_k >= 0), then the
+// image rectangle's x >= -1, x <= W, y >= -1, y <= H.
+__device__ __forceinline__ void clip_line(uint32_t k, const ClipEdges& e, double W, double H, double& la,
+                                          double& lb, double& lc)
+{
+    if (k < 3u) {
+        la = pick3(k, e.a0, e.a1, e.a2);
+        lb = pick3(k, e.b0, e.b1, e.b2);
+        lc = pick3(k, e.c0, e.c1, e.c2);
+    } else {
+        la = k == 3u ? 1.0 : k == 4u ? -1.0 : 0.0;
+        lb = k < 5u ? 0.0 : k == 5u ? 1.0 : -1.0;
+        lc = k == 3u ? 1.0 : k == 4u ? W : k == 5u ? 1.0 : H;
+    }
+}
+
+// The 21 pairs are walked in a rolled loop (lines selected, not indexed): this
+// rare path (unbounded footprints) fully unrolled set the kernel's register
+// footprint (112 VGPRs; 72 without it).
+__device__ __forceinline__ void clipped_box(const double A[3], const double B[3], const double C[3], double W,
+                                            double H, float4& box)
+{
+    const ClipEdges e = {A[0], A[1], A[2], B[0], B[1], B[2], C[0], C[1], C[2]};
     double xmin = __builtin_inf(), xmax = -__builtin_inf();
     double ymin = __builtin_inf(), ymax = -__builtin_inf();
     bool any = false;
-    for (int a = 0; a < 7; ++a) {
-        for (int b = a + 1; b < 7; ++b) {
-            const double det = LA[a] * LB[b] - LA[b] * LB[a];
-            const double scale = (fabs(LA[a]) + fabs(LB[a])) * (fabs(LA[b]) + fabs(LB[b]));
-            if (!(fabs(det) > 1e-9 * scale)) continue;           // parallel (or NaN)
-            const double x = (LB[a] * LC[b] - LB[b] * LC[a]) / det;
-            const double y = (LA[b] * LC[a] - LA[a] * LC[b]) / det;
-            bool ok = isfinite(x) && isfinite(y);
-            for (int k = 0; k < 7 && ok; ++k) {
-                const double v = LA[k] * x + LB[k] * y + LC[k];
-                const double tol = 1e-6 * (fabs(LA[k] * x) + fabs(LB[k] * y) + fabs(LC[k])) + 1e-6;
-                ok = v >= -tol;
-            }
-            if (ok) {
-                xmin = fmin(xmin, x); xmax = fmax(xmax, x);
-                ymin = fmin(ymin, y); ymax = fmax(ymax, y);
-                any = true;
-            }
+#pragma unroll 1
+    for (uint32_t pr = 0; pr < 21u; ++pr) {
+        // pair (a, b), a < b: (0,1) (0,2) ... (0,6) (1,2) ... (5,6)
+        uint32_t a = 0, rest = pr;
+        while (rest >= 6u - a) { rest -= 6u - a; ++a; }
+        const uint32_t b = a + 1u + rest;
+        double la, lb_, lc, ma, mb, mc;
+        clip_line(a, e, W, H, la, lb_, lc);
+        clip_line(b, e, W, H, ma, mb, mc);
+        const double det = la * mb - ma * lb_;
+        const double scale = (fabs(la) + fabs(lb_)) * (fabs(ma) + fabs(mb));
+        if (!(fabs(det) > 1e-9 * scale)) continue;           // parallel (or NaN)
+        const double x = (lb_ * mc - mb * lc) / det;
+        const double y = (ma * lc - la * mc) / det;
+        bool ok = isfinite(x) && isfinite(y);
+#pragma unroll
+        for (uint32_t k = 0; k < 7u; ++k) {
+            double qa, qb, qc;
+            clip_line(k, e, W, H, qa, qb, qc);
+            const double v = qa * x + qb * y + qc;
+            const double tol = 1e-6 * (fabs(qa * x) + fabs(qb * y) + fabs(qc)) + 1e-6;
+            ok = ok && v >= -tol;
+        }
+        if (ok) {
+            xmin = fmin(xmin, x); xmax = fmax(xmax, x);
+            ymin = fmin(ymin, y); ymax = fmax(ymax, y);
+            any = true;
         }
     }
     if (!any) return;
@@ -1532,7 +1558,7 @@ __device__ __forceinline__ void stage_mesh(RegionStage& st, const float4* __rest
 }
 
 __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
-                                                float dz, HitList& hl, bool push = true)
+                                                float dz, HitList& hl)
 {
     // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[7].x)
     const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k];
@@ -1540,19 +1566,13 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
-#if XRT_RCP_FALLTHROUGH
     // the short reciprocal on every survivor, the IEEE division only behind one
     // rarely taken wave-uniform branch (straight-line common path)
     float inv = rcp_newton(det);
     if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) inv = inv_det_of(det);
-#else
-    const float inv = __builtin_expect(__ballot(!rcp_newton_exact_for(det)) == 0ull, 1) ? rcp_newton(det)
-                                                                                      : inv_det_of(det);
-#endif
     bool h;
     const float t = mt_finish_inv(det, inv, u, v, tnum, h);
-    if (push) hl.push_if(h, t);
-    else hl.n += h && t < 1e30f ? 1u : 0u;         // XRT_ABLATE kAblatePush: the test without the insert
+    hl.push_if(h, t);
 }
 
 // The signed model's: the term's triangle id from the footprint (e0.w) and its
@@ -1588,7 +1608,7 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
     const RegionEntry* __restrict__ glob = bins.global_list;
     const uint32_t T = p.num_triangles;
     const bool whole = n_local > d_cap;   // the list overflowed: whole mesh (exact, slower)
-    const uint32_t n_cand = (ablation(p) & kAblateCandidates) ? 0u : whole ? T : n_local + n_glob;
+    const uint32_t n_cand = whole ? T : n_local + n_glob;
     cand = n_cand;
 
     const uint32_t tx0 = reg_x * kRegion + (tile & 3u) * 8u;
@@ -1607,12 +1627,10 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
     bool have_ray = false;                         // wave-uniform
-#if XRT_PREFETCH_OFFSETS
     // the tile's pixel offsets, loaded beside the region's counts: a tile with
     // survivors generates its rays without another memory round trip
     const float pre_v = out.off.v[min(row, p.height - 1u)];
     const float pre_u = out.off.u[min(col, p.width - 1u)];
-#endif
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
@@ -1635,15 +1653,9 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
             if (!m) continue;
             tests += (uint32_t)__popcll(m);
             if (!have_ray) {
-#if XRT_PREFETCH_OFFSETS
                 make_ray_from(*out.frame, pre_v, pre_u, dx, dy, dz, sx, sy, sz);
-#else
-                if constexpr (kSigned) make_tile_ray(p, out, row, col, dx, dy, dz, sx, sy, sz);
-                else if (!(ablation(p) & kAblateRayGen)) make_tile_ray(p, out, row, col, dx, dy, dz);
-#endif
                 have_ray = true;
             }
-            if (ablation(p) & kAblateExact) continue;
             if constexpr (kSigned) {
                 while (m) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(m);
@@ -1654,7 +1666,7 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
                 while (m) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(m);
                     clear_lane_bit(m, b);
-                    test_staged_one(st, k0 + b, dx, dy, dz, hl, !(ablation(p) & kAblatePush));
+                    test_staged_one(st, k0 + b, dx, dy, dz, hl);
                 }
             }
         }
@@ -1675,7 +1687,7 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
         if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
     } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
         ws.rays += (uint32_t)__popcll(__ballot(active));
-        if (active && !(ablation(p) & kAblateStores)) {
+        if (active) {
             if (out.image) out.image[o] = 80.0f;
             if (out.lbuffer) out.lbuffer[o] = out.miss_l;
             if (out.image_u8) out.image_u8[o] = 255u;
@@ -1702,7 +1714,7 @@ __device__ __forceinline__ void fill_region_rows(const RenderParams& p, const Ou
         if (col < p.width && row < p.row_end) {
             ++n;
             const size_t o = (size_t)(row - p.row_begin) * p.width + col;
-            if (!(ablation(p) & kAblateStores) && !out.packed) {
+            if (!out.packed) {
                 if (out.image) out.image[o] = 80.0f;
                 if (out.lbuffer) out.lbuffer[o] = out.miss_l;
                 if (out.image_u8) out.image_u8[o] = 255u;
@@ -1753,12 +1765,11 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         }
         return;
     }
-#if XRT_XCD_REMAP
     // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
     // each run of 8 regions, give XCD x all workgroups of region x, so a region's
     // candidate list and triangle records are cached by one L2 instead of four.
     // A bijection on full runs of the tile workgroups; the tail keeps the identity.
-    constexpr uint32_t kPerXcd = XRT_XCD_REMAP * kBlocksPerRegion;   // XRT_XCD_REMAP regions per XCD per run
+    constexpr uint32_t kPerXcd = kBlocksPerRegion;                   // one region per XCD per run
     constexpr uint32_t kRun = 8u * kPerXcd;
     uint32_t blk = blockIdx.x;
     if (blk < (tile_blocks / kRun) * kRun) {
@@ -1766,9 +1777,6 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         blk = (blk - within) + (within & 7u) * kPerXcd + (within >> 3);
     }
     const uint32_t g = blk * kTileWaves + wave;                      // wave of the grid
-#else
-    const uint32_t g = blockIdx.x * kTileWaves + wave;               // wave of the grid
-#endif
     const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
     render_tile<kSigned>(st, recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);

@@ -349,8 +349,7 @@ RenderParams make_params(const xrt_camera& c, uint32_t row_begin, uint32_t row_e
     p.row_end = row_end;
     p.num_triangles = (uint32_t)T;
     p.hit_capacity = capacity;
-    const char* ab = std::getenv("XRT_ABLATE");   // timing studies only
-    p.ablate = ab ? (uint32_t)std::strtoul(ab, nullptr, 0) : 0u;
+    p.pad_ = 0u;
     return p;
 }
 

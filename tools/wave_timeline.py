@@ -83,6 +83,20 @@ out["slowest"] = [{"record": int(k), "start_us": round(float(s[k]), 2), "dur_us"
                    "rays": int(rec[k, 0]), "hit_rays": int(rec[k, 1]), "overflow_rays": int(rec[k, 3]),
                    "hits": int(rec[k, 4]), "tile_tests": int(rec[k, 5]), "candidates": int(rec[k, 6]),
                    "max_hits": int(rec[k, 7])} for k in slow]
+# tile workgroups (4 tile waves each, ahead of the fill plan's records): how
+# many have no survivor in any of their tiles, and what their waves cost
+tile = rec[:, 0] <= 64
+n_tile = int(np.argmin(tile)) if not tile.all() else len(rec)
+n_wg = n_tile // 4
+tt = rec[:n_wg * 4, 5].reshape(n_wg, 4)
+dd = dur[:n_wg * 4].reshape(n_wg, 4)
+dead_wg = (tt == 0).all(axis=1)
+part_wg = (tt == 0).any(axis=1) & ~dead_wg
+out["tile_workgroups"] = {"n": n_wg, "all_tiles_without_survivor": int(dead_wg.sum()),
+                          "some_tiles_without_survivor": int(part_wg.sum()),
+                          "dead_wg_wave_us": float(dd[dead_wg].sum()),
+                          "dead_waves_in_mixed_wg_us": float(dd[part_wg][tt[part_wg] == 0].sum()),
+                          "all_tile_wave_us": float(dd.sum())}
 ov = live & (rec[:, 3] > 0)
 out["overflow_waves"] = {"n": int(ov.sum()), "dur_us_median": float(np.median(dur[ov])) if ov.any() else None,
                          "dur_us_sum": float(dur[ov].sum()) if ov.any() else 0.0}
