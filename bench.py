@@ -69,8 +69,10 @@ def parse():
     ap.add_argument("--transit", choices=["packed", "dense"], default="packed",
                     help="strips mode: send the regions the strip's fill plan did not fill (packed) or the "
                          "whole L-buffer strip (dense)")
-    ap.add_argument("--root-share", default="auto",
-                    help="strips mode: fraction of the rows rank 0 renders ('auto': strips.root_share, "
+    ap.add_argument("--root-share", default="balanced",
+                    help="strips mode: 'balanced' (default): strips from the frame's measured per-band render "
+                         "cost and packed bytes and the measured link rate (strips.balanced_bounds); or the "
+                         "fraction of the rows rank 0 renders first ('auto': strips.root_share, "
                          "'equal': H/N each as the reference's row partition)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses device 0 (with --dist-backend gloo)")
@@ -154,6 +156,68 @@ def end_to_end(args, W, H, device_index, kernel):
                     "image, L-buffer and u8 (context creation excluded)"}
 
 
+def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32):
+    """Inputs of strips.balanced_bounds from one binned render of the whole frame
+    (rank 0, untimed): per band of 32 rows, its share of the render (the waves'
+    in-kernel timing records, scaled to the frame's span, in us) and the bytes
+    its packed strip sends (a 32x32 block per region the fill plan leaves)."""
+    import numpy as np
+    dev = torch.device("cuda", device_index)
+    img = torch.empty(W * H, dtype=torch.float32, device=dev)
+    lb = torch.empty(W * H, dtype=torch.float32, device=dev)
+    u8 = torch.empty(W * H, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    with xrt.Context(device_index) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(tris)
+        for _ in range(6):
+            c.render_rows_device(cam, 0, H, img.data_ptr(), lb.data_ptr(), u8.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t = c.wave_times().astype(np.int64)
+        span_us = c.read_stats().kernel_ms * 1e3
+        rmap, n_packed = c.plan_region_map(W, H)
+    rx, ry = -(-W // 32), -(-H // 32)
+    dur = ((t[:, 1] - t[:, 0]) % 2**32).astype(np.float64)         # ticks, per statistics record
+    per_slot = dur.reshape(-1, 16).sum(axis=1)                       # 16 records per region slot
+    region_cost = np.zeros(rx * ry)
+    unfilled = rmap != 0xFFFFFFFF
+    region_cost[unfilled] = per_slot[rmap[unfilled].astype(np.int64)]
+    if (~unfilled).any():                                            # the fill plan's regions, evenly
+        region_cost[~unfilled] = per_slot[n_packed:].sum() / (~unfilled).sum()
+    band_wave = region_cost.reshape(ry, rx).sum(axis=1)
+    band_cost = band_wave / max(band_wave.sum(), 1e-9) * span_us
+    band_bytes = 4096.0 * unfilled.reshape(ry, rx).sum(axis=1)
+    return band_cost, band_bytes, span_us
+
+
+def measure_link(dist, torch, world, rank, dev, nccl, nbytes=4 << 20, reps=5):
+    """Bytes per microsecond one sender delivers into rank 0 while every sender
+    sends at once (the gather's pattern), measured with the bench's backend."""
+    import time as _t
+    where = dev if nccl else "cpu"
+    buf = torch.ones(nbytes // 4, dtype=torch.float32, device=where)
+    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+
+    def once():
+        if rank == 0:
+            ops = [dist.P2POp(dist.irecv, bufs[g], g) for g in range(1, world)]
+        else:
+            ops = [dist.P2POp(dist.isend, buf, 0)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        if nccl:
+            torch.cuda.synchronize(dev)
+    once()
+    dist.barrier()
+    t0 = _t.perf_counter()
+    for _ in range(reps):
+        once()
+    dt = (_t.perf_counter() - t0) / reps
+    rate = torch.tensor([nbytes / (dt * 1e6)], dtype=torch.float64, device=where)
+    dist.broadcast(rate, src=0)
+    return float(rate.item())
+
+
 def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_s, launches):
     """The dominant kernel's roofline (DESIGN.md "Measurement").
 
@@ -222,7 +286,8 @@ def main():
 
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.scenes import orbit_camera, tiled_mesh
-    from simpleraytracing_amd.strips import root_share, strip_bounds, unpack_descriptors, weighted_bounds
+    from simpleraytracing_amd.strips import (balanced_bounds, gather_step_us, root_share, strip_bounds,
+                                             unpack_descriptors, weighted_bounds)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -264,9 +329,29 @@ def main():
     gathering = strips and world > 1
     # Row strips.  The root's own rows need no transfer: by default it renders a
     # larger first strip (strips.root_share), the others split the rest.
+    split_info = None
+    balanced = (strips and world > 1 and args.root_share == "balanced" and args.kernel in ("auto", "binned")
+                and -(-H // 32) >= world)
     if args.root_share == "equal" or not strips:
         share0 = None
         bounds = [strip_bounds(H, world, g) for g in range(world)]
+    elif balanced:
+        # the frame's per-band cost and bytes (rank 0) and the link rate (every
+        # rank): strips that balance the root's render against the senders'
+        # renders and transfers (strips.balanced_bounds), sent to every rank
+        share0 = None
+        link = measure_link(dist, torch, world, rank, dev, nccl)
+        flat = torch.zeros(2 * world, dtype=torch.int64, device=dev if nccl else "cpu")
+        if rank == 0:
+            band_cost, band_bytes, span_us = band_model(xrt, torch, tris, cam, W, H, device_index)
+            b = balanced_bounds(band_cost, band_bytes, world, link, H, unpack_us=5.0)
+            flat.copy_(torch.tensor([v for be in b for v in be], dtype=torch.int64))
+            split_info = {"link_bytes_per_us": link, "frame_span_us": span_us,
+                          "predicted_step_us": gather_step_us(b, band_cost, band_bytes, link),
+                          "band_rows": 32}
+        dist.broadcast(flat, src=0)
+        v = flat.cpu().tolist()
+        bounds = [(int(v[2 * g]), int(v[2 * g + 1])) for g in range(world)]
     else:
         share0 = root_share(world) if args.root_share == "auto" else float(args.root_share)
         bounds = [weighted_bounds(H, world, g, share0) for g in range(world)]
@@ -297,8 +382,7 @@ def main():
         ctx.set_miss_code(xrt.XRT_MISS_TRANSIT)
         tbufs = [torch.zeros((r1 - r0) * W, dtype=torch.float32, device=dev) for _ in range(2)]
         pending = [None, None]
-    rest = (H - bounds[0][1]) * W            # rows of strips 1 .. n-1 on rank 0
-    o0 = bounds[0][1] * W
+    rest = W * H - (r1 - r0) * W if strips else 0     # pixels of the other ranks' strips
     frame_no = [0]
 
     # Packed transit: a sender's strip travels as the 32x32 blocks of the regions
@@ -365,9 +449,11 @@ def main():
         if packed:
             ctx.unpack_blocks_device(W, n_desc, d_desc.data_ptr(), rbuf.data_ptr(), lb.data_ptr(), img.data_ptr(),
                                      u8.data_ptr(), stream.cuda_stream)
-        else:
-            ctx.expand_rows_device(rest, lb.data_ptr() + 4 * o0, img.data_ptr() + 4 * o0, u8.data_ptr() + o0,
-                                   stream.cuda_stream)
+        else:                                 # the received rows, above and below the root's strip
+            for b0, e0 in ((0, bounds[0][0]), (bounds[0][1], H)):
+                if e0 > b0:
+                    ctx.expand_rows_device((e0 - b0) * W, lb.data_ptr() + 4 * b0 * W, img.data_ptr() + 4 * b0 * W,
+                                           u8.data_ptr() + b0 * W, stream.cuda_stream)
 
     def step():
         k = frame_no[0]
@@ -447,7 +533,8 @@ def main():
                   "transit": ("L-buffer strips, misses as XRT_MISS_TRANSIT, packed by region (the regions "
                               "each strip's fill plan filled stay behind)") if packed
                   else "L-buffer strips, misses as XRT_MISS_TRANSIT",
-                  "strip_rows": [e - b for b, e in bounds], "root_share": share0}
+                  "strip_rows": [e - b for b, e in bounds], "strips": bounds, "root_share": share0,
+                  "split": split_info or ("balanced" if balanced else args.root_share)}
 
     result = None
     if rank == 0:

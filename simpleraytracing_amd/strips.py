@@ -51,6 +51,115 @@ def weighted_bounds(height: int, n: int, rank: int, share0: float):
     return r0 + b, r0 + e
 
 
+def balanced_bounds(band_cost, band_bytes, n: int, link_bytes_per_us: float, height: int,
+                    band_rows: int = 32, unpack_us: float = 5.0):
+    """Row strips for a gather-bound frame: every rank's rows, [begin, end),
+    from per-band costs (band = `band_rows` image rows, the region height, so
+    each strip's region grid is the frame's): band_cost[b] = render time of
+    band b (us), band_bytes[b] = the bytes its packed strip sends to rank 0.
+
+    The root's own rows need no transfer, a sender's cost it max(render,
+    bytes / link) on its own link, and frame k's gather overlaps frame k+1's
+    render, so the step is the largest of: the root's render (+ the unpack),
+    each sender's render and each sender's transfer.  The root takes ONE
+    contiguous run of bands anywhere in the frame (the dense middle of the
+    object, whose bytes would cost the most on a link); the senders split the
+    bands above and below it into contiguous strips, in frame order (ranks 1..
+    above, then below).  Minimises the step by a search over it (greedy
+    feasibility per candidate step).  Every rank keeps at least one band when
+    there are n bands or more."""
+    cost = [float(c) for c in band_cost]
+    byts = [float(b) for b in band_bytes]
+    nb = len(cost)
+    if nb != len(byts) or nb == 0:
+        raise ValueError("band_cost and band_bytes must have one entry per band")
+    if n <= 1:
+        return [(0, height)]
+    if nb < n:
+        raise ValueError("fewer bands than ranks")
+    link = max(float(link_bytes_per_us), 1e-9)
+    pre_c = [0.0]
+    pre_b = [0.0]
+    for c, b in zip(cost, byts):
+        pre_c.append(pre_c[-1] + c)
+        pre_b.append(pre_b[-1] + b)
+
+    def sender_cost(i, j):            # bands [i, j) on one sender
+        return max(pre_c[j] - pre_c[i], (pre_b[j] - pre_b[i]) / link)
+
+    def pieces(i, j, step):           # fewest senders covering [i, j) within step (greedy); None: impossible
+        k, a = 0, i
+        while a < j:
+            b = a + 1
+            if sender_cost(a, b) > step:
+                return None
+            while b < j and sender_cost(a, b + 1) <= step:
+                b += 1
+            k, a = k + 1, b
+        return k
+
+    def plan(step):                   # (a, b): the root's run of bands, or None
+        for a in range(nb):
+            # the longest run from a within the step that leaves a band for every sender
+            b = None
+            for e in range(nb, a, -1):
+                if a + (nb - e) >= n - 1 and pre_c[e] - pre_c[a] + unpack_us <= step:
+                    b = e
+                    break
+            if b is None:
+                continue
+            ka, kb = pieces(0, a, step), pieces(b, nb, step)
+            if ka is not None and kb is not None and ka + kb <= n - 1:
+                return a, b           # the senders left over split pieces (never raises the step)
+        return None
+
+    lo, hi = 0.0, pre_c[nb] + unpack_us + pre_b[nb] / link
+    root = plan(hi)
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        r = plan(mid)
+        if r is None:
+            lo = mid
+        else:
+            hi, root = mid, r
+    a, b = root
+    # senders: greedy pieces within the step found, then split until n - 1 pieces
+    step = hi
+
+    def split(i, j):
+        out, s0 = [], i
+        while s0 < j:
+            e = s0 + 1
+            while e < j and sender_cost(s0, e + 1) <= step:
+                e += 1
+            out.append([s0, e])
+            s0 = e
+        return out
+    above, below = split(0, a), split(b, nb)
+    while len(above) + len(below) < n - 1:
+        cand = [(sender_cost(x, y), k, side) for side, lst in ((0, above), (1, below))
+                for k, (x, y) in enumerate(lst) if y - x >= 2]
+        if not cand:
+            raise ValueError("cannot give every rank a band")
+        _, k, side = max(cand)
+        lst = above if side == 0 else below
+        x, y = lst[k]
+        m = (x + y) // 2
+        lst[k:k + 1] = [[x, m], [m, y]]
+    rows = lambda band: min(band * band_rows, height)                        # noqa: E731
+    return [(rows(a), rows(b))] + [(rows(x), rows(y)) for x, y in above + below]
+
+
+def gather_step_us(bounds, band_cost, band_bytes, link_bytes_per_us: float, band_rows: int = 32,
+                   unpack_us: float = 5.0) -> float:
+    """The step bounds imply under balanced_bounds' model (us)."""
+    def band(r):
+        return -(-r // band_rows)
+    cost = [sum(band_cost[band(b0):band(e0)]) for b0, e0 in bounds]
+    byts = [sum(band_bytes[band(b0):band(e0)]) for b0, e0 in bounds]
+    return max([cost[0] + unpack_us] + [max(c, b / link_bytes_per_us) for c, b in zip(cost[1:], byts[1:])])
+
+
 EMPTY = 0xFFFFFFFF
 
 

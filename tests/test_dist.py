@@ -118,3 +118,89 @@ def test_gloo_gather_assembles_full_frame(tmp_path, world, W, H):
     assert np.array_equal(got["img"].view(np.uint32), ref[0].view(np.uint32))
     assert np.array_equal(got["lb"].view(np.uint32), ref[1].view(np.uint32))
     assert np.array_equal(got["u8"], ref[2])
+
+
+def _brute_best_step(cost, byts, n, link, unpack):
+    """The smallest step over every layout balanced_bounds may choose: one
+    contiguous root run, the bands above and below it cut into n - 1 non-empty
+    contiguous sender strips."""
+    import itertools
+    nb = len(cost)
+
+    def c(i, j):
+        return sum(cost[i:j])
+
+    def s(i, j):
+        return max(c(i, j), sum(byts[i:j]) / link)
+    best = float("inf")
+    for a in range(nb):
+        for b in range(a + 1, nb + 1):
+            outside = [(0, a), (b, nb)]
+            for k_above in range(0, n):
+                k_below = n - 1 - k_above
+                if k_above > a or k_below > nb - b or (k_above == 0) != (a == 0) or (k_below == 0) != (b == nb):
+                    continue
+                for cuts_a in itertools.combinations(range(1, a), max(k_above - 1, 0)):
+                    ea = [0, *cuts_a, a] if k_above else []
+                    for cuts_b in itertools.combinations(range(b + 1, nb), max(k_below - 1, 0)):
+                        eb = [b, *cuts_b, nb] if k_below else []
+                        parts = [(ea[i], ea[i + 1]) for i in range(len(ea) - 1)] + \
+                                [(eb[i], eb[i + 1]) for i in range(len(eb) - 1)]
+                        step = max([c(a, b) + unpack] + [s(i, j) for i, j in parts])
+                        best = min(best, step)
+            del outside
+    return best
+
+
+def test_balanced_bounds_optimal_small():
+    """strips.balanced_bounds (bench.py --root-share balanced): contiguous strips
+    covering the frame, every rank non-empty, and a step within 0.1 % of the best
+    layout of its family, found by brute force on small random band costs."""
+    from simpleraytracing_amd.strips import balanced_bounds, gather_step_us
+    rng = np.random.default_rng(7)
+    for trial in range(40):
+        nb = int(rng.integers(3, 9))
+        n = int(rng.integers(1, min(nb, 4) + 1))
+        cost = rng.uniform(0.1, 10.0, nb)
+        byts = rng.uniform(0.0, 2e5, nb) * (rng.uniform(size=nb) > 0.3)
+        link = float(rng.uniform(5e3, 8e4))
+        H = 32 * nb - int(rng.integers(0, 31))
+        b = balanced_bounds(cost, byts, n, link, H, unpack_us=1.0)
+        assert len(b) == n
+        cover = sorted(b)
+        assert cover[0][0] == 0 and cover[-1][1] == H
+        assert all(cover[i][1] == cover[i + 1][0] for i in range(n - 1)) and all(e > s for s, e in b)
+        assert all(s0 % 32 == 0 for s0, _ in b)
+        if n == 1:
+            continue
+        got = gather_step_us(b, cost, byts, link, unpack_us=1.0)
+        best = _brute_best_step(list(cost), list(byts), n, link, 1.0)
+        assert got <= best * 1.001 + 1e-9, (trial, got, best, b)
+
+
+def _link_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rate = bench.measure_link(dist, torch, world, rank, None, False, nbytes=1 << 16, reps=2)
+    rates = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(rates, torch.tensor([rate], dtype=torch.float64))
+    if rank == 0:
+        np.save(out_path, np.array([float(r.item()) for r in rates]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_link_rate_agreed(tmp_path, world):
+    """bench.measure_link under gloo: every sender sends to rank 0 at once, rank 0
+    times it and every rank ends with the same positive rate (the balanced
+    split is computed from it on rank 0 and broadcast)."""
+    out = str(tmp_path / "rates.npy")
+    mp.spawn(_link_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rates = np.load(out)
+    assert rates.shape == (world,) and rates[0] > 0 and np.all(rates == rates[0])

@@ -918,7 +918,9 @@ def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
 
 
 @pytest.mark.parametrize("transit,ranks,share", [("packed", 2, "auto"), ("dense", 2, "auto"),
-                                                  ("packed", 3, "equal"), ("dense", 3, "0.5")])
+                                                  ("packed", 3, "equal"), ("dense", 3, "0.5"),
+                                                  ("packed", 3, "balanced"), ("dense", 2, "balanced"),
+                                                  ("packed", 4, "balanced")])
 def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share):
     """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
     packed by region or dense --, expanded there) with 2 ranks on the one GPU
@@ -944,6 +946,11 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share):
     assert sum(rows) == 512 and len(rows) == ranks
     if share == "equal":
         assert max(rows) - min(rows) <= 1
+    elif share == "balanced":                     # band-aligned strips, the root's anywhere in the frame
+        spans = sorted(map(tuple, g["strips"]))
+        assert spans[0][0] == 0 and spans[-1][1] == 512 and all(s0 % 32 == 0 for s0, _ in spans)
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(ranks - 1))
+        assert g["split"]["link_bytes_per_us"] > 0 and g["split"]["predicted_step_us"] > 0
     else:
         assert rows[0] > 512 // ranks
     if transit == "packed":

@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
-"""Bytes a frame's row strips send to rank 0 under packed transit (bench.py
---transit packed) against dense L-buffer strips, for an N-way split.
+"""Multi-GPU model inputs for bench.py's strips mode, measured on one GPU:
+for an N-way split of the frame (the root-weighted split bench.py uses by
+default, strips.root_share, and the reference's equal H/N split), each strip's
+render time (its own context, steady frames, in-kernel spans) and the bytes its
+packed L-buffer strip sends to rank 0, against dense strips.  The predicted
+step per link rate is max(root strip render + unpack, slowest sender render,
+largest sender transfer) -- the gather of frame k overlaps the render of frame
+k+1, each sender has its own link into rank 0 (DESIGN.md "Multi-GPU").
 
-    python tools/transit_sizes.py [--size W H] [--ranks 2 4 8]
+    python tools/transit_sizes.py [--size W H] [--ranks 1 2 4 8] [--link-gbs 64 128]
 """
 import argparse
 import json
@@ -13,35 +19,67 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--size", type=int, nargs=2, default=[4096, 4096])
-    ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
-    args = ap.parse_args()
-    import torch
-    import simpleraytracing_amd as xrt
-    from simpleraytracing_amd.strips import strip_bounds
-    W, H = args.size
-    tris = xrt.load_ply(os.path.join(ROOT, "data", "dragon.ply"))
-    cam = xrt.camera_for_mesh(tris, W, H)
+def strip_time_ms(xrt, torch, tris, cam, r0, r1, W, frames, miss_code):
     dev = torch.device("cuda", 0)
-    out = {}
     with xrt.Context(0) as ctx:
         ctx.upload_mesh(tris)
         ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
-        ctx.set_miss_code(xrt.XRT_MISS_TRANSIT)
+        if miss_code:
+            ctx.set_miss_code(xrt.XRT_MISS_TRANSIT)
+        lb = torch.empty((r1 - r0) * W, device=dev)
+        img = torch.empty((r1 - r0) * W, device=dev) if not miss_code else None
+        u8 = torch.empty((r1 - r0) * W, dtype=torch.uint8, device=dev) if not miss_code else None
+        args = (img.data_ptr() if img is not None else 0, lb.data_ptr(), u8.data_ptr() if u8 is not None else 0)
+        for _ in range(5):
+            ctx.render_rows_device(cam, r0, r1, *args, 0)
+        torch.cuda.synchronize()
+        ctx.timing_begin()
+        for _ in range(frames):
+            ctx.render_rows_device(cam, r0, r1, *args, 0)
+        torch.cuda.synchronize()
+        ms, n = ctx.timing_end()
+        _, n_packed = ctx.plan_region_map(W, r1 - r0)
+    return ms / max(n, 1), n_packed
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, nargs=2, default=[4096, 4096])
+    ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--link-gbs", type=float, nargs="+", default=[64.0, 128.0])
+    ap.add_argument("--frames", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import simpleraytracing_amd as xrt
+    from simpleraytracing_amd.strips import root_share, strip_bounds, weighted_bounds
+    W, H = args.size
+    tris = xrt.load_ply(os.path.join(ROOT, "data", "dragon.ply"))
+    cam = xrt.camera_for_mesh(tris, W, H)
+    out = {}
+    for split in ("weighted", "equal"):
         for n in args.ranks:
-            dense = packed = 0
-            for g in range(1, n):
-                r0, r1 = strip_bounds(H, n, g)
-                lb = torch.empty((r1 - r0) * W, device=dev)
-                ctx.render_rows_device(cam, r0, r1, 0, lb.data_ptr(), 0, 0)
-                _, n_packed = ctx.plan_region_map(W, r1 - r0)
-                dense += 4 * (r1 - r0) * W
-                packed += 4096 * n_packed
-            torch.cuda.synchronize()
-            out[n] = {"dense_bytes": dense, "packed_bytes": packed, "ratio": round(dense / max(packed, 1), 2)}
-    print(json.dumps({"image": [W, H], "strips": out}))
+            if split == "equal" and n == 1:
+                continue
+            share0 = root_share(n)
+            bounds = [weighted_bounds(H, n, g, share0) if split == "weighted" else strip_bounds(H, n, g)
+                      for g in range(n)]
+            ranks = []
+            for g, (r0, r1) in enumerate(bounds):
+                ms, n_packed = strip_time_ms(xrt, torch, tris, cam, r0, r1, W, args.frames, miss_code=g > 0)
+                ranks.append({"rows": r1 - r0, "render_us": round(ms * 1e3, 2),
+                              "packed_bytes": 4096 * n_packed if g else 0, "dense_bytes": 4 * (r1 - r0) * W if g else 0})
+            senders = ranks[1:]
+            unpack_us = 0.0 if n == 1 else 5.0       # one k_unpack_blocks launch (measured ~5 us at 4096^2)
+            pred = {}
+            for gbs in args.link_gbs:
+                transfer = max((s["packed_bytes"] / (gbs * 1e3) for s in senders), default=0.0)
+                step = max(ranks[0]["render_us"] + unpack_us, max((s["render_us"] for s in senders), default=0.0),
+                           transfer)
+                pred[f"{gbs:g}GBs"] = {"step_us": round(step, 1), "transfer_us": round(transfer, 1),
+                                       "mrays_s": round(W * H / step, 0) if step else None}
+            out[f"{split}_{n}"] = {"ranks": ranks, "root_share": share0 if split == "weighted" else 1.0 / n,
+                                   "predicted": pred}
+    print(json.dumps({"image": [W, H], "splits": out}))
 
 
 if __name__ == "__main__":
