@@ -55,14 +55,22 @@ def main():
     W, H = args.size
     tris = xrt.load_ply(os.path.join(ROOT, "data", "dragon.ply"))
     cam = xrt.camera_for_mesh(tris, W, H)
+    import bench
+    from simpleraytracing_amd.strips import balanced_bounds
+    band_cost, band_bytes, _ = bench.band_model(xrt, torch, tris, cam, W, H, 0)
     out = {}
-    for split in ("weighted", "equal"):
+    splits = ["weighted", "equal"] + [f"balanced@{g:g}" for g in args.link_gbs]
+    for split in splits:
         for n in args.ranks:
-            if split == "equal" and n == 1:
+            if split != "weighted" and n == 1:
                 continue
             share0 = root_share(n)
-            bounds = [weighted_bounds(H, n, g, share0) if split == "weighted" else strip_bounds(H, n, g)
-                      for g in range(n)]
+            if split.startswith("balanced@"):
+                link = float(split.split("@")[1]) * 1e3           # GB/s -> bytes/us
+                bounds = balanced_bounds(band_cost, band_bytes, n, link, H)
+            else:
+                bounds = [weighted_bounds(H, n, g, share0) if split == "weighted" else strip_bounds(H, n, g)
+                          for g in range(n)]
             ranks = []
             for g, (r0, r1) in enumerate(bounds):
                 ms, n_packed = strip_time_ms(xrt, torch, tris, cam, r0, r1, W, args.frames, miss_code=g > 0)
@@ -77,8 +85,7 @@ def main():
                            transfer)
                 pred[f"{gbs:g}GBs"] = {"step_us": round(step, 1), "transfer_us": round(transfer, 1),
                                        "mrays_s": round(W * H / step, 0) if step else None}
-            out[f"{split}_{n}"] = {"ranks": ranks, "root_share": share0 if split == "weighted" else 1.0 / n,
-                                   "predicted": pred}
+            out[f"{split}_{n}"] = {"ranks": ranks, "bounds": bounds, "predicted": pred}
     print(json.dumps({"image": [W, H], "splits": out}))
 
 
