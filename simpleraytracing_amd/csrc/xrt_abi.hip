@@ -1069,12 +1069,10 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
-    // The prep stream gets the highest queue priority: its small workgroups
-    // must find CU slots while the previous frame's render fills the chip.
-    int prio_least = 0, prio_greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+    // The prep stream at the default queue priority: frames are prepared ahead
+    // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess &&
-              hipStreamCreateWithPriority(&ctx->prep_stream, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+              hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
