@@ -1249,7 +1249,7 @@ constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 constexpr uint32_t kPrepTris = XRT_PREP_TRIS;     // triangles per k_prep wave (1..64)
 static_assert(kPrepTris >= 1u && kPrepTris <= 64u, "kPrepTris");
 
-__global__ __launch_bounds__(kPrepThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_prep(const float* __restrict__ tris, uint32_t T,
+__global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
                                               TriRec* __restrict__ recs,
                                               float4* __restrict__ culls, BinBuffers bins,
