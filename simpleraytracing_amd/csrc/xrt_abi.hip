@@ -1072,7 +1072,7 @@ int xrt_create(int device, xrt_context** out)
     // The prep stream at the default queue priority: frames are prepared ahead
     // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess;
-ok = ok && hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
