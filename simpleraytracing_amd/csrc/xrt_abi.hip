@@ -37,14 +37,20 @@ constexpr uint64_t kEventStride = 16;
 constexpr double kTicksPerMs = 1e5;
 // Buffer sets in rotation: frame N's preparation reuses the set of frame
 // N - kFrameSets, whose render the host has seen complete by then.
-constexpr int kFrameSets = 4;
+#ifndef XRT_FRAME_SETS
+#define XRT_FRAME_SETS 4
+#endif
+constexpr int kFrameSets = XRT_FRAME_SETS;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
 // Frames prepared ahead of their call when a device-pointer render repeats
 // its geometry (xrt_context::ahead); with kFrameSets sets, two renders can be
 // in flight beside them.
-constexpr size_t kAheadFrames = 2;
+#ifndef XRT_AHEAD_FRAMES
+#define XRT_AHEAD_FRAMES 2
+#endif
+constexpr size_t kAheadFrames = XRT_AHEAD_FRAMES;
 static_assert(kAheadFrames + 2 <= (size_t)kFrameSets, "sets for the renders in flight and the frames ahead");
 
 
