@@ -428,14 +428,166 @@ __device__ float wave_overflow_distance(const TriRec* __restrict__ recs, uint32_
     return distance;
 }
 
+// ---------------------------------------------------------------------------
+// The fix-up over the tile's survivors.  A tile's overflowed rays hit only
+// candidates that passed its tile cull, and there are few of those (a tile
+// with overflowed rays on the 1.12 M-triangle mesh has ~100 survivors of
+// thousands of candidates).  collect_survivors makes one pass over the
+// candidates and keeps the survivors' candidate indices, 64 per slot
+// (survivor s in slot s / 64 of lane s % 64); each overflowed ray then tests
+// at most kSurvSlots records per lane, keeps its hits sorted in registers, and
+// the wave takes them in ascending order, one wave minimum per hit, summing
+// the pairs as main.cxx:703-708 does.  More than 64 * kSurvSlots survivors:
+// the whole-candidate path above.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSurvSlots = 4;
+
+// A cull functor answers "does candidate k pass the tile cull of the render
+// that called finish_ray"; NoCull (the brute-force render, which has none)
+// takes the whole-candidate fix-up, and so does an EntryCull (k_render_binned)
+// of a region rendered from the whole mesh.
+struct NoCull {
+    __device__ bool operator()(uint32_t) const { return true; }
+};
+
+struct EntryCull;
+__device__ __forceinline__ bool cull_enabled(const NoCull&) { return false; }
+template <typename Cull>
+__device__ __forceinline__ bool cull_enabled(const Cull& c)
+{
+    if constexpr (std::is_same<Cull, EntryCull>::value) return c.enabled;
+    else return true;
+}
+
+// Position of the r-th (from 0) set bit of m; r < popcount(m).
+__device__ __forceinline__ uint32_t nth_set_bit(unsigned long long m, uint32_t r)
+{
+    uint32_t pos = 0, w = (uint32_t)m, c = (uint32_t)__popc(w);
+    if (r >= c) { r -= c; w = (uint32_t)(m >> 32); pos = 32u; }
+    c = (uint32_t)__popc(w & 0xFFFFu);
+    if (r >= c) { r -= c; w >>= 16; pos += 16u; }
+    c = (uint32_t)__popc(w & 0xFFu);
+    if (r >= c) { r -= c; w >>= 8; pos += 8u; }
+    c = (uint32_t)__popc(w & 0xFu);
+    if (r >= c) { r -= c; w >>= 4; pos += 4u; }
+    c = (uint32_t)__popc(w & 0x3u);
+    if (r >= c) { r -= c; w >>= 2; pos += 2u; }
+    return pos + (r >= (w & 1u) ? 1u : 0u);
+}
+
+// false (wave-uniform) when the tile has more than 64 * kSurvSlots survivors.
+template <typename Cull>
+__device__ __forceinline__ bool collect_survivors(uint32_t n_cand, Cull cull, uint32_t (&surv)[kSurvSlots],
+                                                  uint32_t& n_surv)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    n_surv = 0;
+    for (uint32_t base = 0; base < n_cand; base += 64u) {
+        const uint32_t k = base + lane;
+        const unsigned long long m = __ballot(k < n_cand && cull(k));
+        const uint32_t c = (uint32_t)__popcll(m);
+        if (n_surv + c > 64u * kSurvSlots) return false;
+        // this batch's survivors take positions [n_surv, n_surv + c); lane keeps p = lane (mod 64)
+        const uint32_t r = (lane - n_surv) & 63u;
+        if (r < c) {
+            const uint32_t slot = (n_surv + r) >> 6, kk = base + nth_set_bit(m, r);
+#pragma unroll
+            for (uint32_t i = 0; i < kSurvSlots; ++i)
+                if (slot == i) surv[i] = kk;
+        }
+        n_surv += c;
+    }
+    return true;
+}
+
+// Minimum over the wave of t >= 0 (ordered like its bits): the maximum of the
+// complemented bits, so DPP's zero fill is the identity.
+__device__ __forceinline__ float wave_min_pos(float t)
+{
+    return __uint_as_float(~wave_reduce_u32<true>(~__float_as_uint(t)));
+}
+
+template <typename Fetch>
+__device__ float wave_survivor_distance(const TriRec* __restrict__ recs, const uint32_t (&surv)[kSurvSlots],
+                                        uint32_t n_surv, Fetch fetch, float dx, float dy, float dz)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    float v[kSurvSlots];
+#pragma unroll
+    for (uint32_t i = 0; i < kSurvSlots; ++i) v[i] = __builtin_inff();
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSurvSlots; ++i) {
+        if (i * 64u >= n_surv) break;                 // wave-uniform
+        float t = 0.0f;
+        if (i * 64u + lane < n_surv && fixup_hit(recs, fetch(surv[i]), dx, dy, dz, t)) {
+            float prev = v[0];                        // sorted insert (a lane holds <= kSurvSlots)
+            v[0] = fminf(prev, t);
+#pragma unroll
+            for (uint32_t r = 1; r < kSurvSlots; ++r) {
+                const float cur = v[r];
+                v[r] = __builtin_amdgcn_fmed3f(prev, cur, t);
+                prev = cur;
+            }
+            ++cnt;
+        }
+    }
+    const uint32_t total = wave_reduce_u32<false>(cnt);
+    if (total & 1u) return 0.0f;                      // odd count: main.cxx:709-713
+    float distance = 0.0f, pending = 0.0f;
+    for (uint32_t pos = 0; pos < total; ++pos) {
+        // the next hit in ascending order: popped from the first lane that holds it
+        // (+inf hits are the largest and equal: whichever lane pops, the value is right)
+        const float mn = wave_min_pos(v[0]);
+        if (lane == (uint32_t)__builtin_ctzll(__ballot(v[0] == mn))) {
+#pragma unroll
+            for (uint32_t r = 0; r + 1 < kSurvSlots; ++r) v[r] = v[r + 1];
+            v[kSurvSlots - 1] = __builtin_inff();
+        }
+        if (pos & 1u) distance += mn - pending;
+        else pending = mn;
+    }
+    return distance;
+}
+
+// The exact distances of the wave's overflowed rays (lanes of om; whole wave):
+// each lane of om gets its ray's.
+template <typename Fetch, typename Cull>
+__device__ __forceinline__ float overflow_fixup(unsigned long long om, const TriRec* __restrict__ recs,
+                                                uint32_t n_cand, Fetch fetch, Cull cull, float dx, float dy,
+                                                float dz)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t surv[kSurvSlots] = {}, n_surv = 0;
+    const bool few = cull_enabled(cull) && collect_survivors(n_cand, cull, surv, n_surv);
+    float mine = 0.0f;
+    // one loop per path: surv is not live in the whole-candidate one
+    auto each = [&](auto dist) {
+        do {
+            const uint32_t L = (uint32_t)__builtin_ctzll(om);
+            om &= om - 1ull;
+            const float d = dist(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), (int)L)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), (int)L)),
+                                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), (int)L)));
+            if (lane == L) mine = d;
+        } while (om);
+    };
+    if (few)
+        each([&](float rx, float ry, float rz) { return wave_survivor_distance(recs, surv, n_surv, fetch, rx, ry, rz); });
+    else
+        each([&](float rx, float ry, float rz) { return wave_overflow_distance(recs, n_cand, fetch, rx, ry, rz); });
+    return mine;
+}
+
 // Must be reached by the whole wave (the overflow fix-up is wave-wide).
 // (dx, dy, dz) is this lane's ray; n_cand / fetch the candidates the render
-// tested (fetch(k) = triangle of the k-th).
-template <typename Fetch>
+// tested (fetch(k) = triangle of the k-th), cull(k) their tile cull.
+template <typename Fetch, typename Cull = NoCull>
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
                                            size_t o, const HitList& hl,
                                            WaveStats& ws, const TriRec* __restrict__ recs, float dx,
-                                           float dy, float dz, uint32_t n_cand, Fetch fetch)
+                                           float dy, float dz, uint32_t n_cand, Fetch fetch,
+                                           Cull cull = Cull())
 {
     const uint32_t lane = threadIdx.x & 63u;
     bool overflow = hl.n > p.hit_capacity;
@@ -448,15 +600,10 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
         if (!odd) distance = hl.path_length();
         lval = distance;
     }
-    unsigned long long om = __ballot(active && overflow);
-    while (om) {                                      // wave-uniform
-        const uint32_t L = (uint32_t)__builtin_ctzll(om);
-        om &= om - 1ull;
-        const float rx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), (int)L));
-        const float ry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), (int)L));
-        const float rz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), (int)L));
-        const float d = wave_overflow_distance(recs, n_cand, fetch, rx, ry, rz);
-        if (lane == L) {                              // n > capacity >= 1: the ray hit
+    const unsigned long long om = __ballot(active && overflow);
+    if (__builtin_expect(om != 0ull, 0)) {            // wave-uniform, rare
+        const float d = overflow_fixup(om, recs, n_cand, fetch, cull, dx, dy, dz);
+        if ((om >> lane) & 1ull) {                    // n > capacity >= 1: the ray hit
             distance = d;
             lval = d;
         }
@@ -517,15 +664,64 @@ __device__ float wave_signed_overflow_distance(const TriRec* __restrict__ recs, 
     return distance;
 }
 
+// The same over the tile's survivors (collect_survivors): each lane tests at
+// most kSurvSlots records and keeps (triangle id, term); the wave takes the
+// terms by ascending id, one wave minimum per hit.
+template <typename Fetch>
+__device__ float wave_signed_survivor_distance(const TriRec* __restrict__ recs,
+                                               const uint32_t (&surv)[kSurvSlots], uint32_t n_surv, Fetch fetch,
+                                               float dx, float dy, float dz, float sx, float sy, float sz)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t id[kSurvSlots];
+    float term[kSurvSlots];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSurvSlots; ++i) {
+        id[i] = 0xFFFFFFFFu;
+        term[i] = 0.0f;
+        if (i * 64u >= n_surv) continue;              // wave-uniform
+        if (i * 64u + lane < n_surv) {
+            const uint32_t j = fetch(surv[i]);
+            float t = 0.0f;
+            if (fixup_hit(recs, j, dx, dy, dz, t)) {
+                const TriRec& r = recs[j];
+                id[i] = j;
+                term[i] = (float)hit_sign(sx, sy, sz, r.pad0, r.pad1, r.pad2) * t;
+                ++cnt;
+            }
+        }
+    }
+    const uint32_t total = wave_reduce_u32<false>(cnt);
+    float distance = 0.0f;
+    for (uint32_t q = 0; q < total; ++q) {
+        uint32_t mine = id[0];
+#pragma unroll
+        for (uint32_t i = 1; i < kSurvSlots; ++i) mine = id[i] < mine ? id[i] : mine;
+        const uint32_t best = ~wave_reduce_u32<true>(~mine);          // ids are distinct
+        const uint32_t owner = (uint32_t)__builtin_ctzll(__ballot(mine == best));
+        float v = 0.0f;
+#pragma unroll
+        for (uint32_t i = 0; i < kSurvSlots; ++i) {
+            if (id[i] == best) {
+                v = term[i];
+                id[i] = 0xFFFFFFFFu;
+            }
+        }
+        distance += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)owner));
+    }
+    return distance;
+}
+
 // finish_ray of the signed model: the fork's L-buffer value (-1 flags) into
 // out.lbuffer (image and u8 come from the hole fill, k_hole_fill).  The odd
 // counter counts flagged rays.
-template <typename Fetch>
+template <typename Fetch, typename Cull = NoCull>
 __device__ __forceinline__ void finish_ray_signed(const RenderParams& p, const Outputs& out, bool active,
                                                   uint32_t row, uint32_t col, const SignedHits& hl,
                                                   WaveStats& ws, const TriRec* __restrict__ recs, float dx,
                                                   float dy, float dz, float sx, float sy, float sz,
-                                                  uint32_t n_cand, Fetch fetch)
+                                                  uint32_t n_cand, Fetch fetch, Cull cull = Cull())
 {
     const uint32_t lane = threadIdx.x & 63u;
     const bool overflow = hl.n > p.hit_capacity;
@@ -533,13 +729,26 @@ __device__ __forceinline__ void finish_ray_signed(const RenderParams& p, const O
     wave_stats(ws, active, hl.n, flagged, overflow);
     float distance = hl.distance();
     unsigned long long om = __ballot(active && overflow && !flagged);
-    while (om) {                                      // wave-uniform
-        const uint32_t L = (uint32_t)__builtin_ctzll(om);
-        om &= om - 1ull;
-        auto at = [L](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)L)); };
-        const float d = wave_signed_overflow_distance(recs, n_cand, fetch, at(dx), at(dy), at(dz), at(sx),
-                                                      at(sy), at(sz));
-        if (lane == L) distance = d;
+    if (om) {                                         // wave-uniform, rare
+        uint32_t surv[kSurvSlots] = {}, n_surv = 0;
+        const bool few = cull_enabled(cull) && collect_survivors(n_cand, cull, surv, n_surv);
+        auto each = [&](auto dist) {                  // one loop per path, as in finish_ray
+            do {
+                const uint32_t L = (uint32_t)__builtin_ctzll(om);
+                om &= om - 1ull;
+                auto at = [L](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)L)); };
+                const float d = dist(at(dx), at(dy), at(dz), at(sx), at(sy), at(sz));
+                if (lane == L) distance = d;
+            } while (om);
+        };
+        if (few)
+            each([&](float rx, float ry, float rz, float qx, float qy, float qz) {
+                return wave_signed_survivor_distance(recs, surv, n_surv, fetch, rx, ry, rz, qx, qy, qz);
+            });
+        else
+            each([&](float rx, float ry, float rz, float qx, float qy, float qz) {
+                return wave_signed_overflow_distance(recs, n_cand, fetch, rx, ry, rz, qx, qy, qz);
+            });
     }
     if (!active || !out.lbuffer) return;
     float lval = 80.0f;                               // no term: 80 * exp(-0.0)
@@ -778,8 +987,13 @@ __device__ __forceinline__ void render_region_tiles(const RenderParams& p, const
         }
         if (tile_live) {
             ws.tile_tests += tests;
+            auto cull = [=](uint32_t k) {
+                const uint32_t j = fetch(k);
+                return edges_pass_tile(culls[(size_t)T + j], culls[2 * (size_t)T + j], culls[3 * (size_t)T + j],
+                                       xc, yc);
+            };
             finish_ray(p, out, active, (size_t)(row - p.row_begin) * p.width + col, hl, ws, recs, dx, dy, dz,
-                       n_cand, fetch);
+                       n_cand, fetch, cull);
         }
     }
 }
@@ -1589,6 +1803,26 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     if (__ballot(h)) hl.push_if(h, t, __float_as_uint(st.q[0][k].w), hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
 }
 
+// The staged loop's tile test of candidate k, from its list entry (the
+// overflow fix-up's survivors; a region rendered from the whole mesh takes
+// the whole-candidate fix-up).  The tile rectangle is recomputed from its
+// corner here rather than kept live from the loop.
+struct EntryCull {
+    const RegionEntry* __restrict__ local;
+    const RegionEntry* __restrict__ glob;
+    uint32_t n_local, tx0, ty0;
+    bool enabled;
+    __device__ bool operator()(uint32_t k) const
+    {
+        uint32_t x = tx0, y = ty0;
+        asm volatile("" : "+s"(x), "+s"(y));
+        const float fx0 = (float)x, fy0 = (float)y;
+        const RegionEntry& e = k < n_local ? local[k] : glob[k - n_local];
+        return edges_pass_tile(e.e0, e.e1, e.e2, fx0 + 3.5f, fy0 + 3.5f) &
+               box_overlaps(e.bb, fx0, fx0 + 7.0f, fy0, fy0 + 7.0f);
+    }
+};
+
 // One wave's 8x8 tile `tile` of the region in launch slot `slot`: the body of
 // k_render_binned.  Every wave of the workgroup calls it for the same slot
 // (they stage the region's candidates together); the statistics accumulate in
@@ -1678,10 +1912,11 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
         auto fetch = [=](uint32_t k) {
             return whole ? k : __float_as_uint((k < nl ? local[k] : glob[k - nl]).e0.w);
         };
+        const EntryCull cull{local, glob, nl, tx0, ty0, !whole};
         if constexpr (kSigned)
-            finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch);
+            finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch, cull);
         else
-            finish_ray(p, out, active, o, hl, ws, recs, dx, dy, dz, n_cand, fetch);
+            finish_ray(p, out, active, o, hl, ws, recs, dx, dy, dz, n_cand, fetch, cull);
     } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
         ws.rays += (uint32_t)__popcll(__ballot(active));
         if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;

@@ -65,3 +65,22 @@ def striped_sheets(seed=3, n=40):
         q = np.array([[x, y0, z0, x, y0 + w, z0, x, y0 + w, z1], [x, y0, z0, x, y0 + w, z1, x, y0, z1]], np.float32)
         out.append(q if rng.random() < 0.5 else q[:, [0, 1, 2, 6, 7, 8, 3, 4, 5]])   # both windings
     return np.ascontiguousarray(np.concatenate(out))
+
+
+def plane_stack(n, spacing=0.01, alternate=False):
+    """n parallel unit squares (2 triangles each) facing the detector: every ray
+    through the square hits each plane (twice on the shared diagonal).  With
+    alternate, every second square is wound the other way (its normal flips),
+    so the signed model's signs cancel over each pair of planes."""
+    x = (np.arange(n, dtype=np.float32) * np.float32(spacing)).astype(np.float32)
+    a = np.stack([x, np.zeros(n, np.float32), np.zeros(n, np.float32)], 1)
+    b = np.stack([x, np.ones(n, np.float32), np.zeros(n, np.float32)], 1)
+    c = np.stack([x, np.ones(n, np.float32), np.ones(n, np.float32)], 1)
+    d = np.stack([x, np.zeros(n, np.float32), np.ones(n, np.float32)], 1)
+    t1 = np.concatenate([a, b, c], 1)
+    t2 = np.concatenate([a, c, d], 1)
+    if alternate:
+        odd = np.arange(n) % 2 == 1
+        t1[odd] = np.concatenate([a, c, b], 1)[odd]
+        t2[odd] = np.concatenate([a, d, c], 1)[odd]
+    return np.ascontiguousarray(np.stack([t1, t2], 1).reshape(2 * n, 9), dtype=np.float32)

@@ -15,7 +15,7 @@ from simpleraytracing_amd.scenes import orbit_camera, tiled_mesh
 from oracle import oracle
 from conftest import DRAGON, GOLDEN, ROOT, bits
 from kat import kat_vectors
-from scene_kit import corner_soup, synthetic_soup
+from scene_kit import corner_soup, plane_stack, synthetic_soup
 
 pytestmark = pytest.mark.gpu
 KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED]
@@ -230,25 +230,15 @@ def test_overflow_path_exact(ctx, dragon, kernel):
 MAX_HITS = 12  # the register hit list (XRT_MAX_HITS); rays past it take the exact fix-up
 
 
-def plane_stack(n, spacing=0.01):
-    """n parallel unit squares (2 triangles each) facing the detector: every ray
-    through the square hits each plane (twice on the shared diagonal)."""
-    x = (np.arange(n, dtype=np.float32) * np.float32(spacing)).astype(np.float32)
-    a = np.stack([x, np.zeros(n, np.float32), np.zeros(n, np.float32)], 1)
-    b = np.stack([x, np.ones(n, np.float32), np.zeros(n, np.float32)], 1)
-    c = np.stack([x, np.ones(n, np.float32), np.ones(n, np.float32)], 1)
-    d = np.stack([x, np.zeros(n, np.float32), np.ones(n, np.float32)], 1)
-    t1 = np.concatenate([a, b, c], 1)
-    t2 = np.concatenate([a, c, d], 1)
-    return np.ascontiguousarray(np.stack([t1, t2], 1).reshape(2 * n, 9), dtype=np.float32)
-
-
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("planes,size", [(40, 48), (300, 16), (2100, 8)])
+@pytest.mark.parametrize("planes,size", [(40, 48), (128, 24), (129, 24), (300, 16), (2100, 8)])
 def test_deep_stack_overflow(ctx, kernel, planes, size):
-    """Rays with 40..4200 hits: the wave-wide overflow fix-up (register lists
-    bitonic-sorted across the wave up to 8 hits a lane, streamed beyond) must
-    equal the oracle's std::sort + pair sum."""
+    """Rays with 40..4200 hits: the wave-wide overflow fix-up must equal the
+    oracle's std::sort + pair sum -- over the tile's survivors (up to 256: 128
+    planes fill all four slots on the diagonal tiles, where both triangles of a
+    square survive), and over all candidates past that (129 planes on the
+    diagonal, 300, 2100; register lists bitonic-sorted across the wave up to 8
+    hits a lane, streamed beyond)."""
     if kernel == xrt.XRT_KERNEL_BRUTE and planes > 100:
         pytest.skip("brute force is covered by the 40-plane case")
     soup = plane_stack(planes)

@@ -14,7 +14,7 @@ import simpleraytracing_amd as xrt
 from simpleraytracing_amd import _abi
 from oracle import oracle
 from conftest import DRAGON, ROOT, bits
-from scene_kit import box, corner_soup, second_mesh_for, striped_sheets, synthetic_soup
+from scene_kit import box, corner_soup, plane_stack, second_mesh_for, striped_sheets, synthetic_soup
 
 pytestmark = pytest.mark.gpu
 KERNELS = [xrt.XRT_KERNEL_BRUTE, xrt.XRT_KERNEL_TILED, xrt.XRT_KERNEL_BINNED]
@@ -150,6 +150,22 @@ def test_signed_overflow_path_exact(signed, dragon, kernel, cap):
     rlb, rnh, _ = oracle.render_signed_rows(meshes, cam13(cam), W, H)
     assert st.overflow_rays > 0
     assert np.array_equal(bits(lb), bits(rlb))
+
+
+@pytest.mark.parametrize("kernel", SIGNED_KERNELS)
+@pytest.mark.parametrize("planes,size", [(40, 24), (128, 16), (150, 16)])
+def test_signed_deep_stack_overflow(signed, kernel, planes, size):
+    """Rays through 40..150 alternately wound planes (signs cancel, so the rays
+    are not flagged and their sums need the overflow path): the fix-up over the
+    tile's survivors (<= 256) and over all candidates past that."""
+    meshes = [plane_stack(planes, alternate=True)]
+    cam = xrt.camera_for_scene(meshes, size, size)
+    signed.set_kernel(kernel)
+    signed.upload_mesh(meshes[0])
+    _, lb, _, st = signed.render_signed(cam)
+    rlb, rnh, flagged = oracle.render_signed_rows(meshes, cam13(cam), size, size)
+    assert int(rnh.max()) > 12 and st.overflow_rays > 0 and flagged < size * size
+    assert np.array_equal(bits(lb), bits(rlb)), np.nonzero(bits(lb) != bits(rlb))[0][:8]
 
 
 def test_signed_strips_assemble(signed, dragon):
