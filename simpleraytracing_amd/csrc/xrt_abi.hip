@@ -41,6 +41,12 @@ constexpr double kTicksPerMs = 1e5;
 #define XRT_FRAME_SETS 4
 #endif
 constexpr int kFrameSets = XRT_FRAME_SETS;
+// LDS a k_prep workgroup holds (its own 10 KB + dynamic padding): at most
+// three share a CU with the render's eight 8-KB workgroups (160 KB), so the
+// preparation beside a render cannot take more of a CU's wave slots than
+// that (1.12 M-triangle frame 1,224 -> 1,143 us, 4096^2 -1.5 %, 2048^2 equal;
+// one or two per CU starve the preparation, DESIGN.md "Pipelining").
+constexpr size_t kPrepLds = 32768;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
@@ -158,6 +164,7 @@ struct xrt_context {
     int next_set = 0;
     FrameSet* last_set = nullptr;      // set of the last enqueued frame
     hipStream_t prep_stream = nullptr;
+    size_t prep_lds = 0;               // dynamic LDS of a k_prep launch (kPrepLds in all)
 
     // Launch layouts of the region grid (SlotLayout): the fixed-capacity one
     // the first frame of a geometry bins into (centre-first order), and the
@@ -477,7 +484,7 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                                                (threads + kPrepThreads - 1) / kPrepThreads);
     const auto t_launch = HostClock::now();
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(kPrepThreads),
-                          0, stream, nullptr, done, 0u,
+                          ctx->prep_lds, stream, nullptr, done, 0u,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
@@ -1079,6 +1086,9 @@ int xrt_create(int device, xrt_context** out)
     // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess;
     ok = ok && hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
+    hipFuncAttributes prep_attr = {};
+    ok = ok && hipFuncGetAttributes(&prep_attr, reinterpret_cast<const void*>(k_prep)) == hipSuccess;
+    ctx->prep_lds = prep_attr.sharedSizeBytes < kPrepLds ? kPrepLds - prep_attr.sharedSizeBytes : 0;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
