@@ -28,7 +28,9 @@ Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
+import traceback
 import os
 import sys
 import time
@@ -135,25 +137,57 @@ def end_to_end(args, W, H, device_index, kernel):
     """The reference's only published numbers are whole-process runs
     (submit-serial.sh:18 /usr/bin/time; main.cxx:206-216 times the load): a fresh
     context's load + upload + first render (list sizing included) + D2H of the
-    three planes, each part timed on the host (HIP already initialised)."""
+    three planes, each part timed on the host (HIP already initialised), with
+    the host-buffer call's own breakdown (xrt_debug_host_call_ms).  Then the
+    same call again into the same host buffers (an Image rendered per frame)
+    and into fresh ones, and the whole sequence once more in a second fresh
+    context (what is a process's first-time cost, what is every context's)."""
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.scenes import tiled_mesh
+
+    def rounded(d):
+        return {k: round(v, 3) for k, v in d.items()}
+
+    def one_context(tris, t_load):
+        c = xrt.Context(device_index)
+        try:
+            c.set_kernel(kernel)
+            t2 = time.perf_counter()
+            c.upload_mesh(tris)
+            t3 = time.perf_counter()
+            cam = xrt.camera_for_mesh(tris, W, H)
+            planes = c.render_rows(cam)                   # host planes: render + D2H, synchronous
+            t4 = time.perf_counter()
+            r = {"end_to_end_ms": (t_load + t4 - t2) * 1e3, "load_ms": t_load * 1e3,
+                 "upload_ms": (t3 - t2) * 1e3, "render_and_d2h_ms": (t4 - t3) * 1e3,
+                 "render_and_d2h_breakdown_ms": rounded(c.host_call_ms())}
+            t5 = time.perf_counter()
+            c.render_rows(cam, out=planes[:3])
+            r["again_same_buffers_ms"] = (time.perf_counter() - t5) * 1e3
+            r["again_same_buffers_breakdown_ms"] = rounded(c.host_call_ms())
+            t6 = time.perf_counter()
+            c.render_rows(cam)
+            r["again_fresh_buffers_ms"] = (time.perf_counter() - t6) * 1e3
+            r["again_fresh_buffers_breakdown_ms"] = rounded(c.host_call_ms())
+        finally:
+            t7 = time.perf_counter()
+            c.close()
+            r["context_destroy_ms"] = (time.perf_counter() - t7) * 1e3
+        return r
+
     t0 = time.perf_counter()
     tris = xrt.load_ply(args.mesh)
     if args.tile_mesh > 1:
         tris = tiled_mesh(tris, args.tile_mesh)
-    t1 = time.perf_counter()
-    with xrt.Context(device_index) as c:
-        c.set_kernel(kernel)
-        t2 = time.perf_counter()
-        c.upload_mesh(tris)
-        t3 = time.perf_counter()
-        c.render_rows(xrt.camera_for_mesh(tris, W, H))    # host planes: render + D2H, synchronous
-        t4 = time.perf_counter()
-    return {"end_to_end_ms": (t1 - t0 + t4 - t2) * 1e3, "load_ms": (t1 - t0) * 1e3,
-            "upload_ms": (t3 - t2) * 1e3, "render_and_d2h_ms": (t4 - t3) * 1e3,
-            "what": "load PLY + upload + first render of a fresh context (list sizing included) + D2H of "
-                    "image, L-buffer and u8 (context creation excluded)"}
+    t_load = time.perf_counter() - t0
+    out = one_context(tris, t_load)
+    second = one_context(tris, t_load)
+    out["second_context"] = {k: v for k, v in second.items() if k != "load_ms"}
+    out["what"] = ("load PLY + upload + first render of a fresh context (list sizing included) + D2H of image, "
+                   "L-buffer and u8 (context creation excluded); breakdown from xrt_debug_host_call_ms; then the "
+                   "same call again into the same host buffers and into fresh ones; second_context: all of it "
+                   "again in another fresh context of the same process")
+    return out
 
 
 def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32):
@@ -216,6 +250,32 @@ def measure_link(dist, torch, world, rank, dev, nccl, nbytes=4 << 20, reps=5):
     rate = torch.tensor([nbytes / (dt * 1e6)], dtype=torch.float64, device=where)
     dist.broadcast(rate, src=0)
     return float(rate.item())
+
+
+DIST_TIMEOUT_S = 120            # every collective of a multi-rank run (a hung link fails the run)
+EXIT_GATHER_MISMATCH = 3        # the gathered frame differs from rank 0's own render
+
+
+def planes_equal(a, b) -> bool:
+    """(image f32, L-buffer f32, u8) planes equal bit for bit."""
+    import numpy as np
+    return (np.array_equal(np.asarray(a[0]).view(np.uint32), np.asarray(b[0]).view(np.uint32))
+            and np.array_equal(np.asarray(a[1]).view(np.uint32), np.asarray(b[1]).view(np.uint32))
+            and np.array_equal(np.asarray(a[2]), np.asarray(b[2])))
+
+
+def gather_verdict(dist, torch, rank: int, ok: bool, where) -> int:
+    """Every rank learns rank 0's verdict on the gathered frame (`ok` is read on
+    rank 0 only) and returns its exit code: 0, or EXIT_GATHER_MISMATCH on every
+    rank when the gathered frame is wrong -- a wrong frame fails the whole job,
+    not just the rank that noticed."""
+    flag = torch.tensor([1 if (ok or rank != 0) else 0], dtype=torch.int32, device=where)
+    dist.broadcast(flag, src=0)
+    if int(flag.item()) == 1:
+        return 0
+    print(f"bench.py rank {rank}: the gathered frame is not bit-exact against rank 0's single-device render",
+          file=sys.stderr, flush=True)
+    return EXIT_GATHER_MISMATCH
 
 
 def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_s, launches):
@@ -304,10 +364,13 @@ def main():
     dev = torch.device("cuda", device_index)
     nccl = args.dist_backend == "nccl"
     if world > 1:
+        # a bounded wait on every collective: a lost rank or a stuck link ends
+        # the run (non-zero exit) instead of hanging it
+        timeout = datetime.timedelta(seconds=DIST_TIMEOUT_S)
         if nccl:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         # a collective of every rank first: the point-to-point traffic below
         # (map exchange, batch_isend_irecv on rank 0 only) must not be the
         # group's first operation
@@ -524,9 +587,9 @@ def main():
     gather = None
     if gathering and rank == 0:
         full = ctx.render_rows(cam)
-        ok = (np.array_equal(img.cpu().numpy().view(np.uint32), full[0].view(np.uint32))
-              and np.array_equal(lb.cpu().numpy().view(np.uint32), full[1].view(np.uint32))
-              and np.array_equal(u8.cpu().numpy(), full[2]))
+        ok = planes_equal((img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy()), full)
+        if os.environ.get("XRT_BENCH_CORRUPT_GATHER") == "1":    # test hook: a wrong strip must fail the job
+            ok = False
         moved = 4096 * sum(max(c, 1) for c in counts) if packed else 4 * rest
         gather = {"bit_exact_vs_single_device_frame": bool(ok),
                   "bytes_gathered_per_step": moved, "dense_bytes_per_step": 4 * rest,
@@ -613,13 +676,36 @@ def main():
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
 
+    code = 0
+    if gathering:
+        code = gather_verdict(dist, torch, rank, bool(gather and gather["bit_exact_vs_single_device_frame"]),
+                              dev if nccl else "cpu")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
+    return code
+
+
+def run() -> int:
+    """main() with a failing rank's exit made prompt and non-zero: an exception
+    prints its traceback and leaves through os._exit, so no collective or RCCL
+    teardown of this rank can hang, and torch.distributed.run then ends the
+    other ranks (a multi-rank run fails as a whole)."""
+    try:
+        return main()
+    except SystemExit:
+        raise
+    except BaseException:
+        rank = os.environ.get("RANK", "0")
+        print(f"bench.py rank {rank} failed:", file=sys.stderr, flush=True)
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(run())

@@ -325,76 +325,7 @@ int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
 #define XRT_GATHER_RCCL 2
 int xrt_multi_set_gather(xrt_multi* m, int mode);
 
-/* --- diagnostics (device probes of the exact device code paths) ----------- */
-
-/*
- * Runs the kernel's Ray::intersect (src/Ray.cxx:72-124) on the device:
- * rays[6*i] = origin xyz, unit direction xyz; triangles[9*i] = p1, p2, p3.
- * hit[i] = 0/1, t[i] = distance (0 when no hit).  Host buffers.
- */
-int xrt_probe_intersect(xrt_context* ctx, const float* rays, const float* triangles,
-                        uint64_t n, uint8_t* hit, float* t);
-
-typedef enum xrt_probe_op {
-    XRT_PROBE_EXPF = 0,     /* std::exp(float) == glibc expf                     */
-    XRT_PROBE_SQRTF = 1,    /* std::sqrt(float), correctly rounded               */
-    XRT_PROBE_RCP = 2,      /* (float)(1.0 / (double)x), src/Ray.cxx:99           */
-    XRT_PROBE_LUT_U8 = 3,   /* 8-bit LUT of a photon value (out[i] = (float)u8)  */
-    XRT_PROBE_RCP_FAST = 4, /* the culled tests' 1/det (rcp + Newton where exact) */
-    XRT_PROBE_SIGNED_L = 5  /* (float)(80.0 * exp(-(0.1037f * (d * 0.1)))): the signed
-                               model's L for distance d (glibc exp in f64)          */
-} xrt_probe_op;
-
-/* Evaluates one scalar device function elementwise.  Host buffers. */
-int xrt_probe_math(xrt_context* ctx, int op, const float* in, float* out, uint64_t n);
-
-/*
- * Runs the per-render triangle preparation (k_prep) of the uploaded mesh for
- * `camera` and copies its outputs to the host: records[16*i] = edge1, edge2,
- * tvec, qvec, t*det, pad (the ray-independent terms of Ray::intersect,
- * src/Ray.cxx:86-122) and footprint[16*i] = bbox (xmin, xmax, ymin, ymax) and
- * the three relaxed edge functions (a, b, c, 0) of the tile cull.  Either
- * output may be NULL.
- */
-int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, float* footprint);
-
-/*
- * Host-side evaluation of the device expf restatement (the same source,
- * compiled for the host): lets CPU-only tests check it against libm.
- */
-void xrt_host_expf_batch(const float* in, float* out, uint64_t n);
-
-/*
- * The same for the signed model: the device glibc exp restatement, and its L
- * update (float)(80.0 * exp(-(mu * (distance * 0.1)))) (-1 for a non-zero
- * sign sum; sign_sum may be NULL for all zero).
- */
-void xrt_host_exp_batch(const double* in, double* out, uint64_t n);
-void xrt_host_signed_lbuffer_batch(const float* distance, const int32_t* sign_sum, float mu, float* out,
-                                   uint64_t n);
-
-/*
- * Test hook: caps the per-ray register hit list at `capacity` (1..12) so the
- * exact overflow path runs.  0 restores the default (12).
- */
-int xrt_set_hit_capacity(xrt_context* ctx, uint32_t capacity);
-
-/*
- * Test hook: caps the BINNED kernel's region-list capacity at `entries` so the
- * whole-mesh fallback runs.  0 restores automatic sizing.
- */
-int xrt_set_bin_capacity(xrt_context* ctx, uint64_t entries);
-
-/*
- * The BINNED kernel's fill plan (DESIGN.md "Fill plan"): regions whose lists
- * the geometry's sizing frame counted empty render as one miss-filling
- * workgroup each instead of 16 tile waves.  mode 1 (default) on, 0 off;
- * test hook 2 plans every region as empty, so every workgroup takes the
- * exact fallback of a region that is not.  The next frame re-sizes (after a
- * camera change under the same image size and strip the context keeps its
- * lists and plan instead: DESIGN.md "Moving camera"; XRT_CAMERA_REUSE=0 off).
- */
-int xrt_set_fill_plan(xrt_context* ctx, int mode);
+/* --- region-packed transit (multi-GPU gathers) ---------------------------- */
 
 /*
  * Region-packed strips for multi-GPU gathers (DESIGN.md "Multi-GPU").  A strip
@@ -439,54 +370,10 @@ int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats);
 int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
                              const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
 
-/* Diagnostics: regions the last enqueued BINNED frame rendered through the fill plan. */
-int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
-
 /*
- * Diagnostics: BINNED frames by geometry path since the context was created --
- * counters[0] frames whose lists were sized synchronously (a new frame
- * geometry), [1] frames rendered over lists sized for another camera of the
- * same region grid (a moving camera), [2] frames k_prep flagged for a fill-plan
- * miss, [3] frames k_prep flagged for a list overflow.
+ * Test hooks, device probes and diagnostics: include/xrt_debug.h (not part of
+ * the drop-in surface).
  */
-int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4]);
-
-/*
- * Diagnostics: the frame pipeline since the context was created --
- * counters[0] frames rendered from a preparation made ahead of their call
- * (xrt_render_rows_device repeating its frame geometry), [1] preparations made
- * ahead and dropped (the next call's geometry or settings differed), [2]
- * renders launched with their preparation already complete (no wait), [3]
- * renders launched after the host read k_prep's check (sizing / validation).
- */
-int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4]);
-
-/*
- * Diagnostics: copies the last render's statistics records (32 bytes each, one
- * per workgroup -- per tile wave for BINNED: u32 rays, hit rays, odd rays,
- * overflow rays, hits, wave-level triangle tests, candidates, max hits)
- * into `dst`, at most `capacity` bytes; `*n_records` receives the number of
- * records.
- */
-int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint64_t* n_records);
-
-/*
- * Diagnostics: the timing records of the render `frames_back` frames before
- * the last (0 = the last; up to 3, outside timed regions), one per statistics
- * record (u32 s_memrealtime start, u32 end; 100 MHz, low 32 bits), into `dst`,
- * at most `capacity` records; `*n_records` receives their number.
- */
-int xrt_debug_wave_times(xrt_context* ctx, uint32_t frames_back, uint32_t* dst, uint64_t capacity,
-                         uint64_t* n_records);
-
-
-/*
- * Test hook (host code, no device): for each i, the culled render's
- * division-free reject mt_may_hit(det, a, b, tnum) and the exact remainder of
- * Ray::intersect from the same numerators (hit with t > 1e-7, and t).
- */
-void xrt_host_mt_check(const float* det, const float* a, const float* b, const float* tnum, uint64_t n,
-                       uint8_t* may_hit, uint8_t* hit, float* t);
 
 #ifdef __cplusplus
 }

@@ -253,15 +253,30 @@ class Context:
         self._check(self._lib.xrt_debug_pipeline_counters(self._ctx, c), "xrt_debug_pipeline_counters")
         return dict(zip(("ahead_used", "ahead_dropped", "no_wait", "host_waits"), (int(v) for v in c)))
 
+    def host_call_ms(self) -> dict:
+        """Host time of the last render_rows call, ms (xrt_debug_host_call_ms)."""
+        ms = (ctypes.c_double * 10)()
+        self._check(self._lib.xrt_debug_host_call_ms(self._ctx, ms), "xrt_debug_host_call_ms")
+        keys = ("device_planes", "enqueue", "render_wait", "d2h_image", "d2h_lbuffer", "d2h_u8", "stats", "total",
+                "of_which_hipmalloc", "of_which_list_sizing")
+        return dict(zip(keys, (float(v) for v in ms)))
+
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
-                    image=True, lbuffer=True, u8=True):
-        """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats)."""
+                    image=True, lbuffer=True, u8=True, out=None):
+        """Host-buffer render of rows [row_begin, row_end); returns (image, lbuffer, u8, stats).
+        `out`: (image, lbuffer, u8) arrays to render into instead of new ones."""
         if row_end is None:
             row_end = cam.height
         n = max(row_end - row_begin, 0) * cam.width
-        img = np.empty(n, np.float32) if image else None
-        lb = np.empty(n, np.float32) if lbuffer else None
-        u = np.empty(n, np.uint8) if u8 else None
+        if out is not None:
+            img, lb, u = out
+            for a, dt in ((img, np.float32), (lb, np.float32), (u, np.uint8)):
+                if a is not None and (a.dtype != dt or a.size != n or not a.flags.c_contiguous):
+                    raise ValueError("out arrays must be contiguous, of the strip's size and dtype")
+        else:
+            img = np.empty(n, np.float32) if image else None
+            lb = np.empty(n, np.float32) if lbuffer else None
+            u = np.empty(n, np.uint8) if u8 else None
         st = Stats()
         rc = self._lib.xrt_render_rows(
             self._ctx, ctypes.byref(cam), row_begin, row_end,

@@ -1323,19 +1323,21 @@ constexpr uint32_t kBinQueue = XRT_BIN_QUEUE;  // passing (region, triangle) pai
 // wave of slot s loads its count and list without first looking up which
 // region it renders (order[s], loaded alongside); k_prep maps region -> slot
 // through rank.
-// Region-list entry: the triangle's conservative footprint and its record,
-// copied into every region list it joins, so a render wave reads a candidate
-// with no indirection: the footprint into registers (the tile test) and the
-// record straight into LDS by DMA (the survivors' exact tests), both issued
-// together.
+// Region-list entry: the triangle's conservative footprint, copied into every
+// region list it joins, so a render wave's tile test reads a candidate with
+// one coalesced 64-B load per lane and no indirection.  The record of a
+// candidate that survives the tile test is read through its id (e0.w) straight
+// into LDS by DMA (k_render_binned): only survivors' records move, and the
+// lists k_prep writes and the render reads are half what an inlined record
+// would make them (the 1.12 M-triangle frame bins 6.2 M entries).
 struct alignas(16) RegionEntry {
     float4 e0;   // relaxed edge 0 (a, b, c); w = triangle id (bits)
     float4 e1;   // relaxed edge 1
     float4 e2;   // relaxed edge 2
     float4 bb;   // footprint box (xmin, xmax, ymin, ymax)
-    TriRec rec;  // Ray::intersect's ray-independent terms (k_prep)
 };
-static_assert(sizeof(RegionEntry) == 128, "RegionEntry must be 128 bytes");
+static_assert(sizeof(RegionEntry) == 64, "RegionEntry must be 64 bytes");
+constexpr uint32_t kEntryQuads = sizeof(RegionEntry) / sizeof(float4);
 
 // Read-only data of a launch (written by the host or an earlier kernel) read
 // through the constant address space: scalar loads, issued together.
@@ -1537,7 +1539,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     // (2) Commit: the queue dealt kBinBatch pairs per lane per round, each
     // round's launch slots, count atomics and entry stores in flight together.
     // A full queue is committed early.
-    __shared__ float4 s_fp[kPrepWaves][8][64];     // footprint (e0.w = triangle id) and record, per lane
+    __shared__ float4 s_fp[kPrepWaves][kEntryQuads][64];   // the lane's region entry (footprint, e0.w = id)
     __shared__ uint2 s_rect[kPrepWaves][64];       // (x0 | x1 << 16, y0 | y1 << 16)
     __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the small cell counts
     __shared__ uint32_t s_qreg[kPrepWaves][kBinQueue];   // passing pairs: region
@@ -1553,7 +1555,6 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
         e->e1 = fp.e1;
         e->e2 = fp.e2;
         e->bb = fp.bbox;
-        e->rec = r;
     }
     const uint32_t cells = has ? (x1 - x0 + 1u) * (y1 - y0 + 1u) : 0u;
     const bool big = cells > kBinSmall;
@@ -1568,19 +1569,15 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     s_fp[wave][1][lane] = fp.e1;
     s_fp[wave][2][lane] = fp.e2;
     s_fp[wave][3][lane] = fp.bbox;
-    {
-        const float4* q = reinterpret_cast<const float4*>(&r);
-        s_fp[wave][4][lane] = q[0];
-        s_fp[wave][5][lane] = q[1];
-        s_fp[wave][6][lane] = q[2];
-        s_fp[wave][7][lane] = q[3];
-    }
     s_rect[wave][lane] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
     s_cum[wave][lane] = cum;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    // No lists (the sizing pass of a new geometry, DESIGN.md "List sizing"):
+    // the pairs are counted, nothing is stored, nothing can overflow.
+    const uint32_t count_only = wave_uniform(bins.list == nullptr ? 1u : 0u);
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
     bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
@@ -1606,11 +1603,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
-                const uint2 bc = reg[b] != kEmpty ? *reinterpret_cast<const uint2*>(bins.desc + reg[b])
-                                                  : make_uint2(0u, 0u);
+                const uint2 bc = reg[b] != kEmpty && count_only == 0u
+                                     ? *reinterpret_cast<const uint2*>(bins.desc + reg[b]) : make_uint2(0u, 0u);
                 lbase[b] = bc.x;
                 lcap[b] = bc.y;
             }
+            if (count_only) continue;              // the sizing pass: counts only
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 if (reg[b] == kEmpty) continue;
@@ -1619,7 +1617,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 else {
                     float4* e = reinterpret_cast<float4*>(bins.list + (size_t)lbase[b] + slot[b]);
 #pragma unroll
-                    for (uint32_t w = 0; w < 8; ++w) e[w] = s_fp[wave][w][own[b]];
+                    for (uint32_t w = 0; w < kEntryQuads; ++w) e[w] = s_fp[wave][w][own[b]];
                 }
             }
         }
@@ -1700,83 +1698,59 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 // ---------------------------------------------------------------------------
 // k_render_binned: the render over the binned region lists.
 //
-// A workgroup of kTileWaves (4) waves renders one 32x8 row of a region's 8x8
-// tiles, one tile per wave.  The region's candidates -- its list entries
-// followed by the global list's, each a 128-B footprint + triangle record --
-// are staged into LDS by DMA (global_load_lds, no registers), kBinStage at a
-// time and structure-of-arrays, by the workgroup's waves together; then each
-// wave tests its tile rectangle against the staged footprints (one candidate
-// per lane, conflict-free reads), a ballot keeps the survivors, and each
-// survivor's record is read back as a wave-uniform broadcast and tested
-// exactly for the tile's 64 rays.  One global round trip after the region's
-// count, and each region's entries are read once per workgroup.  Rays are
-// generated when the first survivor appears (pixel offsets from the frame's
-// tables); a tile without survivors stores the miss constants.
+// A workgroup of kTileWaves waves renders kTileWaves of a region's 8x8 tiles,
+// one tile per wave, and every wave works on its own (render_tile): the
+// region's candidates -- its list entries followed by the global list's,
+// 64-B footprints -- are read by the wave into registers, one per lane per
+// round, and only the survivors of the tile test move their triangle records
+// (into the wave's LDS stage, by DMA).  Round 3 staged every candidate's
+// footprint and record (128 B) through a workgroup-shared stage: every wave
+// of a workgroup waited at two barriers per round for the slowest, and a tile
+// without survivors still paid the records' DMA.  Rays are generated when the
+// first survivor appears (pixel offsets from the frame's tables); a tile
+// without survivors stores the miss constants.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kTileWaves = XRT_TILE_WAVES;         // tile waves per workgroup
 constexpr uint32_t kWavesPerRegion = 16u;               // one 8x8 tile per wave
-constexpr uint32_t kBinStage = XRT_STAGE;                  // candidates staged per round
-static_assert(kBinStage % 64u == 0u && 8u % kTileWaves == 0u, "staging layout");
+// Candidates a tile wave culls per round: kRoundSlots per lane, their
+// footprints loaded together; the survivors of each 64 then have their
+// records staged in the wave's own LDS (64 B each) and tested.
+constexpr uint32_t kBinStage = XRT_STAGE;
+constexpr uint32_t kRoundSlots = kBinStage / 64u;
+static_assert(kBinStage % 64u == 0u && kRoundSlots >= 1u && kRoundSlots <= 4u, "64 to 256 candidates per round");
+static_assert(16u % kTileWaves == 0u, "a workgroup's waves render tiles of one region");
 
-// The staged candidates: q[0..3][k] = footprint (e0 -- w = id --, e1, e2, box),
-// q[4..7][k] = the TriRec, of staged candidate k.
-struct RegionStage {
-    float4 q[8][kBinStage];
+// One tile wave's staged records: q[0..3][L] = the TriRec of lane L's
+// candidate, written by that lane's DMA when the candidate survived the tile
+// test, read back as a broadcast by the survivor loop.  Private to the wave:
+// no workgroup barrier anywhere in the render.
+struct RecStage {
+    float4 q[4][64];
 };
+// LDS of one render workgroup (k_prep's residency cap is derived from it, xrt_abi.hip)
+constexpr uint32_t kRenderLdsPerWave = sizeof(RecStage);
 
-// Candidates [base, base + cnt) into the stage.  Candidate k is the region's
-// entry k (k < n_local), then the global list's; wave w copies quarters
-// [w * 8 / kTileWaves, (w + 1) * 8 / kTileWaves) of every candidate.
-__device__ __forceinline__ void stage_entries(RegionStage& st, const RegionEntry* __restrict__ local,
-                                              uint32_t n_local, const RegionEntry* __restrict__ glob,
-                                              uint32_t base, uint32_t cnt)
+// The survivors of one round slot into st: each survivor lane (`pass`) DMAs
+// its candidate's record (`id`) to q[*][lane].  Wave-private, so a vmcnt
+// wait makes them readable.
+__device__ __forceinline__ void stage_survivor_records(RecStage& st, const TriRec* __restrict__ recs, bool pass,
+                                                       uint32_t id)
 {
-    const uint32_t lane = threadIdx.x & 63u, wave = wave_in_block();
-    constexpr uint32_t kPer = 8u / kTileWaves;
-    for (uint32_t g = 0; g < cnt; g += 64u) {
-        if (g + lane < cnt) {
-            const uint32_t k = base + g + lane;
-            const float4* src = reinterpret_cast<const float4*>(k < n_local ? local + k : glob + (k - n_local));
+    if (pass) {
+        const float4* src = reinterpret_cast<const float4*>(recs + id);
 #pragma unroll
-            for (uint32_t i = 0; i < kPer; ++i) {
-                const uint32_t q = wave * kPer + i;
-                __builtin_amdgcn_global_load_lds((const void*)(src + q),
-                                                 (__attribute__((address_space(3))) void*)&st.q[q][g], 16, 0, 0);
-            }
-        }
+        for (uint32_t q = 0; q < 4u; ++q)
+            __builtin_amdgcn_global_load_lds((const void*)(src + q),
+                                             (__attribute__((address_space(3))) void*)&st.q[q][0], 16, 0, 0);
     }
 }
 
-// The same from the whole mesh (a region whose list overflowed): candidate k
-// is triangle k, its footprint from the SoA cull planes, its record from recs.
-__device__ __forceinline__ void stage_mesh(RegionStage& st, const float4* __restrict__ culls,
-                                           const TriRec* __restrict__ recs, uint32_t T, uint32_t base,
-                                           uint32_t cnt)
+__device__ __forceinline__ void test_staged_one(const RecStage& st, uint32_t k, float dx, float dy, float dz,
+                                                HitList& hl)
 {
-    const uint32_t lane = threadIdx.x & 63u, wave = wave_in_block();
-    constexpr uint32_t kPer = 8u / kTileWaves;
-    for (uint32_t g = 0; g < cnt; g += 64u) {
-        if (g + lane < cnt) {
-            const uint32_t j = base + g + lane;
-            const float4* rec = reinterpret_cast<const float4*>(recs + j);
-            const float4* src[8] = {culls + (size_t)T + j, culls + 2 * (size_t)T + j, culls + 3 * (size_t)T + j,
-                                    culls + j, rec, rec + 1, rec + 2, rec + 3};
-#pragma unroll
-            for (uint32_t i = 0; i < kPer; ++i) {
-                const uint32_t q = wave * kPer + i;
-                __builtin_amdgcn_global_load_lds((const void*)src[q],
-                                                 (__attribute__((address_space(3))) void*)&st.q[q][g], 16, 0, 0);
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
-                                                float dz, HitList& hl)
-{
-    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[7].x)
-    const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k];
-    const float tnum = st.q[7][k].x;
+    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[3].x)
+    const float4 a0 = st.q[0][k], a1 = st.q[1][k], a2 = st.q[2][k];
+    const float tnum = st.q[3][k].x;
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
@@ -1789,24 +1763,24 @@ __device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t 
     hl.push_if(h, t);
 }
 
-// The signed model's: the term's triangle id from the footprint (e0.w) and its
-// sign from the record's unit normal (pad0..2).
-__device__ __forceinline__ void test_staged_one(const RegionStage& st, uint32_t k, float dx, float dy,
+// The signed model's: the term's sign from the record's unit normal (pad0..2),
+// `id` the candidate's triangle id (wave-uniform).
+__device__ __forceinline__ void test_staged_one(const RecStage& st, uint32_t k, uint32_t id, float dx, float dy,
                                                 float dz, float sx, float sy, float sz, SignedHits& hl)
 {
-    const float4 a0 = st.q[4][k], a1 = st.q[5][k], a2 = st.q[6][k], a3 = st.q[7][k];
+    const float4 a0 = st.q[0][k], a1 = st.q[1][k], a2 = st.q[2][k], a3 = st.q[3][k];
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
     bool h;
     const float t = mt_finish(det, u, v, a3.x, h);
-    if (__ballot(h)) hl.push_if(h, t, __float_as_uint(st.q[0][k].w), hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
+    if (__ballot(h)) hl.push_if(h, t, id, hit_sign(sx, sy, sz, a3.y, a3.z, a3.w));
 }
 
-// The staged loop's tile test of candidate k, from its list entry (the
-// overflow fix-up's survivors; a region rendered from the whole mesh takes
-// the whole-candidate fix-up).  The tile rectangle is recomputed from its
-// corner here rather than kept live from the loop.
+// The tile test of candidate k, from its list entry (the overflow fix-up's
+// survivors; a region rendered from the whole mesh takes the whole-candidate
+// fix-up).  The tile rectangle is recomputed from its corner here rather than
+// kept live from the loop.
 struct EntryCull {
     const RegionEntry* __restrict__ local;
     const RegionEntry* __restrict__ glob;
@@ -1824,11 +1798,16 @@ struct EntryCull {
 };
 
 // One wave's 8x8 tile `tile` of the region in launch slot `slot`: the body of
-// k_render_binned.  Every wave of the workgroup calls it for the same slot
-// (they stage the region's candidates together); the statistics accumulate in
+// k_render_binned.  The wave works alone: per round, each lane loads one
+// candidate's footprint (its region-list entry, 64 B, or the whole mesh's cull
+// planes) into registers and tests the tile rectangle against it, a ballot
+// keeps the survivors, each survivor lane DMAs its candidate's record into the
+// wave's LDS stage, and each survivor is tested exactly for the tile's 64
+// rays from a broadcast LDS read.  A tile whose candidates all fail never
+// touches a record; no wave waits for another.  The statistics accumulate in
 // ws, and `cand` gets the region's candidate count.
 template <bool kSigned>
-__device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __restrict__ recs,
+__device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restrict__ recs,
                                             const float4* __restrict__ culls, const RenderParams& p,
                                             const Outputs& out, const BinBuffers& bins, uint32_t n_glob,
                                             uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand)
@@ -1857,56 +1836,76 @@ __device__ __forceinline__ void render_tile(RegionStage& st, const TriRec* __res
     const size_t o = out.packed ? (size_t)slot * kPackBlock + ((tile >> 2) * 8u + (lane >> 3)) * kRegion +
                                       (tile & 3u) * 8u + (lane & 7u)
                                 : (size_t)(row - p.row_begin) * p.width + col;
+    if (!tile_live) return;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
     bool have_ray = false;                         // wave-uniform
-    // the tile's pixel offsets, loaded beside the region's counts: a tile with
+    // the tile's pixel offsets, loaded beside the first footprints: a tile with
     // survivors generates its rays without another memory round trip
     const float pre_v = out.off.v[min(row, p.height - 1u)];
     const float pre_u = out.off.u[min(col, p.width - 1u)];
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
-    // every wave of the workgroup takes part in every round's staging and barriers
     for (uint32_t base = 0; base < n_cand; base += kBinStage) {
-        const uint32_t cnt = min(kBinStage, n_cand - base);
-        if (base) __syncthreads();                 // the previous round's reads are done
-        if (whole) stage_mesh(st, culls, recs, T, base, cnt);
-        else stage_entries(st, local, n_local, glob, base, cnt);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
-        __syncthreads();                           // and every wave's
-        if (!tile_live) continue;
-        for (uint32_t k0 = 0; k0 < cnt; k0 += 64u) {
-            const uint32_t k = k0 + lane;
-            bool pass = false;
-            if (k < cnt)
-                pass = edges_pass_tile(st.q[0][k], st.q[1][k], st.q[2][k], xc, yc) &
-                       box_overlaps(st.q[3][k], fx0, fx1, fy0, fy1);
-            unsigned long long m = __ballot(pass);
-            if (!m) continue;
-            tests += (uint32_t)__popcll(m);
-            if (!have_ray) {
+        // the round's footprints, kRoundSlots per lane, all loads in flight together
+        float4 f[kRoundSlots][4];
+        uint32_t id[kRoundSlots];
+#pragma unroll
+        for (uint32_t r = 0; r < kRoundSlots; ++r) {
+            const uint32_t k = base + r * 64u + lane;
+            id[r] = k;
+            f[r][0] = f[r][1] = f[r][2] = make_float4(0.0f, 0.0f, -1.0f, 0.0f);   // fails the edges
+            f[r][3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (k < n_cand) {
+                if (whole) {                       // SoA cull planes: box, then edges 0..2
+                    f[r][0] = culls[(size_t)T + k];
+                    f[r][1] = culls[2 * (size_t)T + k];
+                    f[r][2] = culls[3 * (size_t)T + k];
+                    f[r][3] = culls[k];
+                } else {
+                    const float4* e = reinterpret_cast<const float4*>(k < n_local ? local + k : glob + (k - n_local));
+                    f[r][0] = e[0];
+                    f[r][1] = e[1];
+                    f[r][2] = e[2];
+                    f[r][3] = e[3];
+                }
+            }
+        }
+        // the tile test of every slot first (the footprints' registers die here)
+        unsigned long long m[kRoundSlots];
+#pragma unroll
+        for (uint32_t r = 0; r < kRoundSlots; ++r) {
+            const bool pass = edges_pass_tile(f[r][0], f[r][1], f[r][2], xc, yc) &
+                              box_overlaps(f[r][3], fx0, fx1, fy0, fy1);
+            if (!whole) id[r] = __float_as_uint(f[r][0].w);
+            m[r] = __ballot(pass);
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kRoundSlots; ++r) {
+            unsigned long long mm = m[r];
+            if (!mm) continue;
+            // the survivors' records into the wave's stage (DMA, no registers)
+            stage_survivor_records(st, recs, (mm >> lane) & 1ull, id[r]);
+            if (!have_ray) {                       // under the records' DMA
                 make_ray_from(*out.frame, pre_v, pre_u, dx, dy, dz, sx, sy, sz);
                 have_ray = true;
             }
-            if constexpr (kSigned) {
-                while (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                    clear_lane_bit(m, b);
-                    test_staged_one(st, k0 + b, dx, dy, dz, sx, sy, sz, hl);
-                }
-            } else {
-                while (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                    clear_lane_bit(m, b);
-                    test_staged_one(st, k0 + b, dx, dy, dz, hl);
-                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's records have landed
+            tests += (uint32_t)__popcll(mm);
+            while (mm) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(mm);
+                clear_lane_bit(mm, b);
+                if constexpr (kSigned)
+                    test_staged_one(st, b, (uint32_t)__builtin_amdgcn_readlane((int)id[r], (int)b), dx, dy, dz, sx,
+                                    sy, sz, hl);
+                else
+                    test_staged_one(st, b, dx, dy, dz, hl);
             }
         }
     }
     ws.tile_tests += tests;
-    if (!tile_live) return;
     if (have_ray) {
         const uint32_t nl = whole ? 0u : n_local;
         auto fetch = [=](uint32_t k) {
@@ -1980,7 +1979,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
                   "a workgroup's waves render tiles of one region");
     constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
-    __shared__ RegionStage st;
+    __shared__ RecStage st[kTileWaves];            // one private stage per wave
     const uint64_t t_start = block_start_stamp();
     const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
     const uint32_t wave = wave_in_block();
@@ -2014,7 +2013,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t g = blk * kTileWaves + wave;                      // wave of the grid
     const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
-    render_tile<kSigned>(st, recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
+    render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
 }

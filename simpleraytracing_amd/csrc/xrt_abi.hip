@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "xrt.h"
+#include "xrt_debug.h"
 #include "kernels/xrt_kernels.h"
 
 using namespace XRT_KERNEL_NS;
@@ -32,6 +32,9 @@ constexpr uint32_t kInitialRegionCap = 256;
 // pair on the render dispatch of every kEventStride-th frame, a cross-check of
 // the in-kernel spans (a start event costs the frame a few microseconds).
 constexpr size_t kTimingRecords = (size_t)1 << 27;
+// After a timed region a context keeps one chunk of at most this many bytes
+// for the next region; larger ones are freed (xrt_timing_end).
+constexpr size_t kKeptTimingBytes = (size_t)64 << 20;
 constexpr uint64_t kEventStride = 16;
 // s_memrealtime ticks per millisecond (100 MHz on gfx950)
 constexpr double kTicksPerMs = 1e5;
@@ -41,12 +44,21 @@ constexpr double kTicksPerMs = 1e5;
 #define XRT_FRAME_SETS 4
 #endif
 constexpr int kFrameSets = XRT_FRAME_SETS;
-// LDS a k_prep workgroup holds (its own 10 KB + dynamic padding): at most
-// three share a CU with the render's eight 8-KB workgroups (160 KB), so the
-// preparation beside a render cannot take more of a CU's wave slots than
-// that (1.12 M-triangle frame 1,224 -> 1,143 us, 4096^2 -1.5 %, 2048^2 equal;
-// one or two per CU starve the preparation, DESIGN.md "Pipelining").
-constexpr size_t kPrepLds = 32768;
+// LDS a k_prep workgroup holds (its own + dynamic padding): the CU's LDS left
+// beside a render at full occupancy (XRT_RENDER_WAVES waves per SIMD, each
+// with its record stage), split over kPrepPerCu workgroups, so no more of
+// them share a CU with the render (round 3: three beside the render, 1.12
+// M-triangle frame 1,224 -> 1,143 us, 4096^2 -1.5 %, 2048^2 equal; one or two
+// per CU starve the preparation, DESIGN.md "Pipelining").  LDS is allocated
+// in 512-B granules.
+#ifndef XRT_PREP_PER_CU
+#define XRT_PREP_PER_CU 3
+#endif
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kLdsGranule = 512;
+constexpr size_t kRenderLdsPerCu = (size_t)XRT_RENDER_WAVES * 4 * kRenderLdsPerWave;
+static_assert(kRenderLdsPerCu < kLdsPerCu, "the render's stages fit a CU at full occupancy");
+constexpr size_t kPrepLds = (kLdsPerCu - kRenderLdsPerCu) / XRT_PREP_PER_CU / kLdsGranule * kLdsGranule;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
@@ -69,6 +81,7 @@ static_assert(kAheadFrames + 2 <= (size_t)kFrameSets, "sets for the renders in f
 // it launches the render, and for the completion event of the render that
 // last used the set before it prepares into the set again.
 constexpr uint32_t kDirtyAll = 0xFFFFFFFFu;
+constexpr int kHostCallFields = 10;    // xrt_debug_host_call_ms
 
 struct FrameSet {
     TriRec* recs = nullptr;        // per-render records
@@ -82,6 +95,10 @@ struct FrameSet {
     size_t block_stats_cap = 0;
     uint2* times = nullptr;              // their timing records (Outputs::wave_times), frames not sampled
     size_t times_cap = 0;
+    // where the set's last render stored its timing records: `times`, or a
+    // timed region's chunk (copied back into `times` by xrt_timing_end)
+    const uint2* last_times = nullptr;
+    uint32_t rendered_blocks = 0;        // records of the set's last render (n_blocks of its frame)
     uint32_t n_blocks = 0;         // records of the set's last render
     bool binned = false;           // the set's last frame was binned (BinState valid)
 
@@ -193,6 +210,13 @@ struct xrt_context {
     size_t stage_cap = 0;
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    // host time of the last host-buffer call (xrt_render_rows), ms:
+    // [0] device planes, [1] enqueue (preparation, sizing, launch), [2] wait for
+    // the render, [3..5] D2H of image / L-buffer / u8, [6] statistics, [7] total;
+    // within them: [8] every hipMalloc of the call, [9] a new geometry's list
+    // sizing (count read-back, layout upload)
+    double host_call_ms[kHostCallFields] = {};
+    double alloc_ms = 0.0, sizing_ms = 0.0;          // running sums ([8], [9])
     // region timing (xrt_timing_begin/end)
     bool timing = false;
     std::vector<hipEvent_t> tev;      // pairs: [2i] start, [2i+1] stop of a sampled render dispatch
@@ -206,8 +230,9 @@ struct xrt_context {
         size_t cap, used;
     };
     std::vector<TimesChunk> tchunks;
-    struct TimesSample {
-        size_t chunk, offset, n;
+    struct TimesSample {              // a frame's records: where they are (chunks never move) and how many
+        const uint2* p;
+        size_t n;
     };
     std::vector<TimesSample> tsamples;
     double event_ms = 0.0;            // the last timed region's HIP-event samples
@@ -318,7 +343,9 @@ int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
         cap = 0;
     }
     size_t n = std::max<size_t>(need_elems, 1);
+    const auto t = HostClock::now();
     XRT_HIP(ctx, hipMalloc(&ptr, n * sizeof(T)));
+    if (ctx) ctx->alloc_ms += std::chrono::duration<double, std::milli>(HostClock::now() - t).count();
     cap = n;
     return XRT_OK;
 }
@@ -739,14 +766,17 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     if (new_geometry) ctx->compact = false;
     const uint32_t fixed_cap = ctx->bin_force_cap ? (uint32_t)std::min<size_t>(kInitialRegionCap, ctx->bin_force_cap)
                                                   : kInitialRegionCap;
+    // A new geometry's first k_prep only counts its pairs (no lists): the
+    // compact lists are sized from the counts and k_prep runs again into them.
+    const bool sizing = new_geometry && !ctx->bin_force_cap;
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
         const bool compact = ctx->compact && !ctx->bin_force_cap;
         bool cleared = false;
-        if ((rc = bin_buffers(ctx, fs, n_regions, compact ? ctx->slot_pool : (uint64_t)n_regions * fixed_cap, bins,
-                              bin_ctl, ps, cleared)))
-            return rc;
+        const uint64_t entries = compact ? ctx->slot_pool : sizing ? 0u : (uint64_t)n_regions * fixed_cap;
+        if ((rc = bin_buffers(ctx, fs, n_regions, entries, bins, bin_ctl, ps, cleared))) return rc;
+        if (sizing) bins.list = nullptr;
         bins.tile_slots = n_regions;
         if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
@@ -756,11 +786,13 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
 
     hipEvent_t prep_done = fs.ready;
     if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
-    if (new_geometry && !ctx->bin_force_cap) {
+    if (sizing) {
         // Size the compact region lists once per frame geometry (mesh, camera,
-        // strip): a synchronous read of every region's count, slot offsets
-        // from them, and a re-run of k_prep into the compact lists.
+        // strip): a synchronous read of every region's count (the count-only
+        // pass above), slot offsets from them, and a re-run of k_prep into the
+        // compact lists.
         ++ctx->hp_sizings;
+        const auto t_sizing = HostClock::now();
         std::vector<uint32_t> counts((size_t)n_regions * kCounterStride);
         BinState st = {};
         XRT_HIP(ctx, hipMemcpyAsync(counts.data(), bins.counts, counts.size() * sizeof(uint32_t),
@@ -798,6 +830,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
         if ((rc = upload_layout(ctx, ctx->compact_layout, rx, ry, std::move(slot_region), base, cap))) return rc;
+        ctx->sizing_ms += std::chrono::duration<double, std::milli>(HostClock::now() - t_sizing).count();
         ctx->plan_tile_slots = tile_slots;
         ctx->plan_valid = tile_slots < n_regions;
         ctx->slot_pool = run;
@@ -851,7 +884,8 @@ int timing_slot(xrt_context* ctx, size_t n, uint2*& slot)
         size_t k = 0;
         while (k < ctx->tchunks.size() && !(ctx->tchunks[k].used == 0 && ctx->tchunks[k].cap >= n)) ++k;
         if (k < ctx->tchunks.size() && k + 1 < ctx->tchunks.size()) {
-            std::swap(ctx->tchunks[k], ctx->tchunks.back());   // an unused chunk to the end
+            // an unused chunk to the end (the samples hold device pointers, not indices)
+            std::swap(ctx->tchunks[k], ctx->tchunks.back());
         } else if (k == ctx->tchunks.size()) {
             xrt_context::TimesChunk c = {nullptr, want, 0};
             XRT_HIP(ctx, hipMalloc(&c.p, want * sizeof(uint2)));
@@ -859,7 +893,7 @@ int timing_slot(xrt_context* ctx, size_t n, uint2*& slot)
         }
     }
     xrt_context::TimesChunk& c = ctx->tchunks.back();
-    ctx->tsamples.push_back({ctx->tchunks.size() - 1, c.used, n});
+    ctx->tsamples.push_back({c.p + c.used, n});
     slot = c.p + c.used;
     c.used += n;
     return XRT_OK;
@@ -942,6 +976,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         if (rc) return rc;
         out.wave_times = slot;
     }
+    fs.last_times = out.wave_times;
+    fs.rendered_blocks = fs.n_blocks;
     if (ctx->timing && rows > 0 && frame_in_region % kEventStride == 0) {
         if (ctx->tev_used + 2 > ctx->tev.size()) {
             for (int k = 0; k < 64; ++k) {
@@ -1088,7 +1124,9 @@ int xrt_create(int device, xrt_context** out)
     ok = ok && hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
     hipFuncAttributes prep_attr = {};
     ok = ok && hipFuncGetAttributes(&prep_attr, reinterpret_cast<const void*>(k_prep)) == hipSuccess;
-    ctx->prep_lds = prep_attr.sharedSizeBytes < kPrepLds ? kPrepLds - prep_attr.sharedSizeBytes : 0;
+    // k_prep's own LDS must fit the cap (else more than XRT_PREP_PER_CU would not fit beside the render)
+    ok = ok && prep_attr.sharedSizeBytes <= kPrepLds;
+    ctx->prep_lds = ok ? kPrepLds - prep_attr.sharedSizeBytes : 0;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
@@ -1469,6 +1507,13 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     return XRT_OK;
 }
 
+int xrt_debug_host_call_ms(xrt_context* ctx, double ms[10])
+{
+    if (!ctx || !ms) return XRT_ERR_ARGUMENT;
+    std::copy(ctx->host_call_ms, ctx->host_call_ms + kHostCallFields, ms);
+    return XRT_OK;
+}
+
 int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4])
 {
     if (!ctx || !counters) return XRT_ERR_ARGUMENT;
@@ -1499,7 +1544,7 @@ int xrt_debug_block_records(xrt_context* ctx, void* dst, uint64_t capacity, uint
         ctx->pending = false;
     }
     const FrameSet* fs = ctx->last_set;
-    *n_records = fs ? fs->n_blocks : 0u;
+    *n_records = fs ? fs->rendered_blocks : 0u;
     const size_t bytes = std::min<size_t>((size_t)capacity, (size_t)*n_records * sizeof(BlockStats));
     if (bytes && dst) XRT_HIP(ctx, hipMemcpy(dst, fs->block_stats, bytes, hipMemcpyDeviceToHost));
     return XRT_OK;
@@ -1509,15 +1554,17 @@ int xrt_debug_wave_times(xrt_context* ctx, uint32_t frames_back, uint32_t* dst, 
                          uint64_t* n_records)
 {
     if (!ctx || !n_records) return XRT_ERR_ARGUMENT;
-    if (frames_back >= (uint32_t)kFrameSets) return fail(ctx, XRT_ERR_ARGUMENT, "frames_back must be < 4");
+    if (frames_back >= (uint32_t)kFrameSets)
+        return fail(ctx, XRT_ERR_ARGUMENT, "frames_back must be < " + std::to_string(kFrameSets));
     XRT_HIP(ctx, hipSetDevice(ctx->device));
     XRT_HIP(ctx, hipDeviceSynchronize());
     const FrameSet* fs = ctx->last_set
                              ? &ctx->sets[((ctx->last_set - ctx->sets) + kFrameSets - (int)frames_back) % kFrameSets]
                              : nullptr;
-    *n_records = fs ? fs->n_blocks : 0u;
+    // the set's last RENDER's count (a frame prepared ahead into the set since has its own)
+    *n_records = fs && fs->last_times ? fs->rendered_blocks : 0u;
     const size_t n = std::min<size_t>((size_t)capacity, (size_t)*n_records);
-    if (n && dst) XRT_HIP(ctx, hipMemcpy(dst, fs->times, n * sizeof(uint2), hipMemcpyDeviceToHost));
+    if (n && dst) XRT_HIP(ctx, hipMemcpy(dst, fs->last_times, n * sizeof(uint2), hipMemcpyDeviceToHost));
     return XRT_OK;
 }
 
@@ -1541,8 +1588,8 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     // The last render's per-workgroup (per-wave) records, summed here.
     std::memset(stats, 0, sizeof *stats);
     const FrameSet* fs = ctx->last_set;
-    if (fs && fs->n_blocks) {
-        std::vector<BlockStats> rec(fs->n_blocks);
+    if (fs && fs->rendered_blocks) {
+        std::vector<BlockStats> rec(fs->rendered_blocks);
         XRT_HIP(ctx, hipMemcpy(rec.data(), fs->block_stats, rec.size() * sizeof(BlockStats),
                                hipMemcpyDeviceToHost));
         for (const BlockStats& b : rec) {
@@ -1558,9 +1605,9 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
     }
     stats->global_triangles = 0;
     double ms = 0.0;
-    if (fs && fs->n_blocks && !ctx->timing) {      // the set's records (a timed region keeps its samples apart)
-        std::vector<uint2> t(fs->n_blocks);
-        XRT_HIP(ctx, hipMemcpy(t.data(), fs->times, t.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    if (fs && fs->rendered_blocks && fs->last_times) {    // where the set's last render stored its records
+        std::vector<uint2> t(fs->rendered_blocks);
+        XRT_HIP(ctx, hipMemcpy(t.data(), fs->last_times, t.size() * sizeof(uint2), hipMemcpyDeviceToHost));
         ms = records_span_ms(t);
     }
     stats->kernel = (uint32_t)ctx->last_kernel;
@@ -1613,14 +1660,37 @@ int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches)
     std::vector<uint2> t;
     for (const auto& smp : ctx->tsamples) {
         t.resize(smp.n);
-        XRT_HIP(ctx, hipMemcpy(t.data(), ctx->tchunks[smp.chunk].p + smp.offset, smp.n * sizeof(uint2),
-                               hipMemcpyDeviceToHost));
+        XRT_HIP(ctx, hipMemcpy(t.data(), smp.p, smp.n * sizeof(uint2), hipMemcpyDeviceToHost));
         sum += records_span_ms(t);
     }
     *total_ms = sum;
     *launches = ctx->tsamples.size();
+    ctx->tsamples.clear();
     ctx->timing = false;
     ctx->tev_used = 0;
+    // Each set's last records back into its own buffer (xrt_read_stats and
+    // xrt_debug_wave_times read them there), then the chunks go: a context
+    // keeps at most one small chunk (kKeptTimingBytes) for its next region.
+    for (FrameSet& fs : ctx->sets) {
+        if (fs.last_times && fs.last_times != fs.times && fs.times && fs.rendered_blocks <= fs.times_cap)
+            XRT_HIP(ctx, hipMemcpy(fs.times, fs.last_times, fs.rendered_blocks * sizeof(uint2),
+                                   hipMemcpyDeviceToDevice));
+        if (fs.last_times) fs.last_times = fs.times;
+    }
+    size_t keep = ctx->tchunks.size();
+    for (size_t k = 0; k < ctx->tchunks.size(); ++k)
+        if (ctx->tchunks[k].cap * sizeof(uint2) <= kKeptTimingBytes &&
+            (keep == ctx->tchunks.size() || ctx->tchunks[k].cap > ctx->tchunks[keep].cap))
+            keep = k;
+    for (size_t k = 0; k < ctx->tchunks.size(); ++k)
+        if (k != keep) (void)hipFree(ctx->tchunks[k].p);
+    if (keep < ctx->tchunks.size()) {
+        xrt_context::TimesChunk c = ctx->tchunks[keep];
+        c.used = 0;
+        ctx->tchunks.assign(1, c);
+    } else {
+        ctx->tchunks.clear();
+    }
     return XRT_OK;
 }
 
@@ -1640,23 +1710,44 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
     int rc = check_camera(ctx, camera, row_begin, row_end);
     if (rc) return rc;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
+    double* hc = ctx->host_call_ms;
+    const auto t0 = HostClock::now();
+    auto lap = [&](int k, HostClock::time_point& t) {
+        const auto now = HostClock::now();
+        hc[k] = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
+    auto t = t0;
+    std::fill(hc, hc + kHostCallFields, 0.0);
+    const double alloc0 = ctx->alloc_ms, sizing0 = ctx->sizing_ms;
     const size_t n = (size_t)(row_end - row_begin) * camera->width;
     size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
     if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
     if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
     if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
     ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
+    lap(0, t);
     rc = enqueue_render(ctx, camera, row_begin, row_end, image ? ctx->d_image : nullptr,
                         lbuffer ? ctx->d_lbuffer : nullptr, image_u8 ? ctx->d_u8 : nullptr, nullptr);
     if (rc) return rc;
+    lap(1, t);
+    XRT_HIP(ctx, hipStreamSynchronize(nullptr));
+    lap(2, t);
     if (n) {
         if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
+        lap(3, t);
         if (lbuffer)
             XRT_HIP(ctx, hipMemcpy(lbuffer, ctx->d_lbuffer, n * sizeof(float), hipMemcpyDeviceToHost));
+        lap(4, t);
         if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
+        lap(5, t);
     }
     xrt_stats local;
     rc = xrt_read_stats(ctx, stats ? stats : &local);
+    lap(6, t);
+    hc[7] = std::chrono::duration<double, std::milli>(t - t0).count();
+    hc[8] = ctx->alloc_ms - alloc0;
+    hc[9] = ctx->sizing_ms - sizing0;
     return rc;
 }
 

@@ -22,13 +22,23 @@ def declared_functions(header):
     return sorted(set(re.findall(r"\b(xrt_\w+)\s*\(", text)) - {"xrt_status"})
 
 
-def test_libxrt_exports_every_declared_symbol():
+@pytest.mark.parametrize("header", ["xrt.h", "xrt_debug.h"])
+def test_libxrt_exports_every_declared_symbol(header):
+    """The drop-in surface (xrt.h) and the test/diagnostic hooks (xrt_debug.h)."""
     lib = _abi.load()
-    names = declared_functions("xrt.h")
-    assert len(names) >= 18
+    names = declared_functions(header)
+    assert len(names) >= (18 if header == "xrt.h" else 10)
     for n in names:
         assert hasattr(lib, n), n
-        assert n in _abi.XRT_SYMBOLS, f"{n} declared in xrt.h but not bound in _abi.py"
+        assert n in _abi.XRT_SYMBOLS, f"{n} declared in {header} but not bound in _abi.py"
+
+
+def test_product_header_has_no_test_hooks():
+    """Probes, test hooks and diagnostics live in xrt_debug.h, not in the drop-in header."""
+    names = declared_functions("xrt.h")
+    hooks = [n for n in names if n.startswith(("xrt_probe_", "xrt_debug_", "xrt_host_"))
+             or n in ("xrt_set_hit_capacity", "xrt_set_bin_capacity", "xrt_set_fill_plan")]
+    assert not hooks, hooks
 
 
 def test_libxrt_host_exports_every_declared_symbol():

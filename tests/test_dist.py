@@ -195,6 +195,44 @@ def _link_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_wrong_gathered_strip_fails_every_rank(corrupt):
+    """bench.py's end of a strips run (bench.planes_equal + bench.gather_verdict)
+    under torch.distributed.run, gloo, 2 ranks: an exact gather exits 0; one
+    flipped L-buffer bit in rank 1's strip makes EVERY rank exit with
+    bench.EXIT_GATHER_MISMATCH, so the launcher reports the job failed."""
+    import subprocess
+    import sys
+    import bench
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "_gather_job.py")] + (["--corrupt"] if corrupt else [])
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    out = r.stdout + r.stderr
+    if not corrupt:
+        assert r.returncode == 0, out
+        assert "rank 0 exit 0" in out and "rank 1 exit 0" in out
+    else:
+        assert r.returncode != 0, out
+        code = bench.EXIT_GATHER_MISMATCH
+        assert f"rank 0 exit {code}" in out and f"rank 1 exit {code}" in out, out
+        assert "not bit-exact" in out
+
+
+def test_bench_exits_nonzero_on_rank_exception():
+    """bench.run(): an exception in main() leaves through os._exit(1) after its
+    traceback (no hang in a collective or RCCL teardown)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import bench\n"
+            "def boom():\n    raise RuntimeError('rank failure')\n"
+            "bench.main = boom\nbench.run()\nprint('not reached')\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1
+    assert "rank failure" in r.stderr and "not reached" not in r.stdout
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_link_rate_agreed(tmp_path, world):
     """bench.measure_link under gloo: every sender sends to rank 0 at once, rank 0

@@ -553,6 +553,105 @@ def test_culled_4096_rows_vs_oracle(ctx, dragon, kernel):
     ref = oracle.render_row_list(dragon, cam, W, H, rows)
     assert np.array_equal(bits(img.reshape(H, W)[rows].ravel()), bits(ref[0]))
     assert np.array_equal(bits(lb.reshape(H, W)[rows].ravel()), bits(ref[1]))
+    assert np.array_equal(u8.reshape(H, W)[rows].ravel(), ref[2])
+
+
+def test_binned_equals_brute_full_4096(ctx, dragon):
+    """The whole 4096^2 frame (BASELINE configs[3]'s): the binned render equals the
+    literal brute-force render bit for bit on every pixel and statistic (about a
+    quarter second of brute force)."""
+    W = H = 4096
+    a = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BINNED)
+    b = render(ctx, dragon, W, H, xrt.XRT_KERNEL_BRUTE)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(bits(x), bits(y))
+    for f in ("rays", "hit_rays", "odd_rays", "hits", "max_hits", "overflow_rays"):
+        assert getattr(a[3], f) == getattr(b[3], f), f
+
+
+def _setters():
+    """Every setter that starts a new settings generation (frames prepared ahead
+    become stale), with a value that changes nothing in the attenuation render's
+    output and one that restores the default: (name, apply, restore)."""
+    return [
+        ("kernel", lambda c: c.set_kernel(xrt.XRT_KERNEL_TILED), lambda c: c.set_kernel(xrt.XRT_KERNEL_BINNED)),
+        ("hit_capacity", lambda c: c.set_hit_capacity(2), lambda c: c.set_hit_capacity(0)),
+        ("bin_capacity", lambda c: c.set_bin_capacity(16), lambda c: c.set_bin_capacity(0)),
+        ("fill_plan", lambda c: c.set_fill_plan(0), lambda c: c.set_fill_plan(1)),
+        ("model", lambda c: c.set_model(xrt.XRT_MODEL_ATTENUATION, 0.5),
+         lambda c: c.set_model(xrt.XRT_MODEL_ATTENUATION, 0.1037)),
+    ]
+
+
+@pytest.mark.parametrize("name", [s[0] for s in _setters()])
+def test_setter_toggles_keep_frames_exact(dragon, name):
+    """the binning of a geometry is trusted across frames (its
+    k_prep check is armed on the first frame over a plan only), so a setting
+    changed and restored between frames of ONE geometry must not leave a stale
+    plan or list behind: every frame -- before, under and after the setting,
+    device-pointer frames prepared ahead included -- equals a fresh brute-force
+    render bit for bit."""
+    import torch
+    apply, restore = [(a, r) for n, a, r in _setters() if n == name][0]
+    W, H = 640, 512
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.Context(0) as fresh:
+        fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        fresh.upload_mesh(dragon)
+        ref = fresh.render_rows(cam)
+    dev = torch.device("cuda", 0)
+    planes = [torch.empty(W * H, dtype=torch.float32, device=dev), torch.empty(W * H, dtype=torch.float32, device=dev),
+              torch.empty(W * H, dtype=torch.uint8, device=dev)]
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        for phase in ("before", "applied", "restored"):
+            if phase == "applied":
+                apply(c)
+            elif phase == "restored":
+                restore(c)
+            for i in range(4):
+                if i % 2:
+                    got = c.render_rows(cam)[:3]
+                else:
+                    for _ in range(3):           # repeated geometry: frames prepared ahead
+                        c.render_rows_device(cam, 0, H, *(t.data_ptr() for t in planes), 0)
+                    torch.cuda.synchronize(dev)
+                    got = [t.cpu().numpy() for t in planes]
+                for x, y in zip(got, ref[:3]):
+                    assert np.array_equal(bits(x), bits(y)), (name, phase, i)
+
+
+def test_two_timed_regions_keep_their_spans(ctx, dragon):
+    """a timed region's frames keep their timing records in device
+    chunks of 64 frames; a second region on the same context reuses the first
+    region's chunks.  Each region's mean span (xrt_timing_end) agrees with its
+    own HIP-event samples and with the last frame's span read afterwards, so no
+    region sums another's (or unwritten) records."""
+    import torch
+    W = H = 1024
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+    ctx.upload_mesh(dragon)
+    dev = torch.device("cuda", 0)
+    planes = [torch.empty(W * H, dtype=torch.float32, device=dev), torch.empty(W * H, dtype=torch.float32, device=dev),
+              torch.empty(W * H, dtype=torch.uint8, device=dev)]
+    means = []
+    for region in range(3):
+        n = 150 if region < 2 else 20
+        ctx.timing_begin()
+        for _ in range(n):
+            ctx.render_rows_device(cam, 0, H, *(t.data_ptr() for t in planes), 0)
+        ms, launches = ctx.timing_end()
+        ev_ms, ev_launches = ctx.timing_events()
+        assert launches == n and ev_launches == -(-n // 16)
+        mean, ev_mean = ms / launches, ev_ms / ev_launches
+        # spans are the kernels' own execution; events add a launch and a write-back
+        assert 0.3 * ev_mean < mean < 1.2 * ev_mean, (region, mean, ev_mean)
+        last = ctx.read_stats().kernel_ms                 # the region's last frame, read after it
+        assert 0.3 * mean < last < 3.0 * mean, (region, last, mean)
+        means.append(mean)
+    assert max(means[:2]) < 1.5 * min(means[:2]), means
 
 
 def test_tiled_mesh_1m_parity(ctx, dragon):

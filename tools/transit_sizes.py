@@ -8,7 +8,8 @@ step per link rate is max(root strip render + unpack, slowest sender render,
 largest sender transfer) -- the gather of frame k overlaps the render of frame
 k+1, each sender has its own link into rank 0 (DESIGN.md "Multi-GPU").
 
-    python tools/transit_sizes.py [--size W H] [--ranks 1 2 4 8] [--link-gbs 64 128]
+    python tools/transit_sizes.py [--size W H] [--tile-mesh n] [--ranks 1 2 4 8] [--link-gbs 64 128]
+                                  [--splits weighted equal balanced]
 """
 import argparse
 import json
@@ -48,18 +49,25 @@ def main():
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--link-gbs", type=float, nargs="+", default=[64.0, 128.0])
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--tile-mesh", type=int, default=1, help="n x n tiled copies (7 = BASELINE configs[4])")
+    ap.add_argument("--splits", nargs="+", default=["weighted", "equal", "balanced"])
     args = ap.parse_args()
     import torch
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.strips import root_share, strip_bounds, weighted_bounds
     W, H = args.size
     tris = xrt.load_ply(os.path.join(ROOT, "data", "dragon.ply"))
+    if args.tile_mesh > 1:
+        from simpleraytracing_amd.scenes import tiled_mesh
+        tris = tiled_mesh(tris, args.tile_mesh)
     cam = xrt.camera_for_mesh(tris, W, H)
     import bench
     from simpleraytracing_amd.strips import balanced_bounds
     band_cost, band_bytes, _ = bench.band_model(xrt, torch, tris, cam, W, H, 0)
     out = {}
-    splits = ["weighted", "equal"] + [f"balanced@{g:g}" for g in args.link_gbs]
+    splits = [s for s in ("weighted", "equal") if s in args.splits]
+    if "balanced" in args.splits:
+        splits += [f"balanced@{g:g}" for g in args.link_gbs]
     for split in splits:
         for n in args.ranks:
             if split != "weighted" and n == 1:
@@ -86,7 +94,7 @@ def main():
                 pred[f"{gbs:g}GBs"] = {"step_us": round(step, 1), "transfer_us": round(transfer, 1),
                                        "mrays_s": round(W * H / step, 0) if step else None}
             out[f"{split}_{n}"] = {"ranks": ranks, "bounds": bounds, "predicted": pred}
-    print(json.dumps({"image": [W, H], "splits": out}))
+    print(json.dumps({"image": [W, H], "triangles": len(tris), "splits": out}))
 
 
 if __name__ == "__main__":
