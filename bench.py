@@ -302,10 +302,16 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
     tests = stats.tile_tests * 64 if kernel != "brute" else rays_per_launch * T
     if kernel == "brute":
         alg_bytes = rays_per_launch * BYTES_OUT_PER_RAY + 64 * T
+    elif kernel == "binned":
+        # outputs + the region lists' entries (one 64-B footprint per region
+        # candidate, read once) + the record (TriRec, 64 B) of every triangle;
+        # the render's other reads (each region's entries by its 16 tile waves,
+        # survivors' records) are re-reads an L2 should hold
+        alg_bytes = rays_per_launch * BYTES_OUT_PER_RAY + 64 * T + 64 * stats.candidates
     else:
         # outputs + cull planes (4 float4) and TriRec (64 B) of every triangle
-        # + one u32 per region-list entry (tiled: the LDS list is built from the
-        # footprint boxes, 16 B per triangle per region swept)
+        # + one u32 per region candidate (the LDS list built from the footprint
+        # boxes, 16 B per triangle per region swept)
         alg_bytes = rays_per_launch * BYTES_OUT_PER_RAY + 128 * T + 4 * stats.candidates
     hbm_rate = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
     r = {

@@ -141,9 +141,11 @@ void xrt_host_mt_check(const float* det, const float* a, const float* b, const f
  * ms[0] device planes (allocated once per size), [1] enqueue (preparation,
  * list sizing of a new geometry, launch), [2] wait for the render, [3..5] D2H
  * of image / L-buffer / u8, [6] statistics, [7] total; within them [8] the
- * time in hipMalloc and [9] a new frame geometry's list sizing.
+ * time in hipMalloc, [9] a new frame geometry's list sizing, [10] device
+ * synchronisations before a launch layout's upload, [11] host waits for the
+ * preparation (k_prep), [12] kernel launches.
  */
-int xrt_debug_host_call_ms(xrt_context* ctx, double ms[10]);
+int xrt_debug_host_call_ms(xrt_context* ctx, double ms[13]);
 
 #ifdef __cplusplus
 }

@@ -255,10 +255,11 @@ class Context:
 
     def host_call_ms(self) -> dict:
         """Host time of the last render_rows call, ms (xrt_debug_host_call_ms)."""
-        ms = (ctypes.c_double * 10)()
+        ms = (ctypes.c_double * 13)()
         self._check(self._lib.xrt_debug_host_call_ms(self._ctx, ms), "xrt_debug_host_call_ms")
         keys = ("device_planes", "enqueue", "render_wait", "d2h_image", "d2h_lbuffer", "d2h_u8", "stats", "total",
-                "of_which_hipmalloc", "of_which_list_sizing")
+                "of_which_hipmalloc", "of_which_list_sizing", "of_which_device_sync", "of_which_prep_wait",
+                "of_which_launches")
         return dict(zip(keys, (float(v) for v in ms)))
 
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,

@@ -1370,6 +1370,10 @@ struct BinBuffers {
     // Slots [0, tile_slots) render as tiles (16 waves a region); the rest are
     // the fill plan's empty regions (one workgroup each).  = regions: no plan.
     uint32_t tile_slots;
+    // Slots [0, split_slots) (the heaviest regions of the plan's order) render
+    // each tile with two waves, each testing half of the tile's survivors, the
+    // halves' hit lists merged (k_render_binned); 0: none.
+    uint32_t split_slots;
     // k_prep's flags (host-mapped memory, read by the host before it launches
     // the render): [0] = 1 when it bins a pair past tile_slots (the fill plan)
     // or a triangle into the global list, [1] = 1 when a region's count passes
@@ -1806,11 +1810,49 @@ struct EntryCull {
 // rays from a broadcast LDS read.  A tile whose candidates all fail never
 // touches a record; no wave waits for another.  The statistics accumulate in
 // ws, and `cand` gets the region's candidate count.
+// Split tiles (BinBuffers::split_slots): the two waves of a tile cull the same
+// candidates (same ballots, so both see the same rounds with survivors and
+// both generate the rays) and test alternate survivors -- half 1 the survivors
+// in odd lanes, half 0 the even ones.  Half 1 then publishes its sorted hit
+// list, its hit count and its test count in its own LDS stage; after one
+// workgroup barrier half 0 inserts them into its own list (the union of two
+// sorted lists is the ray's sorted hit set when the counts fit the list, and
+// a count past it takes the exact fix-up as any overflowed ray does) and
+// finishes the tile alone.  kSplitNone: an ordinary tile.
+constexpr uint32_t kSplitNone = 0u, kSplitHalf0 = 1u, kSplitHalf1 = 2u;
+constexpr bool kCanSplit = kTileWaves % 2u == 0u;   // a tile's two waves share a workgroup
+static_assert(kMaxHits <= 12, "a half's hit list fits three float4 of its stage");
+
+__device__ __forceinline__ void publish_half(RecStage& st, const HitList& hl, uint32_t tests)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    float v[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) v[k] = k < kMaxHits ? hl.h[k < kMaxHits ? k : 0] : __builtin_inff();
+    st.q[0][lane] = make_float4(v[0], v[1], v[2], v[3]);
+    st.q[1][lane] = make_float4(v[4], v[5], v[6], v[7]);
+    st.q[2][lane] = make_float4(v[8], v[9], v[10], v[11]);
+    st.q[3][lane] = make_float4(__uint_as_float(hl.n), __uint_as_float(tests), 0.0f, 0.0f);
+}
+
+__device__ __forceinline__ void merge_half(const RecStage& other, HitList& hl, uint32_t& tests)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const float4 a = other.q[0][lane], b = other.q[1][lane], c = other.q[2][lane], d = other.q[3][lane];
+    const float v[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    const uint32_t n1 = __float_as_uint(d.x), n0 = hl.n;
+#pragma unroll
+    for (int k = 0; k < kMaxHits; ++k) hl.push_if((uint32_t)k < n1, v[k]);
+    hl.n = n0 + n1;                                // past the list: the overflow fix-up recomputes the ray
+    tests += wave_uniform(__float_as_uint(d.y));
+}
+
 template <bool kSigned>
 __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restrict__ recs,
                                             const float4* __restrict__ culls, const RenderParams& p,
                                             const Outputs& out, const BinBuffers& bins, uint32_t n_glob,
-                                            uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand)
+                                            uint32_t slot, uint32_t tile, WaveStats& ws, uint32_t& cand,
+                                            uint32_t split = kSplitNone, const RecStage* partner = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63u;
     // the slot's count (k_prep) and description (host): two scalar loads in flight together
@@ -1836,7 +1878,10 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
     const size_t o = out.packed ? (size_t)slot * kPackBlock + ((tile >> 2) * 8u + (lane >> 3)) * kRegion +
                                       (tile & 3u) * 8u + (lane & 7u)
                                 : (size_t)(row - p.row_begin) * p.width + col;
-    if (!tile_live) return;
+    if (!tile_live) {
+        if (split != kSplitNone) __syncthreads();  // the pair's one barrier (workgroup-uniform count)
+        return;
+    }
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
@@ -1884,14 +1929,17 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
         }
 #pragma unroll
         for (uint32_t r = 0; r < kRoundSlots; ++r) {
-            unsigned long long mm = m[r];
-            if (!mm) continue;
+            if (!m[r]) continue;
+            // a split tile's half takes every other lane's survivor
+            unsigned long long mm = split == kSplitNone ? m[r]
+                                  : m[r] & (split == kSplitHalf0 ? 0x5555555555555555ull : 0xAAAAAAAAAAAAAAAAull);
             // the survivors' records into the wave's stage (DMA, no registers)
-            stage_survivor_records(st, recs, (mm >> lane) & 1ull, id[r]);
+            if (mm) stage_survivor_records(st, recs, (mm >> lane) & 1ull, id[r]);
             if (!have_ray) {                       // under the records' DMA
                 make_ray_from(*out.frame, pre_v, pre_u, dx, dy, dz, sx, sy, sz);
                 have_ray = true;
             }
+            if (!mm) continue;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's records have landed
             tests += (uint32_t)__popcll(mm);
             while (mm) {
@@ -1903,6 +1951,14 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
                 else
                     test_staged_one(st, b, dx, dy, dz, hl);
             }
+        }
+    }
+    if constexpr (!kSigned) {
+        if (split != kSplitNone) {
+            if (split == kSplitHalf1) publish_half(st, hl, tests);
+            __syncthreads();                       // the pair's one barrier
+            if (split == kSplitHalf1) return;      // half 0 finishes the tile
+            if (have_ray) merge_half(*partner, hl, tests);
         }
     }
     ws.tile_tests += tests;
@@ -1982,15 +2038,17 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     __shared__ RecStage st[kTileWaves];            // one private stage per wave
     const uint64_t t_start = block_start_stamp();
     const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
+    const uint32_t split_slots = kSigned || !kCanSplit ? 0u : bins.split_slots;
+    const uint32_t tile_end = tile_blocks + split_slots * kBlocksPerRegion;   // the tile regions' workgroups
     const uint32_t wave = wave_in_block();
     const uint32_t n_glob = as_const(bs)->global_count;
     WaveStats ws = {};
     uint32_t cand = 0;
-    if (!kSigned && blockIdx.x >= tile_blocks) {   // a planned-empty region (workgroup-uniform)
-        const uint32_t slot = bins.tile_slots + (blockIdx.x - tile_blocks);
-        // statistics records: kBlocksPerRegion per wave, after the tile waves'
+    if (!kSigned && blockIdx.x >= tile_end) {      // a planned-empty region (workgroup-uniform)
+        const uint32_t slot = bins.tile_slots + (blockIdx.x - tile_end);
+        // statistics records: kBlocksPerRegion per wave, after the tile waves' (16 per region)
         const uint32_t rec0 =
-            tile_blocks * kTileWaves + ((blockIdx.x - tile_blocks) * kTileWaves + wave) * kBlocksPerRegion;
+            tile_blocks * kTileWaves + ((blockIdx.x - tile_end) * kTileWaves + wave) * kBlocksPerRegion;
         fill_region_rows(p, out, bins, slot, wave, ws);    // (packed layout: counts only)
         store_wave_stats(ws, 0u, out.block_stats, rec0, out.wave_times, t_start, kBlocksPerRegion);
         if ((threadIdx.x & 63u) == 0u) {
@@ -2002,20 +2060,138 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8).  Within
     // each run of 8 regions, give XCD x all workgroups of region x, so a region's
     // candidate list and triangle records are cached by one L2 instead of four.
-    // A bijection on full runs of the tile workgroups; the tail keeps the identity.
-    constexpr uint32_t kPerXcd = kBlocksPerRegion;                   // one region per XCD per run
-    constexpr uint32_t kRun = 8u * kPerXcd;
-    uint32_t blk = blockIdx.x;
-    if (blk < (tile_blocks / kRun) * kRun) {
-        const uint32_t within = blk % kRun;
-        blk = (blk - within) + (within & 7u) * kPerXcd + (within >> 3);
+    // A bijection on full runs of a segment's workgroups (the split regions',
+    // then the other tile regions'); a segment's tail keeps the identity.
+    auto xcd_remap = [](uint32_t b, uint32_t n_blocks, uint32_t per_region) {
+        const uint32_t run = 8u * per_region;                        // one region per XCD per run
+        if (b < (n_blocks / run) * run) {
+            const uint32_t within = b % run;
+            b = (b - within) + (within & 7u) * per_region + (within >> 3);
+        }
+        return b;
+    };
+    // Split regions first (BinBuffers::split_slots, heaviest first): two waves
+    // per tile, 2 * kBlocksPerRegion workgroups a region.
+    const uint32_t split_blocks = split_slots * 2u * kBlocksPerRegion;
+    if (!kSigned && blockIdx.x < split_blocks) {                     // workgroup-uniform
+        const uint32_t blk = xcd_remap(blockIdx.x, split_blocks, 2u * kBlocksPerRegion);
+        const uint32_t g = blk * kTileWaves + wave;                  // wave of the split segment
+        const uint32_t slot = g / (2u * kWavesPerRegion);
+        const uint32_t tile = (g / 2u) % kWavesPerRegion;
+        const uint32_t half = g & 1u;
+        render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand,
+                             half ? kSplitHalf1 : kSplitHalf0, &st[kCanSplit ? wave ^ 1u : wave]);
+        if (!half)                                 // one record per tile (the region's 16), by half 0
+            store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, slot * kWavesPerRegion + tile,
+                             out.wave_times, t_start);
+        return;
     }
-    const uint32_t g = blk * kTileWaves + wave;                      // wave of the grid
+    const uint32_t blk = split_blocks + xcd_remap(blockIdx.x - split_blocks, tile_blocks - split_blocks / 2u,
+                                                  kBlocksPerRegion);
+    const uint32_t g = (blk - split_blocks / 2u) * kTileWaves + wave; // wave of the grid (16 per region)
     const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
     render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
+}
+
+// ---------------------------------------------------------------------------
+// k_reduce_stats: a render's statistics records (one per tile wave / workgroup)
+// and their timing records summed on the device for xrt_read_stats, so the
+// host reads one 80-B record instead of copying every record back (1.2 MB at
+// 2048^2, 32 MB at 8192^2).  Blocks stride over the records and leave their
+// partial sums in `partial`; the last block to finish (a device-scope counter,
+// reset by that block) adds them and the set's BinState into `out`.  The
+// kernel span is the latest end minus the earliest start, as 32-bit tick
+// differences from the first record's start (records_span_ms on the host).
+// ---------------------------------------------------------------------------
+struct StatsSum {
+    unsigned long long rays, hit_rays, odd_rays, overflow_rays, hits, tile_tests, candidates;
+    unsigned int max_hits;
+    int span_lo, span_hi;          // ticks relative to the first record's start
+    unsigned int global_count, overflow;
+    unsigned int pad;
+};
+static_assert(sizeof(StatsSum) == 80, "StatsSum layout");
+constexpr uint32_t kReduceThreads = 256;
+constexpr uint32_t kReduceMaxBlocks = 256;
+
+__global__ __launch_bounds__(kReduceThreads) void k_reduce_stats(const BlockStats* __restrict__ recs,
+                                                               const uint2* __restrict__ times, uint32_t n,
+                                                               const BinState* __restrict__ bs,
+                                                               StatsSum* __restrict__ partial,
+                                                               unsigned int* __restrict__ done, StatsSum* __restrict__ out)
+{
+    __shared__ StatsSum s_part[kReduceThreads / 64];
+    __shared__ bool s_last;
+    StatsSum a = {};
+    a.span_lo = 0x7FFFFFFF;
+    a.span_hi = -0x7FFFFFFF - 1;
+    const uint32_t ref = times && n ? times[0].x : 0u;
+    for (uint32_t i = blockIdx.x * kReduceThreads + threadIdx.x; i < n; i += gridDim.x * kReduceThreads) {
+        const BlockStats b = recs[i];
+        a.rays += b.rays;
+        a.hit_rays += b.hit_rays;
+        a.odd_rays += b.odd_rays;
+        a.overflow_rays += b.overflow_rays;
+        a.hits += b.hits;
+        a.tile_tests += b.tile_tests;
+        a.candidates += b.candidates;
+        a.max_hits = max(a.max_hits, b.max_hits);
+        if (times) {
+            const uint2 t = times[i];
+            a.span_lo = min(a.span_lo, (int)(t.x - ref));
+            a.span_hi = max(a.span_hi, (int)(t.y - ref));
+        }
+    }
+    auto combine = [](StatsSum& x, const StatsSum& y) {
+        x.rays += y.rays;
+        x.hit_rays += y.hit_rays;
+        x.odd_rays += y.odd_rays;
+        x.overflow_rays += y.overflow_rays;
+        x.hits += y.hits;
+        x.tile_tests += y.tile_tests;
+        x.candidates += y.candidates;
+        x.max_hits = max(x.max_hits, y.max_hits);
+        x.span_lo = min(x.span_lo, y.span_lo);
+        x.span_hi = max(x.span_hi, y.span_hi);
+    };
+    // wave, then block
+    for (int off = 32; off > 0; off >>= 1) {
+        StatsSum o;
+        o.rays = __shfl_xor(a.rays, off);
+        o.hit_rays = __shfl_xor(a.hit_rays, off);
+        o.odd_rays = __shfl_xor(a.odd_rays, off);
+        o.overflow_rays = __shfl_xor(a.overflow_rays, off);
+        o.hits = __shfl_xor(a.hits, off);
+        o.tile_tests = __shfl_xor(a.tile_tests, off);
+        o.candidates = __shfl_xor(a.candidates, off);
+        o.max_hits = __shfl_xor(a.max_hits, off);
+        o.span_lo = __shfl_xor(a.span_lo, off);
+        o.span_hi = __shfl_xor(a.span_hi, off);
+        combine(a, o);
+    }
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (lane == 0) s_part[wave] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < kReduceThreads / 64; ++w) combine(a, s_part[w]);
+        partial[blockIdx.x] = a;
+        __threadfence();
+        s_last = atomicAdd(done, 1u) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    StatsSum t = partial[0];
+    for (uint32_t b = 1; b < gridDim.x; ++b) combine(t, partial[b]);
+    t.global_count = bs ? bs->global_count : 0u;
+    t.overflow = bs ? bs->overflow : 0u;
+    t.pad = 0u;
+    *out = t;
+    __threadfence();
+    *done = 0u;                                    // for the next reduction
 }
 
 // ---------------------------------------------------------------------------

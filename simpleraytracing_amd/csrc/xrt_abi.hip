@@ -59,6 +59,12 @@ constexpr size_t kLdsGranule = 512;
 constexpr size_t kRenderLdsPerCu = (size_t)XRT_RENDER_WAVES * 4 * kRenderLdsPerWave;
 static_assert(kRenderLdsPerCu < kLdsPerCu, "the render's stages fit a CU at full occupancy");
 constexpr size_t kPrepLds = (kLdsPerCu - kRenderLdsPerCu) / XRT_PREP_PER_CU / kLdsGranule * kLdsGranule;
+// Regions of at least this many candidates render each tile with two waves
+// (DESIGN.md "Split tiles"); XRT_SPLIT_MIN overrides it, 0 turns it off.
+#ifndef XRT_SPLIT_MIN_DEFAULT
+#define XRT_SPLIT_MIN_DEFAULT 64
+#endif
+constexpr uint32_t kSplitMinDefault = XRT_SPLIT_MIN_DEFAULT;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
@@ -81,7 +87,7 @@ static_assert(kAheadFrames + 2 <= (size_t)kFrameSets, "sets for the renders in f
 // it launches the render, and for the completion event of the render that
 // last used the set before it prepares into the set again.
 constexpr uint32_t kDirtyAll = 0xFFFFFFFFu;
-constexpr int kHostCallFields = 10;    // xrt_debug_host_call_ms
+constexpr int kHostCallFields = 13;    // xrt_debug_host_call_ms
 
 struct FrameSet {
     TriRec* recs = nullptr;        // per-render records
@@ -199,6 +205,11 @@ struct xrt_context {
     // (tests of the exact fallback).
     int fill_plan = 1;
     uint32_t plan_tile_slots = 0;
+    // the plan's heaviest regions render each tile with two waves (BinBuffers::
+    // split_slots): the leading tile slots whose candidate count is at least
+    // split_min (XRT_SPLIT_MIN; 0 = never)
+    uint32_t plan_split_slots = 0;
+    uint32_t split_min = kSplitMinDefault;
     bool plan_valid = false;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
     uint64_t packed_cap = 0;           // xrt_set_transit_layout: the packed L-buffer's floats (0: row-major)
@@ -210,13 +221,21 @@ struct xrt_context {
     size_t stage_cap = 0;
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    // xrt_read_stats: the last render's records summed on the device
+    // (k_reduce_stats) into one record, read through pinned memory
+    StatsSum* d_stats_partial = nullptr;   // [kReduceMaxBlocks]
+    unsigned int* d_stats_done = nullptr;  // the last-block counter (reset by that block)
+    StatsSum* d_stats_out = nullptr;
+    StatsSum* h_stats = nullptr;           // pinned
     // host time of the last host-buffer call (xrt_render_rows), ms:
     // [0] device planes, [1] enqueue (preparation, sizing, launch), [2] wait for
     // the render, [3..5] D2H of image / L-buffer / u8, [6] statistics, [7] total;
     // within them: [8] every hipMalloc of the call, [9] a new geometry's list
-    // sizing (count read-back, layout upload)
+    // sizing (count read-back, layout upload), [10] device synchronisations
+    // before a launch layout's upload, [11] host waits for k_prep, [12] kernel
+    // launches (k_prep and render)
     double host_call_ms[kHostCallFields] = {};
-    double alloc_ms = 0.0, sizing_ms = 0.0;          // running sums ([8], [9])
+    double acc_ms[5] = {};                           // running sums of [8..12]
     // region timing (xrt_timing_begin/end)
     bool timing = false;
     std::vector<hipEvent_t> tev;      // pairs: [2i] start, [2i+1] stop of a sampled render dispatch
@@ -345,7 +364,7 @@ int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
     size_t n = std::max<size_t>(need_elems, 1);
     const auto t = HostClock::now();
     XRT_HIP(ctx, hipMalloc(&ptr, n * sizeof(T)));
-    if (ctx) ctx->alloc_ms += std::chrono::duration<double, std::milli>(HostClock::now() - t).count();
+    if (ctx) ctx->acc_ms[0] += std::chrono::duration<double, std::milli>(HostClock::now() - t).count();
     cap = n;
     return XRT_OK;
 }
@@ -515,6 +534,7 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
+    ctx->acc_ms[4] += std::chrono::duration<double, std::milli>(HostClock::now() - t_launch).count();
     if (ctx->host_profile) ctx->hp_lprep += seconds_since(t_launch);
     return XRT_OK;
 }
@@ -592,7 +612,9 @@ int upload_layout(xrt_context* ctx, SlotLayout& L, uint32_t rx, uint32_t ry, std
         desc[s] = SlotDesc{base[s], cap[s], (r % rx) | ((r / rx) << 16), 0u};
         rank[r] = (uint32_t)s;
     }
+    const auto t_sync = HostClock::now();
     XRT_HIP(ctx, hipDeviceSynchronize());
+    ctx->acc_ms[2] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sync).count();
     int rc;
     if ((rc = ensure(ctx, L.d_desc, L.desc_cap, n))) return rc;
     if ((rc = ensure(ctx, L.d_rank, L.rank_cap, n))) return rc;
@@ -630,6 +652,7 @@ void use_compact(xrt_context* ctx, uint32_t n_regions, BinBuffers& bins, bool fi
     bins.desc = ctx->compact_layout.d_desc;
     bins.rank = ctx->compact_layout.d_rank;
     bins.tile_slots = fill && ctx->plan_valid ? ctx->plan_tile_slots : n_regions;
+    bins.split_slots = fill && ctx->plan_valid && kCanSplit ? ctx->plan_split_slots : 0u;
 }
 
 // Arms the k_prep check of a frame whose region lists or fill plan k_prep's
@@ -808,13 +831,16 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // candidate count, heaviest first (their long tiles start first instead
         // of setting the tail: render 2048^2 -6 %, 1024^2 -10 %).
         std::vector<uint32_t> slot_region = fixed_region;
-        uint32_t tile_slots = n_regions;
+        uint32_t tile_slots = n_regions, split_slots = 0;
         const int plan = ctx->fill_plan;
         if (plan != 0 && st.global_count == 0u && !ctx->moving) {
             std::vector<uint32_t> full, empty;
             for (uint32_t r : fixed_region) (count_of[r] != 0u && plan != 2 ? full : empty).push_back(r);
             std::stable_sort(full.begin(), full.end(), [&](uint32_t a, uint32_t b) { return count_of[a] > count_of[b]; });
             tile_slots = (uint32_t)full.size();
+            // the heaviest regions (the first slots): two waves per tile
+            while (ctx->split_min && split_slots < tile_slots && count_of[full[split_slots]] >= ctx->split_min)
+                ++split_slots;
             full.insert(full.end(), empty.begin(), empty.end());
             slot_region.swap(full);
         }
@@ -830,8 +856,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
         if ((rc = upload_layout(ctx, ctx->compact_layout, rx, ry, std::move(slot_region), base, cap))) return rc;
-        ctx->sizing_ms += std::chrono::duration<double, std::milli>(HostClock::now() - t_sizing).count();
+        ctx->acc_ms[1] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sizing).count();
         ctx->plan_tile_slots = tile_slots;
+        ctx->plan_split_slots = split_slots;
         ctx->plan_valid = tile_slots < n_regions;
         ctx->slot_pool = run;
         ctx->compact = true;
@@ -847,7 +874,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
     // one workgroup per region of the fill plan
     const dim3 grid = kernel == XRT_KERNEL_BRUTE ? dim3((cam->width + 15) / 16, (rows + 15) / 16)
-                    : binned ? dim3(kWavesPerRegion / kTileWaves * bins.tile_slots + (n_regions - bins.tile_slots))
+                    : binned ? dim3(kWavesPerRegion / kTileWaves * (bins.tile_slots + bins.split_slots) +
+                                    (n_regions - bins.tile_slots))
                              : dim3(rx, ry);
     // stats records: one per workgroup; BINNED one per tile wave, 16 per fill region
     const uint32_t n_blocks = !rows ? 0u : binned ? kWavesPerRegion * n_regions : grid.x * grid.y;
@@ -931,6 +959,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     if (pf.prep_done && pf.host_wait) {
         const auto t = HostClock::now();
         XRT_HIP(ctx, hipEventSynchronize(pf.prep_done));
+        ctx->acc_ms[3] += std::chrono::duration<double, std::milli>(HostClock::now() - t).count();
         ++ctx->hp_host_waits;
         if (ctx->host_profile) ctx->hp_prep += seconds_since(t);
     } else if (pf.prep_done) {
@@ -950,7 +979,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         // the next frame re-sizes its lists.
         ++(fs.plan_flag[1] != 0u ? ctx->hp_overflow : ctx->hp_plan_miss);
         bins.tile_slots = rx * ry;
-        grid = dim3(kWavesPerRegion / kTileWaves * bins.tile_slots);
+        grid = dim3(kWavesPerRegion / kTileWaves * (bins.tile_slots + bins.split_slots));
         ctx->bin_key_valid = false;
     }
     ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
@@ -1003,6 +1032,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
             hipExtLaunchKernelGGL(sgn ? k_render_binned<true> : k_render_binned<false>, grid, dim3(64 * kTileWaves),
                                   0, stream, t0, t1, 0, fs.recs, fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
+        ctx->acc_ms[4] += std::chrono::duration<double, std::milli>(HostClock::now() - t_launch).count();
         if (ctx->host_profile) ctx->hp_lrender += seconds_since(t_launch);
         fs.done_ev = t1;
         fs.done_valid = true;
@@ -1118,6 +1148,7 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
+    if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
     // The prep stream at the default queue priority: frames are prepared ahead
     // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess;
@@ -1127,6 +1158,11 @@ int xrt_create(int device, xrt_context** out)
     // k_prep's own LDS must fit the cap (else more than XRT_PREP_PER_CU would not fit beside the render)
     ok = ok && prep_attr.sharedSizeBytes <= kPrepLds;
     ctx->prep_lds = ok ? kPrepLds - prep_attr.sharedSizeBytes : 0;
+    ok = ok && hipMalloc(&ctx->d_stats_partial, kReduceMaxBlocks * sizeof(StatsSum)) == hipSuccess &&
+         hipMalloc(&ctx->d_stats_done, sizeof(unsigned int)) == hipSuccess &&
+         hipMemset(ctx->d_stats_done, 0, sizeof(unsigned int)) == hipSuccess &&
+         hipMalloc(&ctx->d_stats_out, sizeof(StatsSum)) == hipSuccess &&
+         hipHostMalloc((void**)&ctx->h_stats, sizeof(StatsSum), hipHostMallocDefault) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
              hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
@@ -1182,6 +1218,10 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_lbuffer);
     (void)hipFree(ctx->d_u8);
+    (void)hipFree(ctx->d_stats_partial);
+    (void)hipFree(ctx->d_stats_done);
+    (void)hipFree(ctx->d_stats_out);
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     for (auto& c : ctx->tchunks) (void)hipFree(c.p);
     if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
@@ -1507,7 +1547,7 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     return XRT_OK;
 }
 
-int xrt_debug_host_call_ms(xrt_context* ctx, double ms[10])
+int xrt_debug_host_call_ms(xrt_context* ctx, double ms[13])
 {
     if (!ctx || !ms) return XRT_ERR_ARGUMENT;
     std::copy(ctx->host_call_ms, ctx->host_call_ms + kHostCallFields, ms);
@@ -1581,45 +1621,42 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
 {
     if (!ctx || !stats) return XRT_ERR_ARGUMENT;
     XRT_HIP(ctx, hipSetDevice(ctx->device));
-    if (ctx->pending) {
-        XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
-        ctx->pending = false;
-    }
-    // The last render's per-workgroup (per-wave) records, summed here.
     std::memset(stats, 0, sizeof *stats);
-    const FrameSet* fs = ctx->last_set;
-    if (fs && fs->rendered_blocks) {
-        std::vector<BlockStats> rec(fs->rendered_blocks);
-        XRT_HIP(ctx, hipMemcpy(rec.data(), fs->block_stats, rec.size() * sizeof(BlockStats),
-                               hipMemcpyDeviceToHost));
-        for (const BlockStats& b : rec) {
-            stats->rays += b.rays;
-            stats->hit_rays += b.hit_rays;
-            stats->odd_rays += b.odd_rays;
-            stats->overflow_rays += b.overflow_rays;
-            stats->hits += b.hits;
-            stats->tile_tests += b.tile_tests;
-            stats->candidates += b.candidates;
-            stats->max_hits = std::max(stats->max_hits, b.max_hits);
-        }
-    }
-    stats->global_triangles = 0;
-    double ms = 0.0;
-    if (fs && fs->rendered_blocks && fs->last_times) {    // where the set's last render stored its records
-        std::vector<uint2> t(fs->rendered_blocks);
-        XRT_HIP(ctx, hipMemcpy(t.data(), fs->last_times, t.size() * sizeof(uint2), hipMemcpyDeviceToHost));
-        ms = records_span_ms(t);
-    }
     stats->kernel = (uint32_t)ctx->last_kernel;
-    stats->kernel_ms = ms;
-    if (fs && fs->binned && fs->last_state) {
-        BinState bs = {};
-        XRT_HIP(ctx, hipMemcpy(&bs, fs->last_state, sizeof bs, hipMemcpyDeviceToHost));
-        stats->global_triangles = bs.global_count;
-        if (bs.overflow && !ctx->bin_force_cap) {  // the next frame re-sizes its lists
-            ctx->bin_key_valid = false;
-            ++ctx->state_gen;
-        }
+    const FrameSet* fs = ctx->last_set;
+    if (!fs || !fs->rendered_blocks) {
+        if (ctx->pending) XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+        ctx->pending = false;
+        return XRT_OK;
+    }
+    // The last render's records (and where its timing records went, and its
+    // BinState) summed on the device behind the render, on its stream: one
+    // record comes back instead of every wave's.
+    const uint32_t n = fs->rendered_blocks;
+    const hipStream_t s = ctx->last_stream;
+    const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>(kReduceMaxBlocks, (n + 4 * kReduceThreads - 1) /
+                                                                                          (4 * kReduceThreads)));
+    hipLaunchKernelGGL(k_reduce_stats, dim3(blocks), dim3(kReduceThreads), 0, s, fs->block_stats, fs->last_times, n,
+                       fs->binned ? (const BinState*)fs->last_state : nullptr, ctx->d_stats_partial, ctx->d_stats_done,
+                       ctx->d_stats_out);
+    XRT_HIP(ctx, hipGetLastError());
+    XRT_HIP(ctx, hipMemcpyAsync(ctx->h_stats, ctx->d_stats_out, sizeof(StatsSum), hipMemcpyDeviceToHost, s));
+    XRT_HIP(ctx, hipStreamSynchronize(s));
+    ctx->pending = false;
+    const StatsSum& t = *ctx->h_stats;
+    stats->rays = t.rays;
+    stats->hit_rays = t.hit_rays;
+    stats->odd_rays = t.odd_rays;
+    stats->overflow_rays = t.overflow_rays;
+    stats->hits = t.hits;
+    stats->tile_tests = t.tile_tests;
+    stats->candidates = t.candidates;
+    stats->max_hits = t.max_hits;
+    stats->kernel_ms = fs->last_times && t.span_hi > t.span_lo ? (double)(t.span_hi - t.span_lo) / kTicksPerMs : 0.0;
+    stats->global_triangles = fs->binned ? t.global_count : 0u;
+    if (fs->binned && t.overflow && !ctx->bin_force_cap) {   // the next frame re-sizes its lists
+        ctx->bin_key_valid = false;
+        ++ctx->state_gen;
     }
     return XRT_OK;
 }
@@ -1719,7 +1756,8 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
     };
     auto t = t0;
     std::fill(hc, hc + kHostCallFields, 0.0);
-    const double alloc0 = ctx->alloc_ms, sizing0 = ctx->sizing_ms;
+    double acc0[5];
+    std::copy(ctx->acc_ms, ctx->acc_ms + 5, acc0);
     const size_t n = (size_t)(row_end - row_begin) * camera->width;
     size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
     if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
@@ -1746,8 +1784,7 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
     rc = xrt_read_stats(ctx, stats ? stats : &local);
     lap(6, t);
     hc[7] = std::chrono::duration<double, std::milli>(t - t0).count();
-    hc[8] = ctx->alloc_ms - alloc0;
-    hc[9] = ctx->sizing_ms - sizing0;
+    for (int k = 0; k < 5; ++k) hc[8 + k] = ctx->acc_ms[k] - acc0[k];
     return rc;
 }
 

@@ -654,6 +654,40 @@ def test_two_timed_regions_keep_their_spans(ctx, dragon):
     assert max(means[:2]) < 1.5 * min(means[:2]), means
 
 
+@pytest.mark.parametrize("split_min,W,H,r0,r1,cap", [(1, 2048, 2048, 0, None, 0), (1, 1000, 700, 100, 650, 0),
+                                                    (1, 512, 512, 0, None, 2), (1, 512, 512, 0, None, 5),
+                                                    (64, 1024, 1024, 0, None, 0), (0, 1024, 1024, 0, None, 0)])
+def test_split_tiles_exact(dragon, monkeypatch, split_min, W, H, r0, r1, cap):
+    """Split tiles (DESIGN.md "Split tiles"): the plan's heaviest regions render
+    each tile with two waves that test alternate survivors, and half 0 merges
+    half 1's sorted hit list into its own.  XRT_SPLIT_MIN=1 splits every
+    non-empty region; with the hit list capped at 2 or 5 entries the merged
+    counts pass the cap and take the exact fix-up.  Every frame (the sizing
+    frame and a later one) equals the brute-force render bit for bit, with the
+    same statistics."""
+    monkeypatch.setenv("XRT_SPLIT_MIN", str(split_min))
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.Context(0) as b:
+        b.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        b.upload_mesh(dragon)
+        if cap:
+            b.set_hit_capacity(cap)
+        ref = b.render_rows(cam, r0, r1)
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        if cap:
+            c.set_hit_capacity(cap)
+        for frame in range(2):
+            got = c.render_rows(cam, r0, r1)
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y)), (split_min, frame)
+            for f in ("rays", "hit_rays", "odd_rays", "hits", "max_hits", "overflow_rays"):
+                assert getattr(got[3], f) == getattr(ref[3], f), (split_min, frame, f)
+    if cap:
+        assert ref[3].overflow_rays > 0
+
+
 def test_tiled_mesh_1m_parity(ctx, dragon):
     """1,120,434-triangle tiled dragon: tiled == brute at 256^2, rows vs oracle."""
     big = tiled_mesh(dragon, 7)
@@ -752,7 +786,10 @@ def test_prepared_ahead_frames_exact(dragon, W, H, r0, r1, kernel):
         for x, y in zip(planes, ref[:3]):
             assert np.array_equal(bits(x.cpu().numpy()), bits(y)), (i, step)
     assert st.hit_rays == refs["A"][3].hit_rays and st.odd_rays == refs["A"][3].odd_rays
-    assert pc["ahead_used"] >= 8 and pc["ahead_dropped"] >= 4 and pc["no_wait"] > 0, pc
+    assert pc["ahead_used"] >= 8 and pc["ahead_dropped"] >= 4, pc
+    # whether a frame's preparation is complete at its launch is a race with the
+    # host; at 192^2 (TILED) the host can outrun every one of them
+    assert pc["no_wait"] > 0 or kernel == xrt.XRT_KERNEL_TILED, pc
 
 
 def test_pipelined_frames_without_sync(ctx, dragon):
