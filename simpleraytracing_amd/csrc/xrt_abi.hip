@@ -62,7 +62,7 @@ constexpr size_t kPrepLds = (kLdsPerCu - kRenderLdsPerCu) / XRT_PREP_PER_CU / kL
 // Regions of at least this many candidates render each tile with two waves
 // (DESIGN.md "Split tiles"); XRT_SPLIT_MIN overrides it, 0 turns it off.
 #ifndef XRT_SPLIT_MIN_DEFAULT
-#define XRT_SPLIT_MIN_DEFAULT 64
+#define XRT_SPLIT_MIN_DEFAULT 0
 #endif
 constexpr uint32_t kSplitMinDefault = XRT_SPLIT_MIN_DEFAULT;
 // A camera that stays put this many frames over lists sized for another
