@@ -1280,11 +1280,19 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
                                      (float)(ymax + sy));
                 // Regions the loosened triangle can touch, by its size rather than
                 // its box (a sliver's box is far larger): area / 32^2 + perimeter / 32
-                // + the corners' cells (bin_rect's global-list choice).
-                const double area = 0.5 * fabs((vx[1] - vx[0]) * (vy[2] - vy[0]) - (vx[2] - vx[0]) * (vy[1] - vy[0]));
+                // + the corners' cells (bin_rect's global-list choice).  Only its part
+                // inside the image rectangle [-1, W] x [-1, H] can touch a region, and
+                // that convex part has neither more area nor more perimeter than
+                // either set: an edge-on sliver whose loosened triangle runs far past
+                // the image (1.12 M-triangle frame at 8192^2: 44 of them) is walked
+                // over its box's cells, not put on every region's list.
+                const double iw = cp.width + 2.0, ih = cp.height + 2.0;
+                const double area = fmin(0.5 * fabs((vx[1] - vx[0]) * (vy[2] - vy[0]) - (vx[2] - vx[0]) * (vy[1] - vy[0])),
+                                         iw * ih);
                 double perim = 0.0;
                 for (int q = 0; q < 3; ++q)
                     perim += sqrt((vx[pj[q]] - vx[q]) * (vx[pj[q]] - vx[q]) + (vy[pj[q]] - vy[q]) * (vy[pj[q]] - vy[q]));
+                perim = fmin(perim, 2.0 * (iw + ih));
                 c.e2.w = (float)(area / (kRegion * kRegion) + 2.0 * perim / kRegion + 8.0);
             }
         } else {
