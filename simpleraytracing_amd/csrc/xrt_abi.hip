@@ -369,6 +369,21 @@ int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
     return XRT_OK;
 }
 
+// Waits for this context's own work: its preparations (prep stream), every
+// render still marked in flight (the sets' completion events) and the last
+// enqueue's stream (a statistics reduction behind the render).  Not the whole
+// device: other contexts' and the caller's unrelated work are not this
+// context's to wait for (a device-wide synchronise measured 21 ms once, in a
+// process whose device was otherwise idle).
+int sync_context(xrt_context* ctx)
+{
+    XRT_HIP(ctx, hipStreamSynchronize(ctx->prep_stream));
+    for (FrameSet& fs : ctx->sets)
+        if (fs.done_valid) XRT_HIP(ctx, hipEventSynchronize(fs.done_ev));
+    if (ctx->pending) XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+    return XRT_OK;
+}
+
 // The reference's stdmin / stdmax semantics (std::min(a,b) = b<a ? b : a).
 inline float stdmin(float a, float b) { return (b < a) ? b : a; }
 inline float stdmax(float a, float b) { return (a < b) ? b : a; }
@@ -613,9 +628,9 @@ int upload_layout(xrt_context* ctx, SlotLayout& L, uint32_t rx, uint32_t ry, std
         rank[r] = (uint32_t)s;
     }
     const auto t_sync = HostClock::now();
-    XRT_HIP(ctx, hipDeviceSynchronize());
+    int rc = sync_context(ctx);
+    if (rc) return rc;
     ctx->acc_ms[2] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sync).count();
-    int rc;
     if ((rc = ensure(ctx, L.d_desc, L.desc_cap, n))) return rc;
     if ((rc = ensure(ctx, L.d_rank, L.rank_cap, n))) return rc;
     XRT_HIP(ctx, hipMemcpy(L.d_desc, desc.data(), n * sizeof(SlotDesc), hipMemcpyHostToDevice));
@@ -1165,7 +1180,8 @@ int xrt_create(int device, xrt_context** out)
          hipHostMalloc((void**)&ctx->h_stats, sizeof(StatsSum), hipHostMallocDefault) == hipSuccess;
     for (FrameSet& fs : ctx->sets)     // dispatch-attached events need timing enabled
         ok = ok && hipMalloc(&fs.frame, sizeof(RenderParams)) == hipSuccess &&
-             hipEventCreate(&fs.ready) == hipSuccess && hipEventCreate(&fs.done) == hipSuccess &&
+             hipEventCreate(&fs.ready) == hipSuccess &&
+             hipEventCreate(&fs.done) == hipSuccess &&
              hipHostMalloc((void**)&fs.plan_flag, 2 * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
     if (!ok) {
         xrt_destroy(ctx);
@@ -1193,8 +1209,7 @@ void xrt_destroy(xrt_context* ctx)
                      (unsigned long long)ctx->hp_overflow, (unsigned long long)ctx->hp_ahead_used,
                      (unsigned long long)ctx->hp_ahead_dropped, (unsigned long long)ctx->hp_launch_nowait);
     (void)hipSetDevice(ctx->device);
-    if (ctx->pending && ctx->last_stream) (void)hipStreamSynchronize(ctx->last_stream);
-    (void)hipDeviceSynchronize();
+    (void)sync_context(ctx);
     (void)hipFree(ctx->d_tris);
     for (FrameSet& fs : ctx->sets) {
         (void)hipFree(fs.recs);
@@ -1240,8 +1255,9 @@ int xrt_upload_mesh(xrt_context* ctx, const float* triangles, uint64_t num_trian
     if (num_triangles && !triangles) return fail(ctx, XRT_ERR_ARGUMENT, "triangles is NULL");
     if (num_triangles > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many triangles");
     XRT_HIP(ctx, hipSetDevice(ctx->device));
-    XRT_HIP(ctx, hipDeviceSynchronize());        // frames in flight read the mesh (prep stream)
-    int rc = ensure(ctx, ctx->d_tris, ctx->tris_cap, 9 * num_triangles);
+    int rc = sync_context(ctx);                   // frames in flight read the mesh (prep stream)
+    if (rc) return rc;
+    rc = ensure(ctx, ctx->d_tris, ctx->tris_cap, 9 * num_triangles);
     if (rc) return rc;
     if (num_triangles)
         XRT_HIP(ctx, hipMemcpy(ctx->d_tris, triangles, 9 * num_triangles * sizeof(float),
@@ -1597,7 +1613,8 @@ int xrt_debug_wave_times(xrt_context* ctx, uint32_t frames_back, uint32_t* dst, 
     if (frames_back >= (uint32_t)kFrameSets)
         return fail(ctx, XRT_ERR_ARGUMENT, "frames_back must be < " + std::to_string(kFrameSets));
     XRT_HIP(ctx, hipSetDevice(ctx->device));
-    XRT_HIP(ctx, hipDeviceSynchronize());
+    int rc = sync_context(ctx);
+    if (rc) return rc;
     const FrameSet* fs = ctx->last_set
                              ? &ctx->sets[((ctx->last_set - ctx->sets) + kFrameSets - (int)frames_back) % kFrameSets]
                              : nullptr;
@@ -1692,7 +1709,7 @@ int xrt_timing_end(xrt_context* ctx, double* total_ms, uint64_t* launches)
     }
     ctx->event_ms = ev;
     ctx->event_launches = ctx->tev_used / 2;
-    XRT_HIP(ctx, hipDeviceSynchronize());          // the sampled frames' records are written
+    if (int rc = sync_context(ctx)) return rc;     // the sampled frames' records are written
     double sum = 0.0;
     std::vector<uint2> t;
     for (const auto& smp : ctx->tsamples) {
@@ -1854,7 +1871,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     XRT_HIP(ctx, hipSetDevice(ctx->device));
     const uint64_t T = ctx->num_tris;
     if (!T) return XRT_OK;
-    XRT_HIP(ctx, hipDeviceSynchronize());        // no frame in flight uses the set
+    if ((rc = sync_context(ctx))) return rc;      // no frame in flight uses the set
     FrameSet& fs = ctx->sets[ctx->next_set];
     if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
     if ((rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
