@@ -59,12 +59,17 @@ constexpr size_t kLdsGranule = 512;
 constexpr size_t kRenderLdsPerCu = (size_t)XRT_RENDER_WAVES * 4 * kRenderLdsPerWave;
 static_assert(kRenderLdsPerCu < kLdsPerCu, "the render's stages fit a CU at full occupancy");
 constexpr size_t kPrepLds = (kLdsPerCu - kRenderLdsPerCu) / XRT_PREP_PER_CU / kLdsGranule * kLdsGranule;
-// Regions of at least this many candidates render each tile with two waves
-// (DESIGN.md "Split tiles"); XRT_SPLIT_MIN overrides it, 0 turns it off.
-#ifndef XRT_SPLIT_MIN_DEFAULT
-#define XRT_SPLIT_MIN_DEFAULT 0
-#endif
-constexpr uint32_t kSplitMinDefault = XRT_SPLIT_MIN_DEFAULT;
+// Split tiles (DESIGN.md "Split tiles"): in a frame whose tile waves are at
+// most kSplitFillFactor x the GPU's wave slots (its span is its heaviest tiles'),
+// the regions with at least kSplitHeavyFrac of the heaviest region's candidates
+// (and at least kSplitFloor) render each tile with two waves.  Larger frames
+// split nothing (their heavy regions start first and others cover the tail).
+// XRT_SPLIT_MIN=n instead splits every region of at least n candidates in any
+// frame (0: never).
+constexpr double kSplitFillFactor = 2.0;
+constexpr double kSplitHeavyFrac = 0.6;
+constexpr uint32_t kSplitFloor = 64;
+constexpr uint32_t kSplitAuto = 0xFFFFFFFFu;
 // A camera that stays put this many frames over lists sized for another
 // camera is sized for itself.
 constexpr uint32_t kStillFrames = 2;
@@ -209,7 +214,8 @@ struct xrt_context {
     // split_slots): the leading tile slots whose candidate count is at least
     // split_min (XRT_SPLIT_MIN; 0 = never)
     uint32_t plan_split_slots = 0;
-    uint32_t split_min = kSplitMinDefault;
+    uint32_t split_min = kSplitAuto;   // kSplitAuto: the rule above
+    uint32_t wave_slots = 0;           // the device's CUs x 32 (render waves resident at full occupancy)
     bool plan_valid = false;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
     uint64_t packed_cap = 0;           // xrt_set_transit_layout: the packed L-buffer's floats (0: row-major)
@@ -854,7 +860,14 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
             std::stable_sort(full.begin(), full.end(), [&](uint32_t a, uint32_t b) { return count_of[a] > count_of[b]; });
             tile_slots = (uint32_t)full.size();
             // the heaviest regions (the first slots): two waves per tile
-            while (ctx->split_min && split_slots < tile_slots && count_of[full[split_slots]] >= ctx->split_min)
+            uint32_t split_min = ctx->split_min;
+            if (split_min == kSplitAuto) {
+                const bool small = (double)tile_slots * kWavesPerRegion <= kSplitFillFactor * ctx->wave_slots;
+                const uint32_t heaviest = tile_slots ? count_of[full[0]] : 0u;
+                split_min = small ? std::max<uint32_t>(kSplitFloor, (uint32_t)std::ceil(kSplitHeavyFrac * heaviest))
+                                  : 0u;
+            }
+            while (split_min && split_slots < tile_slots && count_of[full[split_slots]] >= split_min)
                 ++split_slots;
             full.insert(full.end(), empty.begin(), empty.end());
             slot_region.swap(full);
@@ -1164,6 +1177,10 @@ int xrt_create(int device, xrt_context** out)
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
+    ctx->wave_slots = (uint32_t)n_cu * 32u;
     // The prep stream at the default queue priority: frames are prepared ahead
     // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess;

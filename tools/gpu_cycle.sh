@@ -6,8 +6,9 @@
 # gpurun_out/cycle.  Usage: tools/gpu_cycle.sh [PATTERN] [CONFIG...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/cycle
+OUT=gpurun_out/cycle/${CYCLE_TAG:-run}_$(date +%H%M%S)_$$
 mkdir -p $OUT
+echo "[cycle] outputs in $OUT"
 export TMPDIR=/tmp
 PAT="${1:-all}"
 shift
@@ -27,6 +28,6 @@ for cfg in "${CFGS[@]}"; do
     XRT_LIB=$lib timeout -k 10 240 python bench.py --no-cpu-baseline $cfg > $OUT/b_$i.json 2> $OUT/b_$i.err
     rc=$?
     if [ $rc -ne 0 ]; then tail -5 $OUT/b_$i.err; exit $rc; fi
-    python3 -c "import json; d=json.load(open('$OUT/b_$i.json')); r=d['roofline']; l=d['latency']; print('%-6s'%'$name', '%-36s'%'$cfg'[:36], 'Mrays/s %7.0f'%d['value'], 'step %.4f'%d['ms_per_step'], 'span %.4f'%r['avg_kernel_ms'], 'e2e %.2f'%l.get('end_to_end_ms', -1), 'r+d2h %.2f'%l.get('render_and_d2h_ms', -1), 'tests/ray %.2f'%d['render_stats']['ray_triangle_tests_per_ray'])"
+    python3 -c "import json; d=json.load(open('$OUT/b_$i.json')); r=d['roofline']; l=d['latency']; print('%-6s'%'$name', '%-36s'%'$cfg'[:36], 'Mrays/s %7.0f'%d['value'], 'step %.4f'%d['ms_per_step'], 'span %.4f'%r['avg_kernel_ms'], 'e2e %.2f'%l.get('end_to_end_ms', -1), 'r+d2h %.2f'%l.get('render_and_d2h_ms', -1), 'tests/ray %.2f'%d['render_stats']['ray_triangle_tests_per_ray']); b=l.get('render_and_d2h_breakdown_ms', {}); print('       slow host call:', {k: v for k, v in b.items() if v > 1.0}, 'camera %.2f'%l.get('camera_ms', 0)) if l.get('render_and_d2h_ms', 0) > 10 else None"
   done
 done
