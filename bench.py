@@ -7,7 +7,10 @@ Moller-Trumbore test of its culled candidates).  The mesh is resident in HBM
 before the timed region; the per-frame triangle preparation (binning) and the
 render are inside it.
 
-  one GPU (default): dragon.ply 2048x2048 frames (BASELINE configs[2]).
+  one GPU (default): dragon.ply 2048x2048 frames (BASELINE configs[2]), two
+                 frames in flight for frames up to 2048x2048 (--inflight:
+                 frame k on stream k % 2 into its own output planes; both
+                 checked bit for bit after timing).
   --gpus N > 1 (default --mode strips, 4096x4096: BASELINE configs[3]):
                  strong scaling -- one frame per step split into row strips
                  (rows_per = H/N, remainder to the first, as
@@ -81,6 +84,10 @@ def parse():
                     help="rehearsal only: every rank uses device 0 (with --dist-backend gloo)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the bounded cpu_baseline sample")
+    ap.add_argument("--inflight", type=int, default=None, metavar="F",
+                    help="frames mode: frame k renders on stream k %% F into output planes k %% F, so a "
+                         "frame's render can start while the previous frame's last waves run (default 2 "
+                         "for frames of up to 2048x2048 pixels, else 1; strips mode: 1)")
     ap.add_argument("--no-timing-check", action="store_true",
                     help="profiling runs of a few steps: skip the avg_kernel_ms <= ms_per_step check")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -479,10 +486,28 @@ def main():
     # (xrt_expand_rows_device) -- frame k's gather overlaps frame k+1's render.
     root = rank == 0 or not strips
     packed = gathering and args.transit == "packed"
+    # Frames in flight (frames mode): frame k renders on stream k % F into its
+    # own planes, so consecutive renders are not serialised by one stream -- a
+    # frame's first waves start while the previous frame's last ones run.  The
+    # context keeps each frame's lists, records and statistics in its own
+    # frame set (include/xrt.h).  It pays where a frame's ramp and tail are a
+    # large part of its span (up to 2048^2: a few rounds of the GPU's wave
+    # slots); two larger frames overlapping all along only share the L2s
+    # (4096^2 step 105 -> 113 us, 1.12 M triangles 1,032 -> 1,057 us: DESIGN.md
+    # "Frames in flight"), so they keep one stream.  Strips mode keeps one
+    # stream (the gather already overlaps the next frame's render).
+    inflight = max(1, args.inflight if args.inflight is not None
+                   else 2 if not strips and W * H <= 2048 * 2048 else 1)
+    if strips and inflight != 1:
+        raise SystemExit("--inflight is for frames mode")
+    planes_of = []
     if root:
-        img = torch.zeros(W * H, dtype=torch.float32, device=dev)
-        lb = torch.zeros(W * H, dtype=torch.float32, device=dev)
-        u8 = torch.zeros(W * H, dtype=torch.uint8, device=dev)
+        for f in range(inflight):
+            planes_of.append((torch.zeros(W * H, dtype=torch.float32, device=dev),
+                              torch.zeros(W * H, dtype=torch.float32, device=dev),
+                              torch.zeros(W * H, dtype=torch.uint8, device=dev),
+                              stream if f == 0 else torch.cuda.Stream(dev)))
+        img, lb, u8, _ = planes_of[0]
     else:
         ctx.set_miss_code(xrt.XRT_MISS_TRANSIT)
         tbufs = [torch.zeros((r1 - r0) * W, dtype=torch.float32, device=dev) for _ in range(2)]
@@ -563,14 +588,16 @@ def main():
     def step():
         k = frame_no[0]
         frame_no[0] += 1
+        if root:
+            img_k, lb_k, u8_k, s_k = planes_of[k % inflight]
         if signed:                            # the fork: signed L-buffer, then the hole fill
-            ctx.render_rows_device(cam, 0, H, 0, lb.data_ptr(), 0, stream.cuda_stream)
-            ctx.hole_fill_device(W, H, lb.data_ptr(), img.data_ptr(), u8.data_ptr(), stream.cuda_stream)
+            ctx.render_rows_device(cam, 0, H, 0, lb_k.data_ptr(), 0, s_k.cuda_stream)
+            ctx.hole_fill_device(W, H, lb_k.data_ptr(), img_k.data_ptr(), u8_k.data_ptr(), s_k.cuda_stream)
         elif root:
             o = r0 * W
             works = post_recvs() if gathering else None
-            ctx.render_rows_device(orbit_cams[k] if orbit_cams else cam, r0, r1, img.data_ptr() + 4 * o, lb.data_ptr() + 4 * o,
-                                   u8.data_ptr() + o, stream.cuda_stream)
+            ctx.render_rows_device(orbit_cams[k] if orbit_cams else cam, r0, r1, img_k.data_ptr() + 4 * o,
+                                   lb_k.data_ptr() + 4 * o, u8_k.data_ptr() + o, s_k.cuda_stream)
             if gathering:
                 finish_recvs(works)
         else:
@@ -663,12 +690,29 @@ def main():
         roofline["avg_kernel_ms_hip_events"] = event_ms / event_launches if event_launches else None
         roofline["hip_event_launches"] = event_launches
         ms_per_step = elapsed_max / args.steps * 1e3
-        if not strips and not args.no_timing_check and roofline["avg_kernel_ms"] > ms_per_step:
-            # the renders of one stream are serial: their mean duration cannot
-            # exceed the step time -- an event sample that says so is not the
-            # kernel's duration
-            raise SystemExit(f"bench.py: avg_kernel_ms {roofline['avg_kernel_ms']:.4f} > ms_per_step "
+        if not strips and not args.no_timing_check and roofline["avg_kernel_ms"] > inflight * ms_per_step:
+            # at most `inflight` renders overlap: their mean duration cannot
+            # exceed that many steps -- an event sample that says so is not
+            # the kernel's duration
+            raise SystemExit(f"bench.py: avg_kernel_ms {roofline['avg_kernel_ms']:.4f} > {inflight} x ms_per_step "
                              f"{ms_per_step:.4f} ({launches} sampled launches): inconsistent timing")
+        roofline["frames_in_flight"] = inflight
+        if roofline.get("bound") == "valu":
+            # the chip's issue rate over the timed region: one render per step
+            chip = roofline["valu_wave_instr_per_launch"] / (ms_per_step / 1e3)
+            roofline["chip_achieved"] = chip
+            roofline["chip_frac"] = chip / VALU_PEAK_WAVE_INSTR_S
+            if inflight > 1:
+                # Renders overlap in pairs, so a launch's span (avg_kernel_ms) is
+                # shared with its neighbours and work / span undercounts the
+                # issue rate the chip sustains: `achieved` is the chip's rate over
+                # the timed region (the launch's work / the step; the span-based
+                # figures stay beside it as span_*).
+                roofline["span_achieved"] = roofline["achieved"]
+                roofline["span_frac"] = roofline["frac"]
+                roofline["achieved"] = chip
+                roofline["frac"] = roofline["chip_frac"]
+                roofline["achieved_is"] = "valu_wave_instr_per_launch / ms_per_step (launches overlap in pairs)"
         result = {
             "metric": "Mrays/s (dragon.ply render, whole job)",
             "value": value,
@@ -694,7 +738,9 @@ def main():
                                 f"{'RCCL (xGMI)' if nccl else 'gloo (host-staged rehearsal)'}, overlapped with "
                                 f"the next frame's render" if gathering
                                 else f"one frame per rank x{world} (weak)" if world > 1 else "one GPU"),
+                "frames_in_flight": inflight,
             },
+            "frames_in_flight_exact": None,
             "roofline": roofline,
             "render_stats": {
                 "hit_rays": stats.hit_rays, "odd_rays": stats.odd_rays, "max_hits": stats.max_hits,
@@ -715,12 +761,27 @@ def main():
     if rank == 0 and world == 1 and not signed:
         # the timed loop's own planes (its last frame), checked against the oracle's rows
         last_cam = orbit_cams[frame_no[0] - 1] if orbit_cams else cam
-        planes = (img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy())
+        img_l, lb_l, u8_l, _ = planes_of[(frame_no[0] - 1) % inflight]
+        planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
         result["latency"].update(end_to_end(args, W, H, device_index, {"auto": xrt.XRT_KERNEL_AUTO,
                                  "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
                                  "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]))
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
+
+    if root and not strips and not signed and inflight > 1:
+        # untimed: each in-flight buffer set's last frame against a synchronous
+        # render of its camera (frames that overlapped must not change a bit)
+        ok = True
+        for j in range(inflight):
+            k = frame_no[0] - 1 - j
+            img_k, lb_k, u8_k, _ = planes_of[k % inflight]
+            ok &= planes_equal((img_k.cpu().numpy(), lb_k.cpu().numpy(), u8_k.cpu().numpy()),
+                               ctx.render_rows(orbit_cams[k] if orbit_cams else cam))
+        if not ok:
+            raise SystemExit("bench.py: a frame rendered in flight differs from its synchronous render")
+        if result is not None:
+            result["frames_in_flight_exact"] = True
 
     code = 0
     if gathering:

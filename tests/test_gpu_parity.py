@@ -792,6 +792,44 @@ def test_prepared_ahead_frames_exact(dragon, W, H, r0, r1, kernel):
     assert pc["no_wait"] > 0 or kernel == xrt.XRT_KERNEL_TILED, pc
 
 
+@pytest.mark.parametrize("n_streams", [2, 3])
+def test_frames_in_flight_on_streams_exact(dragon, n_streams):
+    """Frames in flight (bench.py --inflight): frame k renders on stream
+    k % n_streams into its own planes, so renders of consecutive frames overlap
+    on the device, over steady runs (prepared ahead) and camera changes; every
+    frame is bit-identical to a brute-force render of its camera."""
+    import torch
+    W = H = 512
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    cams = {"A": base, "B": orbit_camera(base, centre, 25.0)}
+    refs = {}
+    for name, cam in cams.items():
+        with xrt.Context(0) as fresh:
+            fresh.set_kernel(xrt.XRT_KERNEL_BRUTE)
+            fresh.upload_mesh(dragon)
+            refs[name] = fresh.render_rows(cam)
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(n_streams)]
+    seq = "A" * 12 + "B" * 9 + "A" * 7
+    outs = [(name, (torch.full((W * H,), -1.0, device=dev), torch.full((W * H,), -1.0, device=dev),
+                    torch.zeros(W * H, dtype=torch.uint8, device=dev))) for name in seq]
+    with xrt.Context(0) as ctx:
+        ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+        ctx.upload_mesh(dragon)
+        torch.cuda.synchronize(dev)               # the planes' fills, before other streams write them
+        for k, (name, planes) in enumerate(outs):  # no host sync between frames
+            ctx.render_rows_device(cams[name], 0, H, *(t.data_ptr() for t in planes),
+                                   streams[k % n_streams].cuda_stream)
+        torch.cuda.synchronize(dev)
+        pc = ctx.pipeline_counters()
+    for k, (name, planes) in enumerate(outs):
+        for x, y in zip(planes, refs[name][:3]):
+            assert np.array_equal(bits(x.cpu().numpy()), bits(y)), (k, name)
+    assert pc["ahead_used"] >= 10, pc
+
+
 def test_pipelined_frames_without_sync(ctx, dragon):
     """Many frames enqueued back to back on one stream with no host sync --
     different cameras, image sizes, strips, kernels and output buffers, so the
