@@ -88,6 +88,10 @@ def parse():
                     help="frames mode: frame k renders on stream k %% F into output planes k %% F, so a "
                          "frame's render can start while the previous frame's last waves run (default 2 "
                          "for frames of up to 2048x2048 pixels, else 1; strips mode: 1)")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the end-to-end latency windows (a child process; profiling runs)")
+    ap.add_argument("--e2e-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--e2e-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-timing-check", action="store_true",
                     help="profiling runs of a few steps: skip the avg_kernel_ms <= ms_per_step check")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -387,8 +391,41 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
     return r
 
 
+def end_to_end_isolated(args, W, H, device_index):
+    """end_to_end() in a child process of its own (bench.py --e2e-only): the
+    fresh contexts it times then share the device with nothing the timed loop
+    left behind (its streams, frame sets and buffers).  The child warms HIP up
+    first (a throwaway context renders a 64x64 frame), as this process was."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--e2e-device", str(device_index),
+           "--size", str(W), str(H), "--mesh", args.mesh, "--tile-mesh", str(args.tile_mesh),
+           "--kernel", args.kernel]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError(f"end-to-end child failed ({r.returncode}): {r.stderr[-2000:]}")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["process"] = "a child process of its own (HIP warmed by a 64x64 frame of a throwaway context)"
+    return out
+
+
+def e2e_only(args) -> int:
+    import simpleraytracing_amd as xrt
+    kernel = {"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
+              "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]
+    tris = xrt.load_ply(args.mesh)
+    with xrt.Context(args.e2e_device) as warm:      # HIP init, code objects, first launches
+        warm.set_kernel(kernel)
+        warm.upload_mesh(tris)
+        warm.render_rows(xrt.camera_for_mesh(tris, 64, 64))
+    W, H = args.size
+    print(json.dumps(end_to_end(args, W, H, args.e2e_device, kernel)), flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.e2e_only:
+        return e2e_only(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -763,9 +800,8 @@ def main():
         last_cam = orbit_cams[frame_no[0] - 1] if orbit_cams else cam
         img_l, lb_l, u8_l, _ = planes_of[(frame_no[0] - 1) % inflight]
         planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
-        result["latency"].update(end_to_end(args, W, H, device_index, {"auto": xrt.XRT_KERNEL_AUTO,
-                                 "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
-                                 "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]))
+        if not args.no_latency:
+            result["latency"].update(end_to_end_isolated(args, W, H, device_index))
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
 

@@ -15,7 +15,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --t
  && timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
  && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver.json 2> $OUT/bench_driver.err \
  && timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench_200.json 2> $OUT/bench_200.err \
- && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 > $OUT/trace_bench.json 2> $OUT/trace.err
+ && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline --no-latency --steps 50 --warmup 5 > $OUT/trace_bench.json 2> $OUT/trace.err
 rc=$?
 tail -3 $OUT/pytest_gpu.log
 cat $OUT/smoke.log $OUT/bench_driver.json $OUT/bench_200.json 2>/dev/null | cut -c1-600

@@ -14,7 +14,7 @@ CFGS=("$@")
 i=0
 for cfg in "${CFGS[@]}"; do
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl_$i -o run -- python3 bench.py --no-cpu-baseline --steps 40 --warmup 5 $cfg > $OUT/bench_$i.json 2> $OUT/tl_$i.err || exit 1
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl_$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --steps 40 --warmup 5 $cfg > $OUT/bench_$i.json 2> $OUT/tl_$i.err || exit 1
   f=$(find $OUT/tl_$i -name "*kernel_trace.csv" | head -1)
   python3 tools/render_timeline.py "$f" > $OUT/timeline_$i.txt || exit 1
   echo "== $cfg"
