@@ -337,12 +337,13 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
     region-list entries) and the counter-measured HBM bytes.  The brute-force
     definition of SURVEY 8(d) (36 B per ray-triangle test) only gives the work
     avoided by the cull, `work_avoided_x`."""
-    traffic = valu = None
+    traffic = traffic_low = valu = None
     try:
         with open(args.traffic_json) as f:
             tr = json.load(f).get(f"{kernel}:{workload}")
         if tr:
             traffic = tr.get("hbm_bytes_per_launch")
+            traffic_low = tr.get("hbm_bytes_per_launch_low")
             valu = tr.get("valu_wave_instr_per_launch")
     except (OSError, ValueError):
         pass
@@ -366,6 +367,9 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
         "avg_kernel_ms": avg_kernel_s * 1e3,
         "launches": launches,
         "traffic": traffic,
+        # FETCH_SIZE x 1 + WRITE_SIZE: the counters' lower reading (the render's
+        # record gathers are counted at full size, its contiguous reads at half)
+        "traffic_low": traffic_low,
         "hbm_bound": "hbm",
         "hbm_achieved": hbm_rate,
         "hbm_peak": HBM_PEAK_GBS,

@@ -6,7 +6,12 @@
 KEY is bench.py's "<kernel>:<workload>" (e.g. "binned:dragon.ply 2048x2048").
 HBM bytes per launch = FETCH_SIZE x 2 (gfx950 reports half of the bytes of a
 wide streaming read: MI355X_MICROARCH.md, HBM section) + WRITE_SIZE, both in KB
-per dispatch; the VALU instruction count per launch is SQ_INSTS_VALU."""
+per dispatch; the VALU instruction count per launch is SQ_INSTS_VALU.  The x 2
+holds for contiguous reads (the region entries); a 64-B gather through an index
+(the survivors' records) is counted at its full size
+(tools/probes/fetch_calib.hip, profiles/r04e/fetch_calib.txt), so the true
+bytes lie between hbm_bytes_per_launch_low (FETCH_SIZE x 1 + WRITE_SIZE) and
+hbm_bytes_per_launch."""
 import json
 import os
 import sys
@@ -25,6 +30,8 @@ data[key] = {
     "fetch_kb_per_launch": row.get("FETCH_SIZE"),
     "write_kb_per_launch": row.get("WRITE_SIZE"),
     "hbm_bytes_per_launch": (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
+    if "FETCH_SIZE" in row and "WRITE_SIZE" in row else None,
+    "hbm_bytes_per_launch_low": (row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
     if "FETCH_SIZE" in row and "WRITE_SIZE" in row else None,
     "valu_wave_instr_per_launch": row.get("SQ_INSTS_VALU"),
     "salu_instr_per_launch": row.get("SQ_INSTS_SALU"),
