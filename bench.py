@@ -395,6 +395,19 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
     return r
 
 
+def frames_in_flight(requested, strips: bool, W: int, H: int) -> int:
+    """Frames in flight of a run (main(): frame k on stream k % F): the
+    requested count, else 2 for frames of up to 2048^2 pixels and 1 above or in
+    strips mode (DESIGN.md "Pipelining")."""
+    if requested is not None:
+        if requested < 1:
+            raise SystemExit("--inflight must be at least 1")
+        if strips and requested != 1:
+            raise SystemExit("--inflight is for frames mode")
+        return requested
+    return 2 if not strips and W * H <= 2048 * 2048 else 1
+
+
 def end_to_end_isolated(args, W, H, device_index):
     """end_to_end() in a child process of its own (bench.py --e2e-only): the
     fresh contexts it times then share the device with nothing the timed loop
@@ -537,10 +550,7 @@ def main():
     # (4096^2 step 105 -> 113 us, 1.12 M triangles 1,032 -> 1,057 us: DESIGN.md
     # "Frames in flight"), so they keep one stream.  Strips mode keeps one
     # stream (the gather already overlaps the next frame's render).
-    inflight = max(1, args.inflight if args.inflight is not None
-                   else 2 if not strips and W * H <= 2048 * 2048 else 1)
-    if strips and inflight != 1:
-        raise SystemExit("--inflight is for frames mode")
+    inflight = frames_in_flight(args.inflight, strips, W, H)
     planes_of = []
     if root:
         for f in range(inflight):

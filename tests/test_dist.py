@@ -220,6 +220,24 @@ def test_wrong_gathered_strip_fails_every_rank(corrupt):
         assert "not bit-exact" in out
 
 
+def test_frames_in_flight_rule():
+    """bench.frames_in_flight: two frames in flight up to 2048^2 in frames mode,
+    one above it and in strips mode; an explicit count wins, but strips mode
+    takes only 1 and no count below 1 is accepted."""
+    import bench
+    assert bench.frames_in_flight(None, False, 2048, 2048) == 2
+    assert bench.frames_in_flight(None, False, 1024, 1024) == 2
+    assert bench.frames_in_flight(None, False, 4096, 4096) == 1
+    assert bench.frames_in_flight(None, False, 8192, 8192) == 1
+    assert bench.frames_in_flight(None, True, 2048, 2048) == 1
+    assert bench.frames_in_flight(3, False, 4096, 4096) == 3
+    assert bench.frames_in_flight(1, True, 4096, 4096) == 1
+    with pytest.raises(SystemExit):
+        bench.frames_in_flight(2, True, 4096, 4096)
+    with pytest.raises(SystemExit):
+        bench.frames_in_flight(0, False, 2048, 2048)
+
+
 def test_bench_exits_nonzero_on_rank_exception():
     """bench.run(): an exception in main() leaves through os._exit(1) after its
     traceback (no hang in a collective or RCCL teardown)."""
