@@ -10,7 +10,10 @@ render are inside it.
   one GPU (default): dragon.ply 2048x2048 frames (BASELINE configs[2]), two
                  frames in flight for frames up to 2048x2048 (--inflight:
                  frame k on stream k % 2 into its own output planes; both
-                 checked bit for bit after timing).
+                 checked bit for bit after timing).  Before the timed
+                 region: the first frame, W warm-up steps, min(K, 20) steps
+                 timed cold (before_clock_ramp) and --ramp-ms of untimed
+                 steps, so the K timed steps run at the GPU's loaded clocks.
   --gpus N > 1 (default --mode strips, 4096x4096: BASELINE configs[3]):
                  strong scaling -- one frame per step split into row strips
                  (rows_per = H/N, remainder to the first, as
@@ -90,6 +93,10 @@ def parse():
                          "for frames of up to 2048x2048 pixels, else 1; strips mode: 1)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the end-to-end latency windows (a child process; profiling runs)")
+    ap.add_argument("--ramp-ms", type=float, default=100.0,
+                    help="untimed frames for this long after the warm-up, so the timed region runs at the "
+                         "GPU's loaded clocks (0: none); the first min(K, 20) frames after the warm-up are "
+                         "timed before it and reported as before_clock_ramp")
     ap.add_argument("--e2e-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-timing-check", action="store_true",
@@ -647,7 +654,8 @@ def main():
         elif root:
             o = r0 * W
             works = post_recvs() if gathering else None
-            ctx.render_rows_device(orbit_cams[k] if orbit_cams else cam, r0, r1, img_k.data_ptr() + 4 * o,
+            ctx.render_rows_device(orbit_cams[k % len(orbit_cams)] if orbit_cams else cam, r0, r1,
+                                   img_k.data_ptr() + 4 * o,
                                    lb_k.data_ptr() + 4 * o, u8_k.data_ptr() + o, s_k.cuda_stream)
             if gathering:
                 finish_recvs(works)
@@ -678,6 +686,34 @@ def main():
     for _ in range(max(args.warmup - 1, 0)):
         step()
     torch.cuda.synchronize(dev)
+    # Clock ramp (DESIGN.md "Measurement"): an idle GPU runs at low clocks and
+    # needs ~30 ms of sustained load to reach its steady rate (2048^2: ~38 us per
+    # frame at first, 29.5 us after ~1,000 frames; an idle gap of 20 ms drops it
+    # back).  The first min(K, 20) frames after the warm-up are timed as they
+    # are (`before_clock_ramp`), then untimed frames keep the GPU loaded for
+    # --ramp-ms before the timed region.  The count is agreed over ranks (a
+    # strips run exchanges data every frame).
+    cold = None
+    ramp_frames = 0
+    if args.ramp_ms > 0:
+        n_cold = min(args.steps, 20)
+        t_c = time.perf_counter()
+        for _ in range(n_cold):
+            step()
+        torch.cuda.synchronize(dev)
+        per_step = (time.perf_counter() - t_c) / n_cold
+        cold = {"steps": n_cold, "ms_per_step": per_step * 1e3}
+        if world > 1:
+            t_ps = torch.tensor([per_step], dtype=torch.float64, device=dev if nccl else "cpu")
+            dist.all_reduce(t_ps, op=dist.ReduceOp.MAX)
+            per_step = float(t_ps.item())
+        ramp_frames = int(min(20000, max(0.0, args.ramp_ms / 1e3 / max(per_step, 1e-7))))
+        t_r = time.perf_counter()
+        for _ in range(ramp_frames):
+            step()
+        torch.cuda.synchronize(dev)
+        cold["ramp_frames"] = ramp_frames
+        cold["ramp_ms"] = (time.perf_counter() - t_r) * 1e3
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -801,6 +837,7 @@ def main():
                 "ray_triangle_tests_per_ray": stats.tile_tests * 64 / max(stats.rays, 1),
             },
             "python_gc_in_timed_region": gc_in_timed,
+            "before_clock_ramp": cold,
             "latency": {"first_frame_ms": first_frame_ms,
                         "first_frame": "this context's first frame: k_prep, the synchronous list sizing, "
                                        "k_prep again and the render (device planes, synchronised)"},
@@ -811,7 +848,7 @@ def main():
 
     if rank == 0 and world == 1 and not signed:
         # the timed loop's own planes (its last frame), checked against the oracle's rows
-        last_cam = orbit_cams[frame_no[0] - 1] if orbit_cams else cam
+        last_cam = orbit_cams[(frame_no[0] - 1) % len(orbit_cams)] if orbit_cams else cam
         img_l, lb_l, u8_l, _ = planes_of[(frame_no[0] - 1) % inflight]
         planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
         if not args.no_latency:
@@ -827,7 +864,7 @@ def main():
             k = frame_no[0] - 1 - j
             img_k, lb_k, u8_k, _ = planes_of[k % inflight]
             ok &= planes_equal((img_k.cpu().numpy(), lb_k.cpu().numpy(), u8_k.cpu().numpy()),
-                               ctx.render_rows(orbit_cams[k] if orbit_cams else cam))
+                               ctx.render_rows(orbit_cams[k % len(orbit_cams)] if orbit_cams else cam))
         if not ok:
             raise SystemExit("bench.py: a frame rendered in flight differs from its synchronous render")
         if result is not None:

@@ -31,11 +31,18 @@ constexpr uint32_t kInitialRegionCap = 256;
 // kTimingRecords of them (8 B each) per region, and put a HIP start/stop event
 // pair on the render dispatch of every kEventStride-th frame, a cross-check of
 // the in-kernel spans (a start event costs the frame a few microseconds).
-constexpr size_t kTimingRecords = (size_t)1 << 27;
+// xrt_timing_begin allocates the region's record space (one chunk of
+// kTimingRecords) and its events up front: an allocation inside the region
+// stalls the host for long enough that the GPU idles, and an idle GPU drops
+// its clocks and takes ~30 ms of load to ramp them back (DESIGN.md
+// "Measurement").  Frames past the record space are not sampled.
+constexpr size_t kTimingRecords = (size_t)1 << 25;
 // After a timed region a context keeps one chunk of at most this many bytes
-// for the next region; larger ones are freed (xrt_timing_end).
-constexpr size_t kKeptTimingBytes = (size_t)64 << 20;
+// (the region's record space) for the next region; larger ones are freed
+// (xrt_timing_end).
+constexpr size_t kKeptTimingBytes = kTimingRecords * sizeof(uint2);
 constexpr uint64_t kEventStride = 16;
+constexpr size_t kTimingEvents = 256;          // start/stop pairs created by xrt_timing_begin
 // s_memrealtime ticks per millisecond (100 MHz on gfx950)
 constexpr double kTicksPerMs = 1e5;
 // Buffer sets in rotation: frame N's preparation reuses the set of frame
@@ -1703,6 +1710,22 @@ int xrt_timing_begin(xrt_context* ctx)
     for (FrameSet& fs : ctx->sets) {
         if (fs.done_valid) XRT_HIP(ctx, hipEventSynchronize(fs.done_ev));
         fs.done_valid = false;
+    }
+    // the region's record space and events, before the region
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    bool have = false;
+    for (auto& c : ctx->tchunks) have = have || c.cap >= kTimingRecords;
+    if (!have) {
+        for (auto& c : ctx->tchunks) (void)hipFree(c.p);
+        ctx->tchunks.clear();
+        xrt_context::TimesChunk c = {nullptr, kTimingRecords, 0};
+        XRT_HIP(ctx, hipMalloc(&c.p, kTimingRecords * sizeof(uint2)));
+        ctx->tchunks.push_back(c);
+    }
+    while (ctx->tev.size() < kTimingEvents) {
+        hipEvent_t e;
+        XRT_HIP(ctx, hipEventCreate(&e));
+        ctx->tev.push_back(e);
     }
     ctx->timing = true;
     ctx->tev_used = 0;
