@@ -643,20 +643,25 @@ def main():
                     ctx.expand_rows_device((e0 - b0) * W, lb.data_ptr() + 4 * b0 * W, img.data_ptr() + 4 * b0 * W,
                                            u8.data_ptr() + b0 * W, stream.cuda_stream)
 
+    # each buffer set's device pointers (the root's rows) and stream handle,
+    # looked up once: the harness's own per-step host time stays small next to
+    # a 20-40 us frame
+    o_root = r0 * W
+    ptrs_of = [(img_f.data_ptr(), lb_f.data_ptr(), u8_f.data_ptr(), s_f.cuda_stream)
+               for img_f, lb_f, u8_f, s_f in planes_of]
+
     def step():
         k = frame_no[0]
         frame_no[0] += 1
         if root:
-            img_k, lb_k, u8_k, s_k = planes_of[k % inflight]
+            img_k, lb_k, u8_k, s_k = ptrs_of[k % inflight]
         if signed:                            # the fork: signed L-buffer, then the hole fill
-            ctx.render_rows_device(cam, 0, H, 0, lb_k.data_ptr(), 0, s_k.cuda_stream)
-            ctx.hole_fill_device(W, H, lb_k.data_ptr(), img_k.data_ptr(), u8_k.data_ptr(), s_k.cuda_stream)
+            ctx.render_rows_device(cam, 0, H, 0, lb_k, 0, s_k)
+            ctx.hole_fill_device(W, H, lb_k, img_k, u8_k, s_k)
         elif root:
-            o = r0 * W
             works = post_recvs() if gathering else None
             ctx.render_rows_device(orbit_cams[k % len(orbit_cams)] if orbit_cams else cam, r0, r1,
-                                   img_k.data_ptr() + 4 * o,
-                                   lb_k.data_ptr() + 4 * o, u8_k.data_ptr() + o, s_k.cuda_stream)
+                                   img_k + 4 * o_root, lb_k + 4 * o_root, u8_k + o_root, s_k)
             if gathering:
                 finish_recvs(works)
         else:
@@ -777,7 +782,10 @@ def main():
         roofline["avg_kernel_ms_hip_events"] = event_ms / event_launches if event_launches else None
         roofline["hip_event_launches"] = event_launches
         ms_per_step = elapsed_max / args.steps * 1e3
-        if not strips and not args.no_timing_check and roofline["avg_kernel_ms"] > inflight * ms_per_step:
+        # (frames past the record space are not sampled: a mean over the first
+        # frames may sit a little above the whole region's step)
+        slack = 1.0 if launches >= args.steps else 1.03
+        if not strips and not args.no_timing_check and roofline["avg_kernel_ms"] > slack * inflight * ms_per_step:
             # at most `inflight` renders overlap: their mean duration cannot
             # exceed that many steps -- an event sample that says so is not
             # the kernel's duration

@@ -32,11 +32,11 @@ constexpr uint32_t kInitialRegionCap = 256;
 // pair on the render dispatch of every kEventStride-th frame, a cross-check of
 // the in-kernel spans (a start event costs the frame a few microseconds).
 // xrt_timing_begin allocates the region's record space (one chunk of
-// kTimingRecords) and its events up front: an allocation inside the region
+// kTimingRecords: 1 GB, 128 frames of 8192^2) and its events up front: an allocation inside the region
 // stalls the host for long enough that the GPU idles, and an idle GPU drops
 // its clocks and takes ~30 ms of load to ramp them back (DESIGN.md
 // "Measurement").  Frames past the record space are not sampled.
-constexpr size_t kTimingRecords = (size_t)1 << 25;
+constexpr size_t kTimingRecords = (size_t)1 << 27;
 // After a timed region a context keeps one chunk of at most this many bytes
 // (the region's record space) for the next region; larger ones are freed
 // (xrt_timing_end).

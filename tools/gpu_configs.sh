@@ -36,7 +36,7 @@ for c in "${CONFIGS[@]}"; do
   i=0
   for grp in "${PASSES[@]}"; do
     i=$((i+1))
-    timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/${name}_pmc/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --no-timing-check $base $short > /dev/null 2> $OUT/${name}_pmc$i.err || exit 1
+    timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/${name}_pmc/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --ramp-ms 0 --no-timing-check $base $short > /dev/null 2> $OUT/${name}_pmc$i.err || exit 1
   done
   python3 tools/pmc_summary.py $OUT/${name}_pmc > $OUT/pmc_summary_${name}.txt || exit 1
   python3 tools/make_traffic_json.py $OUT/${name}_pmc/summary.json "binned:$key" --kernel "k_render_binned<false>" > /dev/null || exit 1

@@ -13,6 +13,6 @@ PASSES=("SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_INST_LEVEL_SMEM SQ_INST_LEVEL_VME
 i=0
 for grp in "${PASSES[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --no-timing-check --steps 8 --warmup 2 "$@" > /dev/null 2> $OUT/p$i.err || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --ramp-ms 0 --no-timing-check --steps 8 --warmup 2 "$@" > /dev/null 2> $OUT/p$i.err || exit 1
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
