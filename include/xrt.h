@@ -170,8 +170,10 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
  * repeats the previous call's frame geometry (mesh, camera, rows) and
  * settings, the preparations of the next two frames of that geometry are
  * enqueued at once; a later call that matches takes one (rendered with no
- * wait), any other call drops them.  Call xrt_read_stats() (which
- * synchronises the stream) for counters and kernel time.
+ * wait), any other call drops them.  Renders enqueued on different streams
+ * (each into its own buffers) may run at once: every frame's lists, records
+ * and statistics live in its own buffer set.  Call xrt_read_stats() (which
+ * synchronises the last frame's stream) for counters and kernel time.
  */
 int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin,
                            uint32_t row_end, float* d_image, float* d_lbuffer,
