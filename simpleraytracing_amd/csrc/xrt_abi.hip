@@ -31,16 +31,17 @@ constexpr uint32_t kInitialRegionCap = 256;
 // kTimingRecords of them (8 B each) per region, and put a HIP start/stop event
 // pair on the render dispatch of every kEventStride-th frame, a cross-check of
 // the in-kernel spans (a start event costs the frame a few microseconds).
-// xrt_timing_begin allocates the region's record space (one chunk of
-// kTimingRecords: 1 GB, 128 frames of 8192^2) and its events up front: an allocation inside the region
+// xrt_timing_begin allocates the region's record space (one chunk: room for
+// kTimingFrames frames of the context's last frame size, at most
+// kTimingRecords = 1 GB, 128 frames of 8192^2) and its events up front: an allocation inside the region
 // stalls the host for long enough that the GPU idles, and an idle GPU drops
 // its clocks and takes ~30 ms of load to ramp them back (DESIGN.md
 // "Measurement").  Frames past the record space are not sampled.
 constexpr size_t kTimingRecords = (size_t)1 << 27;
+constexpr size_t kTimingFrames = 256;
 // After a timed region a context keeps one chunk of at most this many bytes
-// (the region's record space) for the next region; larger ones are freed
-// (xrt_timing_end).
-constexpr size_t kKeptTimingBytes = kTimingRecords * sizeof(uint2);
+// for the next region; larger ones are freed (xrt_timing_end).
+constexpr size_t kKeptTimingBytes = (size_t)64 << 20;
 constexpr uint64_t kEventStride = 16;
 constexpr size_t kTimingEvents = 256;          // start/stop pairs created by xrt_timing_begin
 // s_memrealtime ticks per millisecond (100 MHz on gfx950)
@@ -255,6 +256,7 @@ struct xrt_context {
     size_t tev_used = 0;
     uint64_t timed_frames = 0;        // frames enqueued since xrt_timing_begin
     size_t timed_records = 0;         // their timing records kept
+    size_t timing_space = 0;          // records the region's chunk holds (xrt_timing_begin)
     // the sampled frames' timing records: chunks of device memory (a chunk is
     // never moved while kernels may write it), and where each frame's are
     struct TimesChunk {
@@ -1033,7 +1035,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     out.wave_times = fs.times;
     hipEvent_t t0 = nullptr, t1 = fs.done;
     const uint64_t frame_in_region = ctx->timing ? ctx->timed_frames++ : 0;
-    if (ctx->timing && rows > 0 && ctx->timed_records + fs.n_blocks <= kTimingRecords) {
+    if (ctx->timing && rows > 0 && ctx->timed_records + fs.n_blocks <= ctx->timing_space) {
         ctx->timed_records += fs.n_blocks;
         uint2* slot = nullptr;
         int rc = timing_slot(ctx, fs.n_blocks, slot);
@@ -1713,15 +1715,18 @@ int xrt_timing_begin(xrt_context* ctx)
     }
     // the region's record space and events, before the region
     XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t last_blocks = ctx->last_set ? ctx->last_set->n_blocks : 0u;
+    const size_t space = std::min(kTimingRecords, std::max<size_t>((size_t)1 << 20, kTimingFrames * last_blocks));
     bool have = false;
-    for (auto& c : ctx->tchunks) have = have || c.cap >= kTimingRecords;
+    for (auto& c : ctx->tchunks) have = have || c.cap >= space;
     if (!have) {
         for (auto& c : ctx->tchunks) (void)hipFree(c.p);
         ctx->tchunks.clear();
-        xrt_context::TimesChunk c = {nullptr, kTimingRecords, 0};
-        XRT_HIP(ctx, hipMalloc(&c.p, kTimingRecords * sizeof(uint2)));
+        xrt_context::TimesChunk c = {nullptr, space, 0};
+        XRT_HIP(ctx, hipMalloc(&c.p, space * sizeof(uint2)));
         ctx->tchunks.push_back(c);
     }
+    ctx->timing_space = space;
     while (ctx->tev.size() < kTimingEvents) {
         hipEvent_t e;
         XRT_HIP(ctx, hipEventCreate(&e));
