@@ -700,7 +700,7 @@ def main():
     # strips run exchanges data every frame).
     cold = None
     ramp_frames = 0
-    if args.ramp_ms > 0:
+    if args.ramp_ms > 0 and args.steps > 0:
         n_cold = min(args.steps, 20)
         t_c = time.perf_counter()
         for _ in range(n_cold):
