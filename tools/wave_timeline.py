@@ -23,6 +23,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, nargs=2, default=[2048, 2048])
 ap.add_argument("--tile-mesh", type=int, default=1)
 ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--inflight", type=int, default=1,
+                help="frame k on stream k %% N into its own planes (bench.py --inflight); the last four "
+                     "frames' start/end then show how consecutive renders overlap")
 a = ap.parse_args()
 import torch                                             # noqa: E402
 
@@ -32,14 +35,14 @@ if a.tile_mesh > 1:
     tris = tiled_mesh(tris, a.tile_mesh)
 cam = xrt.camera_for_mesh(tris, W, H)
 dev = torch.device("cuda", 0)
-img = torch.empty(W * H, dtype=torch.float32, device=dev)
-lb = torch.empty(W * H, dtype=torch.float32, device=dev)
-u8 = torch.empty(W * H, dtype=torch.uint8, device=dev)
-stream = torch.cuda.current_stream(dev)
+sets = [(torch.empty(W * H, dtype=torch.float32, device=dev), torch.empty(W * H, dtype=torch.float32, device=dev),
+         torch.empty(W * H, dtype=torch.uint8, device=dev),
+         torch.cuda.current_stream(dev) if f == 0 else torch.cuda.Stream(dev)) for f in range(max(1, a.inflight))]
 with xrt.Context(0) as ctx:
     ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
     ctx.upload_mesh(tris)
-    for _ in range(a.frames):
+    for k in range(a.frames):
+        img, lb, u8, stream = sets[k % len(sets)]
         ctx.render_rows_device(cam, 0, H, img.data_ptr(), lb.data_ptr(), u8.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize(dev)
     frames = [ctx.wave_times(k).astype(np.int64) for k in (3, 2, 1, 0)]   # oldest first
