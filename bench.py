@@ -11,9 +11,11 @@ render are inside it.
                  frames in flight for frames up to 2048x2048 (--inflight:
                  frame k on stream k % 2 into its own output planes; both
                  checked bit for bit after timing).  Before the timed
-                 region: the first frame, W warm-up steps, min(K, 20) steps
-                 timed cold (before_clock_ramp) and --ramp-ms of untimed
-                 steps, so the K timed steps run at the GPU's loaded clocks.
+                 region: W untimed steps (the first frame, with its list
+                 sizing, and W - 1 warm-up steps), nothing else unless
+                 --ramp-ms asks for it.  After it, --loaded-ms of untimed
+                 steps and K more timed steps give the rate at the GPU's
+                 loaded clocks (at_loaded_clocks, reported beside `value`).
   --gpus N > 1 (default --mode strips, 4096x4096: BASELINE configs[3]):
                  strong scaling -- one frame per step split into row strips
                  (rows_per = H/N, remainder to the first, as
@@ -93,10 +95,26 @@ def parse():
                          "for frames of up to 2048x2048 pixels, else 1; strips mode: 1)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the end-to-end latency windows (a child process; profiling runs)")
-    ap.add_argument("--ramp-ms", type=float, default=100.0,
-                    help="untimed frames for this long after the warm-up, so the timed region runs at the "
-                         "GPU's loaded clocks (0: none); the first min(K, 20) frames after the warm-up are "
-                         "timed before it and reported as before_clock_ramp")
+    ap.add_argument("--ramp-ms", type=float, default=0.0,
+                    help="opt-in: untimed frames for this long after the warm-up, so the timed region runs at "
+                         "the GPU's loaded clocks (default 0: the K timed steps follow the W warm-up steps "
+                         "directly); with it, the first min(K, 20) frames after the warm-up are timed before "
+                         "it and reported as before_clock_ramp")
+    ap.add_argument("--loaded-ms", type=float, default=100.0,
+                    help="after the timed region (never inside `value`): keep the GPU loaded this long, then "
+                         "time K more steps, reported beside the headline as at_loaded_clocks (0: skip)")
+    ap.add_argument("--host-loop", choices=["batch", "python"], default="batch",
+                    help="frames mode, one camera: 'batch' (default) enqueues a run of steps in one "
+                         "xrt_render_frames_device call; 'python' calls xrt_render_rows_device once per step")
+    ap.add_argument("--capi-multi", choices=["auto", "off"], default="auto",
+                    help="strips mode over N > 1 ranks: after the torch path, rank 0 also times the C ABI's own "
+                         "multi-GPU entry (xrt_render_rows_multi_device over devices 0..N-1 in ONE process, RCCL "
+                         "gather, the split of xrt_multi_set_split) in a child process, reported as capi_multi")
+    ap.add_argument("--capi-devices", default=None, metavar="LIST",
+                    help="devices of the capi_multi leg, e.g. 0,0,0,0,0,0,0,0 (one GPU listed 8 times: a one-rank "
+                         "RCCL rehearsal); runs the leg in any mode")
+    ap.add_argument("--capi-split", choices=["balanced", "equal"], default="balanced")
+    ap.add_argument("--capi-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-timing-check", action="store_true",
@@ -107,10 +125,19 @@ def parse():
 
 
 def cpu_baseline(tris, cam, W, H, budget_s, gpu_rows):
-    """The oracle (a restatement of main.cxx's serial loop, threaded over pixel
-    blocks like main-pthreads-redo.cxx) timed on a bounded row sample of the same
-    frame; also checks those rows against the planes the timed loop's last frame
-    left on the GPU."""
+    """The CPU path timed on the box's host cores, on bounded samples of the same
+    frame, each checked bit for bit against the planes the timed loop's last
+    frame left on the GPU:
+
+      kind "reference" (when oracle/_ref is built): the reference's own
+        src/Ray.cxx, Triangle.cxx and TriangleMesh.cxx (compiled unmodified,
+        -O2) driven by renderLoop's per-pixel loop (oracle/ref_harness.cpp),
+        spans of rows on every host thread over one shared mesh -- the
+        structure of main-pthreads-redo.cxx;
+      kind "port": oracle/xrt_oracle.c (the C restatement of the same loop)
+        threaded over 64-px blocks.
+
+    Half of `budget_s` each; their single-thread rates beside them."""
     import numpy as np
 
     from oracle import oracle
@@ -118,6 +145,9 @@ def cpu_baseline(tris, cam, W, H, budget_s, gpu_rows):
     threads = max(1, min(threads, 64))
     cam = np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) + [cam.pixel_spacing],
                    np.float32)                         # the oracle's 13-float camera
+    g_img, g_lb, g_u8 = (np.asarray(a).reshape(H, W) for a in gpu_rows)
+    ref = oracle.ref_lib()
+    share = budget_s / 2 if ref is not None else budget_s
     # serial rate on a span of one row (the reference main.cxx is single-threaded),
     # sized to about 1 s
     mid = H // 2
@@ -129,16 +159,15 @@ def cpu_baseline(tris, cam, W, H, budget_s, gpu_rows):
     serial_rate = span / serial_s
     # threaded sample sized to the budget
     est_rate = serial_rate * threads
-    nrows = int(max(1, min(H, budget_s * est_rate / W)))
+    nrows = int(max(1, min(H, share * est_rate / W)))
     rows = np.unique(np.linspace(0, H - 1, nrows).astype(np.uint32))
     t0 = time.perf_counter()
     img, lb, u8, nh, odd = oracle.render_row_list(tris, cam, W, H, rows, threads=threads)
     dt = time.perf_counter() - t0
-    g_img, g_lb, g_u8 = gpu_rows
-    parity = bool(np.array_equal(img.view(np.uint32), g_img.reshape(H, W)[rows].ravel().view(np.uint32))
-                  and np.array_equal(lb.view(np.uint32), g_lb.reshape(H, W)[rows].ravel().view(np.uint32))
-                  and np.array_equal(u8, g_u8.reshape(H, W)[rows].ravel()))
-    return {
+    parity = bool(np.array_equal(img.view(np.uint32), g_img[rows].ravel().view(np.uint32))
+                  and np.array_equal(lb.view(np.uint32), g_lb[rows].ravel().view(np.uint32))
+                  and np.array_equal(u8, g_u8[rows].ravel()))
+    port = {
         "value": len(rows) * W / dt / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
@@ -149,6 +178,47 @@ def cpu_baseline(tris, cam, W, H, budget_s, gpu_rows):
         "serial_sample": f"{span} rays of row {mid}, 1 thread ({serial_s:.2f} s)",
         "sample_bit_exact_vs_gpu": parity,
         "gpu_planes": "the timed loop's last frame (device planes copied back after timing)",
+    }
+    if ref is None:
+        return port
+    # the reference's own classes: serial on the same span, then every thread
+    t0 = time.perf_counter()
+    r_img, r_lb, _ = oracle.ref_render_spans(tris, cam, W, H, [mid], c0, c0 + span, threads=1)
+    r_serial_s = time.perf_counter() - t0
+    r_serial = span / r_serial_s
+    ok = (np.array_equal(r_img.view(np.uint32), g_img[mid, c0:c0 + span].reshape(1, -1).view(np.uint32))
+          and np.array_equal(r_lb.view(np.uint32), g_lb[mid, c0:c0 + span].reshape(1, -1).view(np.uint32)))
+    rays = share * r_serial * threads
+    if rays >= threads * W:                    # whole rows, spread over the frame
+        n_r, b0, b1 = int(min(H, rays // W)), 0, W
+    else:                                      # one centred span per thread
+        n_r = threads
+        w_s = int(max(8, min(W, rays // threads)))
+        b0 = (W - w_s) // 2
+        b1 = b0 + w_s
+    rrows = np.unique(np.linspace(0, H - 1, n_r).astype(np.uint32))
+    t0 = time.perf_counter()
+    r_img, r_lb, _ = oracle.ref_render_spans(tris, cam, W, H, rrows, b0, b1, threads=threads)
+    r_dt = time.perf_counter() - t0
+    ok = ok and bool(np.array_equal(r_img.view(np.uint32), g_img[rrows, b0:b1].view(np.uint32))
+                     and np.array_equal(r_lb.view(np.uint32), g_lb[rrows, b0:b1].view(np.uint32))
+                     and np.array_equal(oracle.lut_u8_array(r_img.ravel()), g_u8[rrows, b0:b1].ravel()))
+    return {
+        "value": len(rrows) * (b1 - b0) / r_dt / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "reference",
+        "sample": f"{len(rrows)} rows x columns [{b0}, {b1}) of the same {W}x{H} frame "
+                  f"({len(rrows) * (b1 - b0)} rays, {r_dt:.1f} s): the reference's src/Ray.cxx, Triangle.cxx, "
+                  f"TriangleMesh.cxx compiled unmodified (-O2, oracle/_ref) under renderLoop's per-pixel loop "
+                  f"(oracle/ref_harness.cpp), one row per task on {threads} host threads over one shared mesh "
+                  f"(main-pthreads-redo.cxx's structure)",
+        "serial_value": r_serial / 1e6,
+        "serial_sample": f"{span} rays of row {mid}, 1 thread ({r_serial_s:.2f} s)",
+        "sample_bit_exact_vs_gpu": ok,
+        "gpu_planes": port["gpu_planes"],
+        "port": {k: port[k] for k in ("value", "cores", "sample", "serial_value", "serial_sample",
+                                      "sample_bit_exact_vs_gpu")},
     }
 
 
@@ -168,7 +238,9 @@ def end_to_end(args, W, H, device_index, kernel):
         return {k: round(v, 3) for k, v in d.items()}
 
     def one_context(tris, t_load):
-        c = xrt.Context(device_index)
+        t_c = time.perf_counter()
+        c = xrt.Context(device_index)                 # streams, pinned D2H ring, copy threads
+        r = {"context_create_ms": (time.perf_counter() - t_c) * 1e3}
         try:
             c.set_kernel(kernel)
             t2 = time.perf_counter()
@@ -178,7 +250,7 @@ def end_to_end(args, W, H, device_index, kernel):
             t3c = time.perf_counter()
             planes = c.render_rows(cam)                   # host planes: render + D2H, synchronous
             t4 = time.perf_counter()
-            r = {"end_to_end_ms": (t_load + t4 - t2) * 1e3, "load_ms": t_load * 1e3,
+            r |= {"end_to_end_ms": (t_load + t4 - t2) * 1e3, "load_ms": t_load * 1e3,
                  "upload_ms": (t3 - t2) * 1e3, "camera_ms": (t3c - t3) * 1e3, "render_and_d2h_ms": (t4 - t3) * 1e3,
                  "render_and_d2h_breakdown_ms": rounded(c.host_call_ms())}
             t5 = time.perf_counter()
@@ -193,6 +265,7 @@ def end_to_end(args, W, H, device_index, kernel):
             t7 = time.perf_counter()
             c.close()
             r["context_destroy_ms"] = (time.perf_counter() - t7) * 1e3
+            r["context_destroy_breakdown_ms"] = rounded(xrt.Context.last_destroy_ms())
         return r
 
     # Python's cyclic garbage collector, not the path, can stop the harness for
@@ -377,7 +450,6 @@ def make_roofline(args, kernel, workload, stats, T, rays_per_launch, avg_kernel_
         # FETCH_SIZE x 1 + WRITE_SIZE: the counters' lower reading (the render's
         # record gathers are counted at full size, its contiguous reads at half)
         "traffic_low": traffic_low,
-        "hbm_bound": "hbm",
         "hbm_achieved": hbm_rate,
         "hbm_peak": HBM_PEAK_GBS,
         "hbm_unit": "GB/s",
@@ -446,10 +518,94 @@ def e2e_only(args) -> int:
     return 0
 
 
+def capi_multi_only(args) -> int:
+    """bench.py --capi-only: the C ABI's multi-GPU entry timed in this process --
+    one xrt_multi over --capi-devices (its own RCCL communicators from
+    ncclCommInitAll, or one rank when one device is listed n times), the strips
+    of xrt_multi_set_split, device-0 planes on one stream, W untimed frames (the
+    first plans the split and sizes the lists), then K frames timed with the
+    frames' gathers overlapping the next frames' renders; the last frame is
+    compared bit for bit with one device's render of the whole frame."""
+    import numpy as np
+    import torch
+
+    import simpleraytracing_amd as xrt
+    from simpleraytracing_amd.scenes import tiled_mesh
+    devices = [int(d) for d in args.capi_devices.split(",")]
+    kernel = {"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
+              "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]
+    tris = xrt.load_ply(args.mesh)
+    if args.tile_mesh > 1:
+        tris = tiled_mesh(tris, args.tile_mesh)
+    W, H = args.size
+    cam = xrt.camera_for_mesh(tris, W, H)
+    with xrt.Context(devices[0]) as one:
+        one.set_kernel(kernel)
+        one.upload_mesh(tris)
+        ref = one.render_rows(cam)
+    distinct = len(set(devices))
+    dev = torch.device("cuda", devices[0])
+    with xrt.MultiContext(devices) as m:
+        m.set_kernel(kernel)
+        m.upload_mesh(tris)
+        if distinct == 1 and len(devices) > 1:
+            m.set_gather(xrt.XRT_GATHER_RCCL)          # one-rank communicator: the RCCL calls on one GPU
+        m.set_split(xrt.XRT_SPLIT_BALANCED if args.capi_split == "balanced" else xrt.XRT_SPLIT_EQUAL)
+        t_p = time.perf_counter()
+        bounds, info = m.plan(cam)
+        plan_ms = (time.perf_counter() - t_p) * 1e3
+        img = torch.empty(W * H, dtype=torch.float32, device=dev)
+        lb = torch.empty(W * H, dtype=torch.float32, device=dev)
+        u8 = torch.empty(W * H, dtype=torch.uint8, device=dev)
+        s = torch.cuda.Stream(dev)
+        ptrs = (img.data_ptr(), lb.data_ptr(), u8.data_ptr(), s.cuda_stream)
+        for _ in range(max(args.warmup, 1)):
+            m.render_device(cam, *ptrs)
+        s.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            m.render_device(cam, *ptrs)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        st = m.read_stats()
+    ok = (np.array_equal(img.cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
+          and np.array_equal(lb.cpu().numpy().view(np.uint32), ref[1].view(np.uint32))
+          and np.array_equal(u8.cpu().numpy(), ref[2]))
+    out = {"entry": "xrt_render_rows_multi_device (include/xrt.h), one process",
+           "devices": devices,
+           "gather": "RCCL, one communicator per device (ncclCommInitAll)" if distinct == len(devices) and distinct > 1
+           else "RCCL, one rank (a device listed n times)" if distinct == 1 and len(devices) > 1 else "device copies",
+           "split": args.capi_split, "strips": bounds, "strip_rows": [e - b for b, e in bounds],
+           "plan": info, "plan_ms": plan_ms, "steps": args.steps, "warmup": max(args.warmup, 1),
+           "ms_per_step": dt / args.steps * 1e3, "value": W * H * args.steps / dt / 1e6, "unit": "Mrays/s",
+           "hit_rays": st.hit_rays, "bit_exact_vs_single_device_frame": bool(ok)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def capi_multi_isolated(args, W, H, devices, timeout_s=100):
+    """capi_multi_only() in a child process (bounded by timeout_s): its RCCL
+    communicators and device contexts are its own, and a failure or a hang there
+    is recorded instead of ending this rank's run."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--capi-only", "--capi-devices", ",".join(map(str, devices)),
+           "--size", str(W), str(H), "--mesh", args.mesh, "--tile-mesh", str(args.tile_mesh), "--kernel", args.kernel,
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--capi-split", args.capi_split]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s} s", "devices": devices}
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}: {r.stderr[-1500:]}", "devices": devices}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def main():
     args = parse()
     if args.e2e_only:
         return e2e_only(args)
+    if args.capi_only:
+        return capi_multi_only(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -485,6 +641,10 @@ def main():
         # (map exchange, batch_isend_irecv on rank 0 only) must not be the
         # group's first operation
         dist.barrier()
+    # host-side waits (no GPU kernel spinning on the other ranks' devices while
+    # rank 0's capi_multi leg uses them)
+    cpu_group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=DIST_TIMEOUT_S))
+                 if world > 1 and nccl else None)
 
     tris = xrt.load_ply(args.mesh)
     if args.tile_mesh > 1:
@@ -682,29 +842,47 @@ def main():
                 ctx.render_rows_device(cam, r0, r1, 0, tbufs[b].data_ptr(), 0, stream.cuda_stream)
                 pending[b] = send_strip(tbufs[b])
 
+    # Frames mode with one camera: n steps in ONE call (xrt_render_frames_device,
+    # frame k into plane set k % F on stream k % F -- every frame prepared and
+    # rendered in full, the host side of all n in one pass instead of a Python
+    # loop around one call per frame); otherwise one step() per frame.
+    batch = (args.host_loop == "batch" and root and not strips and not signed and not orbit_cams)
+
+    def run_steps(n):
+        if n <= 0:
+            return
+        if batch:
+            k0 = frame_no[0]
+            ctx.render_frames_device(cam, 0, H, n, [ptrs_of[(k0 + j) % inflight] for j in range(inflight)])
+            frame_no[0] += n
+        else:
+            for _ in range(n):
+                step()
+
     # the first frame of this context (list sizing included), then the warm-up
     torch.cuda.synchronize(dev)
     t_first = time.perf_counter()
     step()
     torch.cuda.synchronize(dev)
     first_frame_ms = (time.perf_counter() - t_first) * 1e3
-    for _ in range(max(args.warmup - 1, 0)):
-        step()
+    run_steps(max(args.warmup - 1, 0))
     torch.cuda.synchronize(dev)
     # Clock ramp (DESIGN.md "Measurement"): an idle GPU runs at low clocks and
     # needs ~30 ms of sustained load to reach its steady rate (2048^2: ~38 us per
     # frame at first, 29.5 us after ~1,000 frames; an idle gap of 20 ms drops it
-    # back).  The first min(K, 20) frames after the warm-up are timed as they
-    # are (`before_clock_ramp`), then untimed frames keep the GPU loaded for
-    # --ramp-ms before the timed region.  The count is agreed over ranks (a
-    # strips run exchanges data every frame).
+    # back).  By default the K timed steps follow the W warm-up steps directly
+    # (`value` is that rate) and the loaded-clock rate is measured after them
+    # (--loaded-ms, `at_loaded_clocks`).  Opt-in (--ramp-ms): the first min(K,
+    # 20) frames after the warm-up are timed as they are (`before_clock_ramp`),
+    # then untimed frames keep the GPU loaded for --ramp-ms before the timed
+    # region.  Frame counts are agreed over ranks (a strips run exchanges data
+    # every frame).
     cold = None
     ramp_frames = 0
     if args.ramp_ms > 0 and args.steps > 0:
         n_cold = min(args.steps, 20)
         t_c = time.perf_counter()
-        for _ in range(n_cold):
-            step()
+        run_steps(n_cold)
         torch.cuda.synchronize(dev)
         per_step = (time.perf_counter() - t_c) / n_cold
         cold = {"steps": n_cold, "ms_per_step": per_step * 1e3}
@@ -714,8 +892,7 @@ def main():
             per_step = float(t_ps.item())
         ramp_frames = int(min(20000, max(0.0, args.ramp_ms / 1e3 / max(per_step, 1e-7))))
         t_r = time.perf_counter()
-        for _ in range(ramp_frames):
-            step()
+        run_steps(ramp_frames)
         torch.cuda.synchronize(dev)
         cold["ramp_frames"] = ramp_frames
         cold["ramp_ms"] = (time.perf_counter() - t_r) * 1e3
@@ -725,8 +902,7 @@ def main():
     ctx.timing_begin()
     GC.active = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     if not root:
         for p_ in pending:
             if p_ is not None:
@@ -746,6 +922,41 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
+    untimed_before = max(args.warmup, 1) + (cold["steps"] if cold else 0) + ramp_frames
+
+    # After the timed region, never inside `value`: --loaded-ms of untimed
+    # steps, then K more timed steps -- the rate once the GPU's clocks have
+    # ramped under sustained load (DESIGN.md "Measurement").  The frame count
+    # comes from the region's max-over-ranks step, so every rank agrees.
+    loaded = None
+    if args.loaded_ms > 0 and args.steps > 0:
+        n_load = int(min(20000, max(0.0, args.loaded_ms / 1e3 / max(elapsed_max / args.steps, 1e-7))))
+        t_r = time.perf_counter()
+        run_steps(n_load)
+        torch.cuda.synchronize(dev)
+        load_ms = (time.perf_counter() - t_r) * 1e3
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t_l = time.perf_counter()
+        run_steps(args.steps)
+        if not root:
+            for p_ in pending:
+                if p_ is not None:
+                    p_.wait()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t_lt = torch.tensor([time.perf_counter() - t_l], dtype=torch.float64, device=dev if nccl else "cpu")
+        if world > 1:
+            dist.all_reduce(t_lt, op=dist.ReduceOp.MAX)
+        el = float(t_lt.item())
+        loaded = {"value": W * H * args.steps * (1 if strips else world) / el / 1e6,
+                  "ms_per_step": el / args.steps * 1e3, "steps": args.steps,
+                  "untimed_frames_before": n_load, "untimed_ms_before": load_ms,
+                  "what": "after the timed region: --loaded-ms of untimed steps keep the GPU loaded (its clocks "
+                          "ramp), then K steps timed as the region is; not the headline value"}
 
     # untimed: the gathered frame against rank 0's own render of the whole frame
     gather = None
@@ -834,6 +1045,8 @@ def main():
                                 f"the next frame's render" if gathering
                                 else f"one frame per rank x{world} (weak)" if world > 1 else "one GPU"),
                 "frames_in_flight": inflight,
+                "host_loop": ("xrt_render_frames_device: the timed steps in one call" if batch
+                              else "one xrt_render_rows_device call per step"),
             },
             "frames_in_flight_exact": None,
             "roofline": roofline,
@@ -845,7 +1058,11 @@ def main():
                 "ray_triangle_tests_per_ray": stats.tile_tests * 64 / max(stats.rays, 1),
             },
             "python_gc_in_timed_region": gc_in_timed,
+            # every frame rendered before the timed region: the first frame +
+            # the warm-up steps (+ the opt-in --ramp-ms frames and their cold sample)
+            "untimed_frames_before_timed_region": untimed_before,
             "before_clock_ramp": cold,
+            "at_loaded_clocks": loaded,
             "latency": {"first_frame_ms": first_frame_ms,
                         "first_frame": "this context's first frame: k_prep, the synchronous list sizing, "
                                        "k_prep again and the render (device planes, synchronised)"},
@@ -860,7 +1077,14 @@ def main():
         img_l, lb_l, u8_l, _ = planes_of[(frame_no[0] - 1) % inflight]
         planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
         if not args.no_latency:
-            result["latency"].update(end_to_end_isolated(args, W, H, device_index))
+            # in this process, right after the timed loop's streams and frame
+            # sets (what a drop-in caller that renders an Image after streaming
+            # device frames sees), and beside it in a child process of its own
+            kernel_id = {"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE, "tiled": xrt.XRT_KERNEL_TILED,
+                         "binned": xrt.XRT_KERNEL_BINNED}[args.kernel]
+            result["latency"].update(end_to_end(args, W, H, device_index, kernel_id))
+            result["latency"]["process"] = "the bench process, after the timed loop (its contexts still open)"
+            result["latency"]["child_process"] = end_to_end_isolated(args, W, H, device_index)
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
 
@@ -882,6 +1106,18 @@ def main():
     if gathering:
         code = gather_verdict(dist, torch, rank, bool(gather and gather["bit_exact_vs_single_device_frame"]),
                               dev if nccl else "cpu")
+    # The C ABI's own multi-GPU entry (the drop-in's renderLoopMultiGPU / xrt_main
+    # -g N path) beside the torch path: rank 0 times it in a child process over
+    # every rank's device while the other ranks wait on the host.
+    capi_devices = ([int(d) for d in args.capi_devices.split(",")] if args.capi_devices
+                    else ([device_index] * world if args.same_device else list(range(world)))
+                    if gathering and args.capi_multi == "auto" else None)
+    if capi_devices:
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            result["capi_multi"] = capi_multi_isolated(args, W, H, capi_devices)
+        if world > 1:
+            dist.barrier(group=cpu_group)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 3
+#define XRT_ABI_VERSION 4
 
 typedef enum xrt_status {
     XRT_OK = 0,
@@ -182,6 +182,35 @@ int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t 
 int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
 
 /*
+ * Many frames of one geometry (camera, rows) in one call -- a series of
+ * projections of a fixed set-up, or a throughput run.  Frame k (k = 0 ..
+ * n_frames-1) renders into plane set s = k % n_sets -- d_image[s],
+ * d_lbuffer[s], d_u8[s] (device pointers; a NULL array or entry skips that
+ * plane) -- on stream streams[s] (hipStream_t; a NULL array or entry is the
+ * default stream).  Each frame is prepared and rendered as by one
+ * xrt_render_rows_device call (its own k_prep, prepared ahead beside earlier
+ * renders; nothing is reused between frames), with the host side of all
+ * n_frames frames done in one pass: no per-frame crossing of the boundary,
+ * which at 1024^2 costs about as much host time as the GPU's frame.
+ * Asynchronous, like xrt_render_rows_device.  Replaces the caller's loop
+ * around renderLoop (src/main.cxx:237) for a batch of frames.
+ */
+int xrt_render_frames_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin, uint32_t row_end,
+                             uint32_t n_frames, uint32_t n_sets, float* const* d_image, float* const* d_lbuffer,
+                             uint8_t* const* d_u8, void* const* streams);
+
+/*
+ * The host-buffer form: n_frames frames rendered back to back into the
+ * context's device planes, then the last frame's planes copied into the host
+ * buffers (any may be NULL) as xrt_render_rows does.  *ms_per_frame (may be
+ * NULL) = host wall time from the first frame's enqueue to the last frame's
+ * completion, / n_frames.  Synchronous.
+ */
+int xrt_render_frames(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin, uint32_t row_end,
+                      uint32_t n_frames, float* image, float* lbuffer, uint8_t* image_u8, xrt_stats* stats,
+                      double* ms_per_frame);
+
+/*
  * Kernel timing over a region of many renders without host synchronisation.
  * Every render's waves store their s_memrealtime start and end beside their
  * statistics records (xrt_stats::kernel_ms is the last frame's span: last end -
@@ -268,11 +297,12 @@ int xrt_render_signed(xrt_context* ctx, const xrt_camera* camera, float* image, 
 
 /*
  * The image split into contiguous row strips over several devices, as the
- * reference's parallel drivers split the pixel index space: rows_per = H / n,
- * the remainder going to the first strips (src/main-pthreads-rows.cxx:311-334).
- * Strip g renders on devices[g]; the strips' planes are gathered into device
- * 0's frame with grouped ncclSend / ncclRecv over xGMI -- the analogue of the
- * MPI root gather of src/main-mpi.cxx:855-881 -- on one communicator per device
+ * reference's parallel drivers split the pixel index space
+ * (src/main-pthreads-rows.cxx:311-334, src/main-mpi.cxx:262-290; see
+ * xrt_multi_set_split for the two rules).  Strip g renders on devices[g]; the
+ * strips' planes are gathered into device 0's frame with grouped ncclSend /
+ * ncclRecv over xGMI -- the analogue of the MPI root gather of
+ * src/main-mpi.cxx:855-881 -- on one communicator per device
  * (ncclCommInitAll).  A device listed more than once (rehearsing the strip
  * logic on fewer GPUs) gathers with device copies instead.
  */
@@ -326,6 +356,56 @@ int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
 #define XRT_GATHER_COPY 1
 #define XRT_GATHER_RCCL 2
 int xrt_multi_set_gather(xrt_multi* m, int mode);
+
+/*
+ * How the rows are split over the devices.
+ *   XRT_SPLIT_EQUAL     rows_per = H / n, the remainder going to the first
+ *                       strips, strip g = device g in frame order -- the
+ *                       reference's row rule (src/main-pthreads-rows.cxx:311-334).
+ *   XRT_SPLIT_BALANCED  (the default) the gather bounds a multi-GPU frame: a
+ *                       sender's rows cost their transfer over ONE link into
+ *                       device 0, device 0's rows only their render.  Device 0
+ *                       renders ONE run of 32-row bands anywhere in the frame,
+ *                       devices 1 .. n-1 the bands above it, then below it, in
+ *                       frame order, so that max(device 0's render + unpack,
+ *                       each sender's max(render, bytes / link)) is least
+ *                       (xrt_balanced_bounds).  The model comes from device 0:
+ *                       the whole frame rendered (binned) once per frame
+ *                       geometry -- per band its share of the render (the waves'
+ *                       timing records) and its packed bytes -- and the link
+ *                       rate: link_bytes_per_us when > 0, else measured once
+ *                       (every sender sends 4 MB to device 0 at once through
+ *                       this context's gather).  Planning is synchronous and
+ *                       happens on the first frame of a geometry.  The signed
+ *                       model, and frames with fewer bands than devices, split
+ *                       equally.
+ * Every split is exact: the gathered frame equals one device's frame.
+ */
+#define XRT_SPLIT_EQUAL 0
+#define XRT_SPLIT_BALANCED 1
+int xrt_multi_set_split(xrt_multi* m, int mode, double link_bytes_per_us);
+
+/*
+ * The strips of `camera`'s frame (planned now when its geometry is new):
+ * bounds[2g], bounds[2g+1] = [begin, end) rows of device g's strip (2n
+ * entries).  info (may be NULL): [0] the link rate the plan used (bytes per
+ * microsecond), [1] the modelled frame's render span (us), [2] the step the
+ * plan predicts (us); zeros for an equal split.
+ */
+int xrt_multi_plan(xrt_multi* m, const xrt_camera* camera, uint32_t* bounds, double* info);
+
+/*
+ * The balanced split as host arithmetic (no device): band_cost[b] = render time
+ * of band b (us), band_bytes[b] = the bytes band b's strip sends to device 0,
+ * n devices, link rate in bytes per microsecond, `band_rows` rows per band
+ * (the last band may be shorter: rows are clamped to `height`), unpack_us =
+ * device 0's per-frame unpack.  bounds: 2n entries as xrt_multi_plan's;
+ * *step_us (may be NULL) = the step the split implies.  XRT_ERR_ARGUMENT when
+ * there are fewer bands than devices.
+ */
+int xrt_balanced_bounds(const double* band_cost, const double* band_bytes, uint32_t n_bands, uint32_t n,
+                        double link_bytes_per_us, uint32_t height, uint32_t band_rows, double unpack_us,
+                        uint32_t* bounds, double* step_us);
 
 /* --- region-packed transit (multi-GPU gathers) ---------------------------- */
 

@@ -139,13 +139,24 @@ void xrt_host_mt_check(const float* det, const float* a, const float* b, const f
 /*
  * Diagnostics: host time of the last xrt_render_rows call (host buffers), ms:
  * ms[0] device planes (allocated once per size), [1] enqueue (preparation,
- * list sizing of a new geometry, launch), [2] wait for the render, [3..5] D2H
- * of image / L-buffer / u8, [6] statistics, [7] total; within them [8] the
- * time in hipMalloc, [9] a new frame geometry's list sizing, [10] device
- * synchronisations before a launch layout's upload, [11] host waits for the
- * preparation (k_prep), [12] kernel launches.
+ * list sizing of a new geometry, launch), [2] wait for the render, [3] D2H of
+ * the planes (DMA into the context's pinned ring, overlapped with its copy
+ * threads moving the pieces into the caller's pages), [4] copy threads (a
+ * count), [5] MB copied, [6] statistics, [7] total; within them [8] the time
+ * in hipMalloc, [9] a new frame geometry's list sizing, [10] synchronisations
+ * before a launch layout's upload (only when frames in flight may read it) --
+ * [13] of which the prep stream's, [14] the buffer sets' render events',
+ * [15] the last stream's --, [11] host waits for the preparation (k_prep),
+ * [12] kernel launches.
  */
-int xrt_debug_host_call_ms(xrt_context* ctx, double ms[13]);
+int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16]);
+
+/*
+ * Diagnostics: the phases of the last xrt_destroy, ms: [0] waiting for the
+ * context's own work, [1] device frees, [2] pinned host frees, [3] streams and
+ * events destroyed.
+ */
+int xrt_debug_destroy_ms(double ms[4]);
 
 #ifdef __cplusplus
 }

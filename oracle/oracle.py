@@ -100,6 +100,13 @@ def ref_lib():
         R.ref_render_rows.restype = ctypes.c_int64
         R.ref_render_rows.argtypes = [_F, ctypes.c_uint64, _F, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, _F, _F]
+        R.ref_mesh_create.restype = ctypes.c_void_p
+        R.ref_mesh_create.argtypes = [_F, ctypes.c_uint64]
+        R.ref_mesh_destroy.restype = None
+        R.ref_mesh_destroy.argtypes = [ctypes.c_void_p]
+        R.ref_render_span.restype = ctypes.c_int64
+        R.ref_render_span.argtypes = [ctypes.c_void_p, _F, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, _F, _F]
         _ref = R
     return _ref
 
@@ -245,6 +252,36 @@ def ref_intersect_batch(rays, tris):
     return hit, t
 
 
+def ref_render_spans(tris, cam13, width, height, rows, col_begin=0, col_end=None, threads=1):
+    """Pixels [col_begin, col_end) of each of `rows` through the reference's own
+    compiled classes (oracle/_ref), one row per task on `threads` host threads
+    over one shared TriangleMesh (main-pthreads-redo.cxx's threads share theirs):
+    (image, lbuffer) as (len(rows), span) float32 arrays, and the odd-ray count.
+    ctypes releases the GIL for every call."""
+    from concurrent.futures import ThreadPoolExecutor
+    R = ref_lib()
+    if R is None:
+        raise RuntimeError("oracle/_ref is not built")
+    if col_end is None:
+        col_end = width
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    cam = np.ascontiguousarray(cam13, np.float32)
+    rows = [int(r) for r in rows]
+    span = col_end - col_begin
+    img = np.empty((len(rows), span), np.float32)
+    lb = np.empty((len(rows), span), np.float32)
+    mesh = R.ref_mesh_create(_fp(tris), len(tris))
+    try:
+        def one(i):
+            return R.ref_render_span(mesh, _fp(cam), width, height, rows[i], col_begin, col_end,
+                                     _fp(img[i]), _fp(lb[i]))
+        with ThreadPoolExecutor(max(1, int(threads))) as ex:
+            odd = sum(ex.map(one, range(len(rows))))
+    finally:
+        R.ref_mesh_destroy(mesh)
+    return img, lb, odd
+
+
 def expf(x):
     x = np.ascontiguousarray(x, np.float32)
     out = np.empty_like(x)
@@ -272,6 +309,17 @@ def text_bytes(img, width, height):
 
 def lut_u8(v):
     return lib().orc_lut_u8(float(v))
+
+
+def lut_u8_array(v):
+    """lut_u8 over an array: Image::applyLUT's per-pixel formula (include/Image.inl:195-211)
+    with vmin 0, vmax 80 -- round(255 * (v - 0) / 80) in f64, half away from zero, clamped
+    to [0, 255], NaN -> 0.  255 * v is exact in f64 and the quotient is rounded once, as in
+    the reference; for v >= 0 the half-away rounding is floor(x + 0.5)."""
+    x = 255.0 * (np.asarray(v, np.float32) - np.float32(0.0)).astype(np.float64) / 80.0
+    out = np.where(x >= 0, np.floor(x + 0.5), -np.floor(-x + 0.5))
+    out = np.where(np.isnan(x), 0.0, np.clip(out, 0.0, 255.0))
+    return out.astype(np.uint8)
 
 
 # --- scenes of several meshes, the signed L-buffer fork -----------------------

@@ -89,55 +89,94 @@ void ref_camera(const float lower_in[3], const float upper_in[3], uint32_t width
     cam[12] = spacing;
 }
 
+// One pixel of renderLoop (src/main.cxx:652-742) through the reference
+// classes; returns true for an odd hit count ("Only one intersect", :710).
+static bool ref_pixel(const TriangleMesh& mesh, const float cam[13], uint32_t width, uint32_t height,
+                      uint32_t row, uint32_t col, std::vector<float>& hits, float& photon, float& lval)
+{
+    const Vec3 origin(cam[0], cam[1], cam[2]);
+    const Vec3 detector(cam[3], cam[4], cam[5]);
+    const Vec3 up(cam[6], cam[7], cam[8]);
+    const Vec3 right(cam[9], cam[10], cam[11]);
+    const float spacing = cam[12];
+    float v_off = spacing * (0.5 + row - height / 2.0);
+    float u_off = spacing * (0.5 + col - width / 2.0);
+    Vec3 dir = detector + up * v_off + right * u_off - origin;
+    dir.normalise();
+    Ray ray(origin, dir);
+
+    hits.clear();
+    for (unsigned int k = 0; k < mesh.getNumberOfTriangles(); ++k) {
+        float t;
+        if (ray.intersect(mesh.getTriangle(k), t) && t > 0.0000001) hits.push_back(t);
+    }
+    float path = 0;
+    bool odd = false;
+    lval = std::numeric_limits<float>::infinity();
+    if (!hits.empty()) {
+        if (hits.size() % 2 == 0) {
+            std::sort(hits.begin(), hits.end());
+            for (size_t i = 0; i < hits.size(); i += 2) path += hits[i + 1] - hits[i];
+        } else {
+            odd = true;
+        }
+        lval = path;
+    }
+    path = path * 0.1;
+    photon = 80.000f * std::exp(-(0.3971f * path));
+    return odd;
+}
+
+static TriangleMesh* make_mesh(const float* tris, uint64_t ntris)
+{
+    std::vector<float> v(tris, tris + 9 * ntris);
+    std::vector<unsigned int> idx(3 * ntris);
+    for (uint64_t i = 0; i < 3 * ntris; ++i) idx[i] = (unsigned int)i;
+    return new TriangleMesh(v, idx);
+}
+
 // One image row range through the reference classes.  Outputs are
 // strip-relative; odd-count rays are counted and returned.
 int64_t ref_render_rows(const float* tris, uint64_t ntris, const float cam[13],
                         uint32_t width, uint32_t height, uint32_t row_begin,
                         uint32_t row_end, float* image, float* lbuffer)
 {
-    std::vector<float> v(tris, tris + 9 * ntris);
-    std::vector<unsigned int> idx(3 * ntris);
-    for (uint64_t i = 0; i < 3 * ntris; ++i) idx[i] = (unsigned int)i;
-    TriangleMesh mesh(v, idx);
-
-    const Vec3 origin(cam[0], cam[1], cam[2]);
-    const Vec3 detector(cam[3], cam[4], cam[5]);
-    const Vec3 up(cam[6], cam[7], cam[8]);
-    const Vec3 right(cam[9], cam[10], cam[11]);
-    const float spacing = cam[12];
-
+    TriangleMesh* mesh = make_mesh(tris, ntris);
     int64_t odd = 0;
     std::vector<float> hits;
     for (uint32_t row = row_begin; row < row_end; ++row) {
         for (uint32_t col = 0; col < width; ++col) {
-            float v_off = spacing * (0.5 + row - height / 2.0);
-            float u_off = spacing * (0.5 + col - width / 2.0);
-            Vec3 dir = detector + up * v_off + right * u_off - origin;
-            dir.normalise();
-            Ray ray(origin, dir);
-
-            hits.clear();
-            for (unsigned int k = 0; k < mesh.getNumberOfTriangles(); ++k) {
-                float t;
-                if (ray.intersect(mesh.getTriangle(k), t) && t > 0.0000001) hits.push_back(t);
-            }
-            float path = 0;
-            float lval = std::numeric_limits<float>::infinity();
-            if (!hits.empty()) {
-                if (hits.size() % 2 == 0) {
-                    std::sort(hits.begin(), hits.end());
-                    for (size_t i = 0; i < hits.size(); i += 2) path += hits[i + 1] - hits[i];
-                } else {
-                    ++odd;
-                }
-                lval = path;
-            }
-            path = path * 0.1;
-            float photon = 80.000f * std::exp(-(0.3971f * path));
+            float photon, lval;
+            odd += ref_pixel(*mesh, cam, width, height, row, col, hits, photon, lval) ? 1 : 0;
             size_t o = (size_t)(row - row_begin) * width + col;
             if (image) image[o] = photon;
             if (lbuffer) lbuffer[o] = lval;
         }
+    }
+    delete mesh;
+    return odd;
+}
+
+// A TriangleMesh built once and shared, read-only, by several threads
+// (bench.py's "reference" CPU baseline renders spans of rows on every host
+// thread over one mesh, as main-pthreads-redo.cxx's threads share theirs).
+void* ref_mesh_create(const float* tris, uint64_t ntris) { return make_mesh(tris, ntris); }
+
+void ref_mesh_destroy(void* mesh) { delete static_cast<TriangleMesh*>(mesh); }
+
+// Pixels [col_begin, col_end) of one row over a shared mesh; outputs indexed
+// from col_begin.  Returns the odd-count rays.
+int64_t ref_render_span(const void* mesh, const float cam[13], uint32_t width, uint32_t height, uint32_t row,
+                        uint32_t col_begin, uint32_t col_end, float* image, float* lbuffer)
+{
+    const TriangleMesh& m = *static_cast<const TriangleMesh*>(mesh);
+    int64_t odd = 0;
+    std::vector<float> hits;
+    for (uint32_t col = col_begin; col < col_end; ++col) {
+        float photon, lval;
+        odd += ref_pixel(m, cam, width, height, row, col, hits, photon, lval) ? 1 : 0;
+        if (image) image[col - col_begin] = photon;
+        if (lbuffer) lbuffer[col - col_begin] = lval;
     }
     return odd;
 }

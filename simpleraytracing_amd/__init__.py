@@ -20,13 +20,15 @@ import numpy as np
 from . import _abi
 from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
                    XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT, XRT_MODEL_ATTENUATION,
-                   XRT_MODEL_SIGNED, XRT_GATHER_AUTO, XRT_GATHER_COPY, XRT_GATHER_RCCL)
+                   XRT_MODEL_SIGNED, XRT_GATHER_AUTO, XRT_GATHER_COPY, XRT_GATHER_RCCL, XRT_SPLIT_EQUAL,
+                   XRT_SPLIT_BALANCED)
 
 __all__ = [
     "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
     "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT", "load_meshes", "scene_bbox", "camera_for_scene",
     "XRT_MODEL_ATTENUATION", "XRT_MODEL_SIGNED", "XRT_GATHER_AUTO", "XRT_GATHER_COPY", "XRT_GATHER_RCCL",
+    "XRT_SPLIT_EQUAL", "XRT_SPLIT_BALANCED",
 ]
 
 
@@ -255,12 +257,21 @@ class Context:
 
     def host_call_ms(self) -> dict:
         """Host time of the last render_rows call, ms (xrt_debug_host_call_ms)."""
-        ms = (ctypes.c_double * 13)()
+        ms = (ctypes.c_double * 16)()
         self._check(self._lib.xrt_debug_host_call_ms(self._ctx, ms), "xrt_debug_host_call_ms")
-        keys = ("device_planes", "enqueue", "render_wait", "d2h_image", "d2h_lbuffer", "d2h_u8", "stats", "total",
+        keys = ("device_planes", "enqueue", "render_wait", "d2h", "d2h_copy_threads", "d2h_mb", "stats", "total",
                 "of_which_hipmalloc", "of_which_list_sizing", "of_which_device_sync", "of_which_prep_wait",
-                "of_which_launches")
+                "of_which_launches", "device_sync_prep_stream", "device_sync_set_events",
+                "device_sync_last_stream")
         return dict(zip(keys, (float(v) for v in ms)))
+
+    @staticmethod
+    def last_destroy_ms() -> dict:
+        """Phases of the last xrt_destroy in this process, ms (xrt_debug_destroy_ms)."""
+        ms = (ctypes.c_double * 4)()
+        _abi.load().xrt_debug_destroy_ms(ms)
+        return dict(zip(("wait_for_work", "device_frees", "pinned_host_frees", "streams_events"),
+                        (float(v) for v in ms)))
 
     def render_rows(self, cam: Camera, row_begin: int = 0, row_end: int | None = None,
                     image=True, lbuffer=True, u8=True, out=None):
@@ -299,6 +310,28 @@ class Context:
         st = Stats()
         self._check(self._lib.xrt_read_stats(self._ctx, ctypes.byref(st)), "xrt_read_stats")
         return st
+
+    def render_frames_device(self, cam: Camera, row_begin: int, row_end: int, n_frames: int, sets):
+        """n_frames frames of one geometry in one call (xrt_render_frames_device); frame k into
+        sets[k % len(sets)] = (d_image, d_lbuffer, d_u8, stream) raw pointers (0 = none / default)."""
+        ns = len(sets)
+        arrs = [(ctypes.c_void_p * ns)(*[(s[i] or None) for s in sets]) for i in range(4)]
+        rc = self._lib.xrt_render_frames_device(self._ctx, ctypes.byref(cam), row_begin, row_end, int(n_frames), ns,
+                                                *arrs)
+        self._check(rc, "xrt_render_frames_device")
+
+    def render_frames(self, cam: Camera, n_frames: int, row_begin: int = 0, row_end: int | None = None):
+        """n_frames frames back to back, the last one's host planes: (image, lbuffer, u8, stats, ms_per_frame)."""
+        if row_end is None:
+            row_end = cam.height
+        n = max(row_end - row_begin, 0) * cam.width
+        img, lb, u = np.empty(n, np.float32), np.empty(n, np.float32), np.empty(n, np.uint8)
+        st = Stats()
+        ms = ctypes.c_double()
+        self._check(self._lib.xrt_render_frames(self._ctx, ctypes.byref(cam), row_begin, row_end, int(n_frames),
+                                                _fptr(img), _fptr(lb), _u8ptr(u), ctypes.byref(st), ctypes.byref(ms)),
+                    "xrt_render_frames")
+        return img, lb, u, st, ms.value
 
     def set_miss_code(self, bits: int):
         """L-buffer bits of a miss in later renders: 0 (+inf) or XRT_MISS_TRANSIT."""
@@ -441,6 +474,20 @@ class MultiContext:
 
     def set_model(self, model: int, mu: float = 0.1037):
         self._check(self._lib.xrt_multi_set_model(self._m, int(model), float(np.float32(mu))), "xrt_multi_set_model")
+
+    def set_split(self, mode: int, link_bytes_per_us: float = 0.0):
+        """XRT_SPLIT_EQUAL (the reference's H/N rows) or XRT_SPLIT_BALANCED (the default;
+        link rate in bytes/us, 0 = measured once)."""
+        self._check(self._lib.xrt_multi_set_split(self._m, int(mode), float(link_bytes_per_us)), "xrt_multi_set_split")
+
+    def plan(self, cam: Camera):
+        """The strips of cam's frame: ([(begin, end) per device], {link, span_us, step_us})."""
+        n = len(self.devices)
+        b = (ctypes.c_uint32 * (2 * n))()
+        info = (ctypes.c_double * 3)()
+        self._check(self._lib.xrt_multi_plan(self._m, ctypes.byref(cam), b, info), "xrt_multi_plan")
+        return ([(int(b[2 * g]), int(b[2 * g + 1])) for g in range(n)],
+                {"link_bytes_per_us": info[0], "frame_span_us": info[1], "predicted_step_us": info[2]})
 
     def render(self, cam: Camera, image=True, lbuffer=True, u8=True):
         """The whole frame, gathered to the host: (image, lbuffer, u8, stats)."""

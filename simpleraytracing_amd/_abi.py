@@ -40,6 +40,9 @@ XRT_GATHER_AUTO = 0
 XRT_GATHER_COPY = 1
 XRT_GATHER_RCCL = 2
 
+XRT_SPLIT_EQUAL = 0
+XRT_SPLIT_BALANCED = 1
+
 XRT_IMAGE_TEXT = 0
 XRT_IMAGE_TGA = 1
 XRT_IMAGE_PGM = 2
@@ -117,6 +120,11 @@ XRT_SYMBOLS = {
     "xrt_render_rows_device": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _vp, _vp,
                                               _vp, _vp]),
     "xrt_read_stats": (ctypes.c_int, [_CtxP, ctypes.POINTER(Stats)]),
+    "xrt_render_frames_device": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _u32, _u32,
+                                                ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                                ctypes.POINTER(_vp)]),
+    "xrt_render_frames": (ctypes.c_int, [_CtxP, ctypes.POINTER(Camera), _u32, _u32, _u32, _fp, _fp, _u8p,
+                                         ctypes.POINTER(Stats), _dp]),
     "xrt_timing_begin": (ctypes.c_int, [_CtxP]),
     "xrt_timing_end": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
     "xrt_timing_events": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
@@ -139,6 +147,7 @@ XRT_SYMBOLS = {
     "xrt_debug_geometry_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_pipeline_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_host_call_ms": (ctypes.c_int, [_CtxP, _dp]),
+    "xrt_debug_destroy_ms": (ctypes.c_int, [_dp]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_wave_times": (ctypes.c_int, [_CtxP, _u32, ctypes.POINTER(_u32), _u64, ctypes.POINTER(_u64)]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
@@ -162,6 +171,10 @@ XRT_SYMBOLS = {
     "xrt_render_rows_multi_device": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), _vp, _vp, _vp, _vp]),
     "xrt_multi_read_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(Stats)]),
     "xrt_multi_set_gather": (ctypes.c_int, [_MultiP, ctypes.c_int]),
+    "xrt_multi_set_split": (ctypes.c_int, [_MultiP, ctypes.c_int, ctypes.c_double]),
+    "xrt_multi_plan": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), ctypes.POINTER(_u32), _dp]),
+    "xrt_balanced_bounds": (ctypes.c_int, [_dp, _dp, _u32, _u32, ctypes.c_double, _u32, _u32, ctypes.c_double,
+                                           ctypes.POINTER(_u32), _dp]),
 }
 
 # every C symbol declared in include/xrt_host.h

@@ -209,6 +209,29 @@ void renderLoopRows(Image& image, const std::vector<TriangleMesh>& meshes, const
                  image.getData() + (size_t)row_begin * image.getWidth(), lbuffer_strip, u8_strip, stats);
 }
 
+double renderLoopFrames(Image& image, const std::vector<TriangleMesh>& meshes, const RayTracerInfo& info,
+                        unsigned int frames, unsigned int row_begin, unsigned int row_end, xrt_stats* stats)
+{
+    if (row_begin > row_end || row_end > image.getHeight())
+        throw std::out_of_range("renderLoopFrames: row range outside the image");
+    xrt_camera cam = camera_for(image, meshes, info);
+    std::vector<float> soup = mesh0_soup(meshes);
+    DeviceSlot& slot = device_slot(device_choice());
+    std::lock_guard<std::mutex> g(slot.lock);
+    xrt_context* ctx = slot.ctx;
+    check(ctx, xrt_set_kernel(ctx, kernel_choice()), "xrt_set_kernel");
+    if (!slot.uploaded || slot.mesh != soup) {
+        check(ctx, xrt_upload_mesh(ctx, soup.data(), soup.size() / 9), "xrt_upload_mesh");
+        slot.mesh = soup;
+        slot.uploaded = true;
+    }
+    double ms = 0.0;
+    check(ctx, xrt_render_frames(ctx, &cam, row_begin, row_end, frames,
+                                 image.getData() + (size_t)row_begin * image.getWidth(), nullptr, nullptr, stats, &ms),
+          "xrt_render_frames");
+    return ms;
+}
+
 namespace {
 thread_local unsigned long long t_last_odd_rays = 0;
 }

@@ -65,6 +65,13 @@ void renderLoopRows(Image& output_image, const std::vector<TriangleMesh>& meshes
                     const RayTracerInfo& info, unsigned int row_begin, unsigned int row_end,
                     float* lbuffer_strip, unsigned char* u8_strip, xrt_stats* stats);
 
+// renderLoop's rows [row_begin, row_end) rendered `frames` times back to back
+// (one xrt_render_frames call: every frame prepared and rendered in full, the
+// host side of all of them in one pass); output_image holds the last frame,
+// *stats its counters.  Returns the device time per frame in ms.  Does not print.
+double renderLoopFrames(Image& output_image, const std::vector<TriangleMesh>& meshes, const RayTracerInfo& info,
+                        unsigned int frames, unsigned int row_begin, unsigned int row_end, xrt_stats* stats);
+
 // The L-buffer fork, src/main-pthreads-lbuffer.cxx: renderLoopCallBack over
 // the whole image (:733-813, the signed multi-material L-buffer, mesh 0's
 // coefficient 0.1037) and main's hole fill (:327-404) into output_image.

@@ -18,10 +18,18 @@
 //       --lbuffer FILE         also write the L-buffer as raw little-endian f32
 //       --u8 FILE              also write the 8-bit image (LUT 0..80) as PGM
 //       --time                 print render wall-clock and Mrays/s
+//       --rows A:B             render image rows [A, B) only and write that
+//                              strip (B - A text rows), as one pthreads
+//                              thread's share of the frame
+//       --batch N              render the frame N times back to back (one
+//                              xrt_render_frames call) and write the last;
+//                              with --time, the device time per frame
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -47,6 +55,8 @@ void showUsage(const std::string& prog)
               << "\t--lbuffer FILE\t\t\tWrite the L-buffer as raw float32\n"
               << "\t--u8 FILE\t\t\tWrite the 8-bit image (0..80 keV LUT) as PGM\n"
               << "\t--time\t\t\t\tPrint render time and Mrays/s\n"
+              << "\t--rows A:B\t\t\tRender and write image rows [A, B) only\n"
+              << "\t--batch N\t\t\tRender the frame N times back to back, write the last\n"
               << std::endl;
 }
 
@@ -59,6 +69,9 @@ struct Options {
     std::string lbuffer, u8;
     bool time = false;
     bool signed_model = false;
+    bool rows = false;
+    unsigned row_begin = 0, row_end = 0;
+    unsigned batch = 0;
 };
 
 unsigned parse_uint(const char* prog, int argc, char** argv, int& i)
@@ -117,12 +130,32 @@ Options processCmd(int argc, char** argv)
             o.signed_model = true;
         } else if (a == "--time") {
             o.time = true;
+        } else if (a == "--rows") {
+            const std::string r = parse_str(argv[0], argc, argv, i);
+            const size_t colon = r.find(':');
+            if (colon == std::string::npos || colon == 0 || colon + 1 >= r.size()) {
+                showUsage(argv[0]);
+                std::exit(EXIT_FAILURE);
+            }
+            o.rows = true;
+            o.row_begin = (unsigned)std::stoul(r.substr(0, colon));
+            o.row_end = (unsigned)std::stoul(r.substr(colon + 1));
+        } else if (a == "--batch") {
+            o.batch = parse_uint(argv[0], argc, argv, i);
+            if (!o.batch) {
+                showUsage(argv[0]);
+                std::exit(EXIT_FAILURE);
+            }
         } else {
             showUsage(argv[0]);
             std::exit(EXIT_FAILURE);
         }
     }
     if (o.inputs.empty()) o.inputs.push_back("./dragon.ply");
+    if (o.rows && (o.row_begin >= o.row_end || o.row_end > o.height))
+        throw std::out_of_range("--rows A:B must satisfy 0 <= A < B <= image height");
+    if ((o.rows || o.batch) && (o.signed_model || o.gpus > 1))
+        throw std::runtime_error("--rows and --batch render the attenuation model on one GPU");
     return o;
 }
 
@@ -153,16 +186,26 @@ int main(int argc, char** argv)
 
         auto r0 = std::chrono::high_resolution_clock::now();
         std::vector<float> lb;
-        if (opt.signed_model && opt.gpus > 1) {
+        const unsigned rb = opt.rows ? opt.row_begin : 0u, re = opt.rows ? opt.row_end : opt.height;
+        double ms_per_frame = 0.0;
+        if (opt.batch) {                          // N frames back to back, the last one kept
+            xrt_stats st;
+            ms_per_frame = renderLoopFrames(image, meshes, info, opt.batch, rb, re, &st);
+            for (unsigned long long k = 0; k < st.odd_rays; ++k) std::cout << "Only one intersect on this ray" << std::endl;
+        } else if (opt.rows && opt.lbuffer.empty()) {
+            xrt_stats st;
+            renderLoopRows(image, meshes, info, rb, re, nullptr, nullptr, &st);
+            for (unsigned long long k = 0; k < st.odd_rays; ++k) std::cout << "Only one intersect on this ray" << std::endl;
+        } else if (opt.signed_model && opt.gpus > 1) {
             renderLoopLBufferMultiGPU(image, meshes, info, opt.gpus, opt.lbuffer.empty() ? nullptr : &lb);
         } else if (opt.signed_model) {
             renderLoopLBuffer(image, meshes, info, opt.lbuffer.empty() ? nullptr : &lb);
         } else if (opt.gpus > 1) {
             renderLoopMultiGPU(image, meshes, info, opt.gpus);
         } else if (!opt.lbuffer.empty()) {       // the image and the L-buffer in one render
-            lb.resize((size_t)opt.width * opt.height);
+            lb.resize((size_t)opt.width * (re - rb));
             xrt_stats st;
-            renderLoopRows(image, meshes, info, 0, opt.height, lb.data(), nullptr, &st);
+            renderLoopRows(image, meshes, info, rb, re, lb.data(), nullptr, &st);
             for (unsigned long long k = 0; k < st.odd_rays; ++k) std::cout << "Only one intersect on this ray" << std::endl;
         } else {
             renderLoop(image, meshes, info);
@@ -170,18 +213,29 @@ int main(int argc, char** argv)
         auto r1 = std::chrono::high_resolution_clock::now();
         if (opt.time) {
             double s = std::chrono::duration<double>(r1 - r0).count();
-            std::cout << "Render took: " << s << " seconds ("
-                      << (double)opt.width * opt.height / s / 1e6 << " Mrays/s, " << opt.gpus
-                      << " GPU(s))" << std::endl;
+            const double rays = (double)opt.width * (re - rb);
+            std::cout << "Render took: " << s << " seconds (" << rays * (opt.batch ? opt.batch : 1) / s / 1e6
+                      << " Mrays/s, " << opt.gpus << " GPU(s))" << std::endl;
+            if (opt.batch)
+                std::cout << "Frames: " << opt.batch << ", device time per frame " << ms_per_frame << " ms ("
+                          << rays / (ms_per_frame * 1e3) << " Mrays/s)" << std::endl;
         }
 
-        image.saveTextFile(opt.output);
-        if (!opt.u8.empty()) image.savePGMFile(opt.u8, 0.0f, 80.0f);
+        Image* out = &image;
+        Image strip;
+        if (opt.rows) {                           // the strip's rows only
+            strip = Image(opt.width, re - rb, 0.0f);
+            std::copy(image.getData() + (size_t)rb * opt.width, image.getData() + (size_t)re * opt.width,
+                      strip.getData());
+            out = &strip;
+        }
+        out->saveTextFile(opt.output);
+        if (!opt.u8.empty()) out->savePGMFile(opt.u8, 0.0f, 80.0f);
         if (!opt.lbuffer.empty()) {
-            if (lb.empty()) {                   // multi-GPU: the L-buffer of the same frame
-                lb.resize((size_t)opt.width * opt.height);
+            if (lb.empty()) {                   // multi-GPU, batch: the L-buffer of the same frame
+                lb.resize((size_t)opt.width * (re - rb));
                 xrt_stats st;
-                renderLoopRows(image, meshes, info, 0, opt.height, lb.data(), nullptr, &st);
+                renderLoopRows(image, meshes, info, rb, re, lb.data(), nullptr, &st);
             }
             std::FILE* f = std::fopen(opt.lbuffer.c_str(), "wb");
             if (!f) throw std::runtime_error("Cannot create the file " + opt.lbuffer);

@@ -33,7 +33,7 @@
 #define XRT_RENDER_WAVES 8   // binned render: minimum waves per SIMD (8 = 64 VGPRs)
 #endif
 #ifndef XRT_STAGE
-#define XRT_STAGE 64      // binned render: candidates staged in LDS per round (8 KB; 128: 16 KB, 4 % slower at 2048^2 with the heavy-first plan)
+#define XRT_STAGE 64      // binned render: candidates a tile wave culls per round -- one footprint per lane, read into registers (64..256); only survivors' records go to the wave's 4-KB LDS stage
 #endif
 #ifndef XRT_PREP_THREADS
 #define XRT_PREP_THREADS 64  // k_prep workgroup size (64: single-wave groups fill the render's holes)
@@ -73,7 +73,7 @@ struct RenderParams {
     uint32_t row_begin, row_end;
     uint32_t num_triangles;
     uint32_t hit_capacity;  // <= XRT_MAX_HITS
-    uint32_t pad_;
+    uint32_t prep_tris;     // triangles per k_prep wave (prep_tris_for)
     uint32_t model;         // kModelAttenuation (main.cxx) or kModelSigned (the L-buffer fork)
 };
 

@@ -1326,6 +1326,15 @@ constexpr uint32_t kCounterStride = 32;
 constexpr uint32_t kBinBatch = XRT_BIN_BATCH;  // queued pairs per lane per commit round (their atomics in flight together)
 constexpr uint32_t kBinSmall = 64;           // region rectangles up to this many cells are flattened over the wave
 constexpr uint32_t kBinQueue = XRT_BIN_QUEUE;  // passing (region, triangle) pairs queued per wave before a commit
+// Launch slots of a k_prep wave's regions cached in LDS (0: off): when the
+// union of the wave's region rectangles has at most this many cells, the
+// wave DMAs their region -> slot entries into LDS before its cell tests, so
+// the commit reads LDS instead of a dependent global load.
+#ifndef XRT_PREP_RANK_LDS
+#define XRT_PREP_RANK_LDS 0
+#endif
+constexpr uint32_t kRankCache = XRT_PREP_RANK_LDS;
+static_assert(kRankCache % 64u == 0u, "whole DMA rounds");
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -1474,8 +1483,14 @@ constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 #ifndef XRT_PREP_TRIS
 #define XRT_PREP_TRIS 32
 #endif
-constexpr uint32_t kPrepTris = XRT_PREP_TRIS;     // triangles per k_prep wave (1..64)
+constexpr uint32_t kPrepTris = XRT_PREP_TRIS;     // triangles per k_prep wave (1..64) of small meshes
 static_assert(kPrepTris >= 1u && kPrepTris <= 64u, "kPrepTris");
+// Meshes of at least kPrepBigMesh triangles prepare 64 per wave: half the
+// waves, each binning twice the pairs (1.12 M triangles at 8192^2: k_prep
+// 922 -> 760 us beside the render, step 1,064 -> 1,056 us; 1024^2 dragon
+// frames lose 1.6 us with 64, so small meshes keep kPrepTris).
+constexpr uint32_t kPrepBigMesh = 1u << 18;
+__host__ __device__ constexpr uint32_t prep_tris_for(uint64_t T) { return T >= kPrepBigMesh ? 64u : kPrepTris; }
 
 __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__ tris, uint32_t T,
                                               RenderParams p, CullParams cp,
@@ -1490,12 +1505,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     // renders, and a raised priority only took issue slots from the render
     // (1024^2 step 29.0 -> 27.6 us without it).
     // i: the thread's index over the grid (pixel-offset tables, counter
-    // clears); tri: its triangle -- kPrepTris per wave (fewer than 64 spreads
+    // clears); tri: its triangle -- p.prep_tris per wave (fewer than 64 spreads
     // the binning's cells and commits of a frame over more waves).
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t tri_lane = threadIdx.x & 63u;
-    const uint32_t tri = (blockIdx.x * kPrepWaves + (threadIdx.x >> 6)) * kPrepTris + tri_lane;
-    const bool valid = tri_lane < kPrepTris && tri < T;
+    const uint32_t tri = (blockIdx.x * kPrepWaves + (threadIdx.x >> 6)) * p.prep_tris + tri_lane;
+    const bool valid = tri_lane < p.prep_tris && tri < T;
     if (i == 0 && frame_out) *frame_out = p;       // the render's make_ray reads it (Outputs::frame)
     if (offsets_out) {                             // v_off of every row, then u_off of every column
         if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
@@ -1583,6 +1598,33 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     s_fp[wave][3][lane] = fp.bbox;
     s_rect[wave][lane] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
     s_cum[wave][lane] = cum;
+    // The slots of the union of the wave's rectangles (mesh-adjacent triangles
+    // bin to neighbouring regions), DMAed into LDS under phase 1 when few.
+    bool cached = false;
+    uint32_t ux0 = 0, uy0 = 0, uw = 0;
+#if XRT_PREP_RANK_LDS
+    __shared__ uint32_t s_rank[kPrepWaves][kRankCache];
+    if (__ballot(has) != 0ull) {
+        ux0 = ~wave_reduce_u32<true>(has ? ~x0 : 0u);
+        uy0 = ~wave_reduce_u32<true>(has ? ~y0 : 0u);
+        const uint32_t ux1 = wave_reduce_u32<true>(has ? x1 : 0u);
+        const uint32_t uy1 = wave_reduce_u32<true>(has ? y1 : 0u);
+        uw = ux1 - ux0 + 1u;
+        const uint32_t ucells = uw * (uy1 - uy0 + 1u);
+        cached = ucells <= kRankCache;
+        if (cached) {
+            for (uint32_t c0 = 0; c0 < ucells; c0 += 64u) {
+                const uint32_t c = c0 + lane;
+                if (c < ucells)
+                    __builtin_amdgcn_global_load_lds((const void*)(bins.rank + (uy0 + c / uw) * bins.regions_x + ux0 +
+                                                                   c % uw),
+                                                     (__attribute__((address_space(3))) void*)&s_rank[wave][c0], 4, 0,
+                                                     0);
+            }
+        }
+    }
+#endif
+    bool rank_waited = false;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1594,6 +1636,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
     auto commit = [&]() {
+#if XRT_PREP_RANK_LDS
+        if (cached && !rank_waited) {              // the slots' DMA has landed (issued before phase 1)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            rank_waited = true;
+        }
+#endif
         for (uint32_t base = 0; base < queued; base += 64u * kBinBatch) {
             uint32_t reg[kBinBatch], own[kBinBatch], slot[kBinBatch];
 #pragma unroll
@@ -1602,7 +1650,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 reg[b] = kEmpty;
                 own[b] = 0u;
                 if (q < queued) {
+#if XRT_PREP_RANK_LDS
+                    reg[b] = cached ? s_rank[wave][s_qreg[wave][q]] : bins.rank[s_qreg[wave][q]];
+#else
                     reg[b] = bins.rank[s_qreg[wave][q]];
+#endif
                     own[b] = s_qown[wave][q];
                 }
             }
@@ -1648,7 +1700,8 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
         if (pass) {
             const uint32_t q = queued + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            s_qreg[wave][q] = ry * bins.regions_x + rx;
+            // the cached slot's index, or the region
+            s_qreg[wave][q] = cached ? (ry - uy0) * uw + (rx - ux0) : ry * bins.regions_x + rx;
             s_qown[wave][q] = (uint8_t)owner;
         }
         queued += (uint32_t)__popcll(m);

@@ -5,14 +5,20 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <limits>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "xrt_debug.h"
@@ -100,7 +106,29 @@ static_assert(kAheadFrames + 2 <= (size_t)kFrameSets, "sets for the renders in f
 // it launches the render, and for the completion event of the render that
 // last used the set before it prepares into the set again.
 constexpr uint32_t kDirtyAll = 0xFFFFFFFFu;
-constexpr int kHostCallFields = 13;    // xrt_debug_host_call_ms
+constexpr int kHostCallFields = 16;    // xrt_debug_host_call_ms
+constexpr int kAccFields = 8;          // running sums behind host_call_ms[8..15]
+// D2H of the host-buffer entry points (xrt_render_rows, ...): the planes are
+// DMAed in pieces of at most kStageChunk into a pinned staging ring of
+// kStageSlots pieces (allocated with the context), and the context's copy
+// threads move each piece into the caller's pages while the DMA of the next
+// pieces runs.  A pageable hipMemcpy stages through one thread at 12.7 GB/s
+// into fresh pages (tools/probes/d2h_probe.hip); the DMA into pinned memory
+// runs at ~54 GB/s and the page faults of fresh caller pages are taken by
+// several threads at once.  Pieces end at 2-MB boundaries of the caller's
+// buffer (a transparent huge page is faulted in by one thread: 512-KB parts of
+// one page on several threads measured 3.7-4.9 ms for 37.7 MB of fresh pages
+// against 1.5-1.8 ms).  XRT_D2H_THREADS overrides the thread count (0:
+// pageable hipMemcpy).
+constexpr size_t kStageChunk = (size_t)2 << 20;
+constexpr size_t kStageSlots = 16;
+constexpr int kD2HThreads = 8;
+// Pinned scratch of the list sizing (the count read-back) and of the launch
+// layouts' uploads, allocated with the context and grown on demand: pageable
+// copies there stage or pin the caller-side memory inside the HIP call, and a
+// fresh context's first sizing right after a long frame loop once waited
+// 10-22 ms in them (DESIGN.md "Measurement").
+constexpr size_t kSizingScratch = (size_t)1 << 20;
 
 struct FrameSet {
     TriRec* recs = nullptr;        // per-render records
@@ -152,6 +180,68 @@ struct FrameSet {
 };
 
 using HostClock = std::chrono::steady_clock;
+
+// A fixed set of host threads that run the pieces of one job at a time
+// (start: tasks 0 .. count-1 claimed in order; wait: until every piece ran).
+class CopyPool {
+public:
+    explicit CopyPool(int n)
+    {
+        for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : threads_) t.join();
+    }
+    int size() const { return (int)threads_.size(); }
+    void start(size_t count, std::function<void(size_t)> task)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            task_ = std::move(task);
+            count_ = count;
+            next_.store(0);
+            active_ = threads_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+    }
+    void wait()
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return active_ == 0; });
+    }
+
+private:
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            const size_t count = count_;
+            lk.unlock();
+            for (size_t i; (i = next_.fetch_add(1)) < count;) task_(i);
+            lk.lock();
+            if (--active_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(size_t)> task_;
+    size_t count_ = 0, active_ = 0;
+    std::atomic<size_t> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 // A launch layout of a region grid: launch slot -> region and list
 // (SlotDesc, device), region -> slot (k_prep's binning), and the host copy of
@@ -233,6 +323,26 @@ struct xrt_context {
     float* d_lbuffer = nullptr;
     uint8_t* d_u8 = nullptr;
     size_t stage_cap = 0;
+    // The host-buffer entry points run on this context-owned non-blocking
+    // stream (never the null stream, whose legacy semantics order it against
+    // every blocking stream of the device), and copy back through the pinned
+    // ring h_stage (kStageSlots x kStageChunk) with the copy threads of `pool`.
+    hipStream_t host_stream = nullptr;
+    uint8_t* h_stage = nullptr;
+    hipEvent_t stage_ev[kStageSlots] = {};
+    uint8_t* h_sizing = nullptr;       // pinned scratch of the sizing path (kSizingScratch, grown on demand)
+    size_t h_sizing_cap = 0;
+    hipEvent_t sizing_ev = nullptr;    // the last upload from h_sizing (prep stream)
+    bool sizing_busy = false;
+    hipEvent_t host_render_done = nullptr;
+    std::unique_ptr<CopyPool> pool;
+    // the preparation stream holds work that reads a launch layout (k_prep)
+    // since it was last synchronised (upload_layout needs it idle)
+    bool prep_reads_layout = false;
+    // XRT_SIZING_PROFILE=1: a new geometry's preparation step by step, each
+    // step synchronised and timed on the host (stderr) -- diagnostics only
+    int sizing_profile = 0;
+    HostClock::time_point prof_t{};
 
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     // xrt_read_stats: the last render's records summed on the device
@@ -243,13 +353,15 @@ struct xrt_context {
     StatsSum* h_stats = nullptr;           // pinned
     // host time of the last host-buffer call (xrt_render_rows), ms:
     // [0] device planes, [1] enqueue (preparation, sizing, launch), [2] wait for
-    // the render, [3..5] D2H of image / L-buffer / u8, [6] statistics, [7] total;
-    // within them: [8] every hipMalloc of the call, [9] a new geometry's list
-    // sizing (count read-back, layout upload), [10] device synchronisations
-    // before a launch layout's upload, [11] host waits for k_prep, [12] kernel
-    // launches (k_prep and render)
+    // the render, [3] D2H of the planes (DMA into the pinned ring overlapped with
+    // the copy threads), [4] copy threads, [5] MB copied, [6] statistics,
+    // [7] total; within them: [8] every hipMalloc of the call, [9] a new
+    // geometry's list sizing (count read-back, layout upload), [10] the
+    // synchronisations before a launch layout's upload -- [13] of them the prep
+    // stream's, [14] the sets' render events', [15] the last stream's --,
+    // [11] host waits for k_prep, [12] kernel launches (k_prep and render)
     double host_call_ms[kHostCallFields] = {};
-    double acc_ms[5] = {};                           // running sums of [8..12]
+    double acc_ms[kAccFields] = {};                  // running sums of [8..15]
     // region timing (xrt_timing_begin/end)
     bool timing = false;
     std::vector<hipEvent_t> tev;      // pairs: [2i] start, [2i+1] stop of a sampled render dispatch
@@ -344,7 +456,25 @@ inline double seconds_since(HostClock::time_point t)
     return std::chrono::duration<double>(HostClock::now() - t).count();
 }
 
+// XRT_SIZING_PROFILE: synchronise the prep stream and print the time since the
+// last mark (the step's enqueue + execution).
+void prof_mark(xrt_context* ctx, const char* what)
+{
+    if (!ctx->sizing_profile) return;
+    const auto t_enq = HostClock::now();
+    // XRT_SIZING_PROFILE=2: host time per step only, no synchronisation
+    const hipError_t e = ctx->sizing_profile == 2 ? hipSuccess : hipStreamSynchronize(ctx->prep_stream);
+    const auto now = HostClock::now();
+    std::fprintf(stderr, "xrt sizing profile: %-34s %9.3f ms (of which sync %8.3f ms)%s\n", what,
+                 std::chrono::duration<double, std::milli>(now - ctx->prof_t).count(),
+                 std::chrono::duration<double, std::milli>(now - t_enq).count(), e == hipSuccess ? "" : " ERROR");
+    ctx->prof_t = HostClock::now();
+}
+
 static std::string g_create_error;
+// xrt_destroy's phases, ms (xrt_debug_destroy_ms): [0] waiting for the
+// context's work, [1] device frees, [2] pinned host frees, [3] streams and events
+static double g_destroy_ms[4] = {};
 
 // AUTO switches from TILED to BINNED past this many footprint-box tests
 // (T x regions) per frame (DESIGN.md "Kernels").
@@ -384,6 +514,25 @@ int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
     return XRT_OK;
 }
 
+// The pinned sizing scratch, at least `bytes`, once no upload from it is still
+// in flight (its last upload's event, long complete as a rule).
+int sizing_scratch(xrt_context* ctx, size_t bytes, uint8_t*& out)
+{
+    if (ctx->sizing_busy) {
+        XRT_HIP(ctx, hipEventSynchronize(ctx->sizing_ev));
+        ctx->sizing_busy = false;
+    }
+    if (ctx->h_sizing_cap < bytes) {
+        if (ctx->h_sizing) (void)hipHostFree(ctx->h_sizing);
+        ctx->h_sizing = nullptr;
+        ctx->h_sizing_cap = 0;
+        XRT_HIP(ctx, hipHostMalloc((void**)&ctx->h_sizing, bytes, hipHostMallocDefault));
+        ctx->h_sizing_cap = bytes;
+    }
+    out = ctx->h_sizing;
+    return XRT_OK;
+}
+
 // Waits for this context's own work: its preparations (prep stream), every
 // render still marked in flight (the sets' completion events) and the last
 // enqueue's stream (a statistics reduction behind the render).  Not the whole
@@ -392,11 +541,31 @@ int ensure(xrt_context* ctx, T*& ptr, size_t& cap, size_t need_elems)
 // process whose device was otherwise idle).
 int sync_context(xrt_context* ctx)
 {
+    auto t = HostClock::now();
+    auto lap = [&](int k) {
+        const auto now = HostClock::now();
+        ctx->acc_ms[k] += std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
     XRT_HIP(ctx, hipStreamSynchronize(ctx->prep_stream));
+    ctx->prep_reads_layout = false;
+    lap(5);
     for (FrameSet& fs : ctx->sets)
         if (fs.done_valid) XRT_HIP(ctx, hipEventSynchronize(fs.done_ev));
+    lap(6);
     if (ctx->pending) XRT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+    lap(7);
     return XRT_OK;
+}
+
+// True when a render or preparation of this context may still read its launch
+// layouts (upload_layout must not overwrite them under it).
+bool layouts_in_use(const xrt_context* ctx)
+{
+    if (ctx->prep_reads_layout || ctx->pending) return true;
+    for (const FrameSet& fs : ctx->sets)
+        if (fs.done_valid) return true;
+    return false;
 }
 
 // The reference's stdmin / stdmax semantics (std::min(a,b) = b<a ? b : a).
@@ -438,7 +607,7 @@ RenderParams make_params(const xrt_camera& c, uint32_t row_begin, uint32_t row_e
     p.row_end = row_end;
     p.num_triangles = (uint32_t)T;
     p.hit_capacity = capacity;
-    p.pad_ = 0u;
+    p.prep_tris = prep_tris_for(T);
     return p;
 }
 
@@ -554,9 +723,10 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                 const BinBuffers& bins, BinState* bin_ctl, hipStream_t stream, hipEvent_t done)
 {
     const uint64_t T = ctx->num_tris;
-    // kPrepTris triangles per wave; every thread covers a pixel-offset entry / counter
+    // p.prep_tris triangles per wave; every thread covers a pixel-offset entry / counter
     const uint64_t threads = std::max<uint64_t>((uint64_t)p.height + p.width, bins.clear ? bins.clear_regions : 0u);
-    const uint64_t blocks = std::max<uint64_t>((T + kPrepWaves * kPrepTris - 1) / (kPrepWaves * kPrepTris),
+    const uint64_t per_block = (uint64_t)kPrepWaves * p.prep_tris;
+    const uint64_t blocks = std::max<uint64_t>((T + per_block - 1) / per_block,
                                                (threads + kPrepThreads - 1) / kPrepThreads);
     const auto t_launch = HostClock::now();
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(kPrepThreads),
@@ -564,6 +734,7 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
                           fs.frame, fs.offsets);
     XRT_HIP(ctx, hipGetLastError());
+    if (bins.counts) ctx->prep_reads_layout = true;
     ctx->acc_ms[4] += std::chrono::duration<double, std::milli>(HostClock::now() - t_launch).count();
     if (ctx->host_profile) ctx->hp_lprep += seconds_since(t_launch);
     return XRT_OK;
@@ -642,14 +813,27 @@ int upload_layout(xrt_context* ctx, SlotLayout& L, uint32_t rx, uint32_t ry, std
         desc[s] = SlotDesc{base[s], cap[s], (r % rx) | ((r / rx) << 16), 0u};
         rank[r] = (uint32_t)s;
     }
-    const auto t_sync = HostClock::now();
-    int rc = sync_context(ctx);
-    if (rc) return rc;
-    ctx->acc_ms[2] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sync).count();
+    // Frames in flight may read the old layout: wait for them, but only when
+    // there are any (a fresh context's first frame waits for nothing).
+    int rc;
+    if (layouts_in_use(ctx)) {
+        const auto t_sync = HostClock::now();
+        if ((rc = sync_context(ctx))) return rc;
+        ctx->acc_ms[2] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sync).count();
+    }
     if ((rc = ensure(ctx, L.d_desc, L.desc_cap, n))) return rc;
     if ((rc = ensure(ctx, L.d_rank, L.rank_cap, n))) return rc;
-    XRT_HIP(ctx, hipMemcpy(L.d_desc, desc.data(), n * sizeof(SlotDesc), hipMemcpyHostToDevice));
-    XRT_HIP(ctx, hipMemcpy(L.d_rank, rank.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // from the pinned scratch, on the prep stream, in order before the k_prep
+    // that reads them
+    uint8_t* h = nullptr;
+    if ((rc = sizing_scratch(ctx, n * (sizeof(SlotDesc) + sizeof(uint32_t)), h))) return rc;
+    std::memcpy(h, desc.data(), n * sizeof(SlotDesc));
+    std::memcpy(h + n * sizeof(SlotDesc), rank.data(), n * sizeof(uint32_t));
+    XRT_HIP(ctx, hipMemcpyAsync(L.d_desc, h, n * sizeof(SlotDesc), hipMemcpyHostToDevice, ctx->prep_stream));
+    XRT_HIP(ctx, hipMemcpyAsync(L.d_rank, h + n * sizeof(SlotDesc), n * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                ctx->prep_stream));
+    XRT_HIP(ctx, hipEventRecord(ctx->sizing_ev, ctx->prep_stream));
+    ctx->sizing_busy = true;
     L.slot_region = std::move(slot_region);
     L.rx = rx;
     L.ry = ry;
@@ -822,6 +1006,10 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     // A new geometry's first k_prep only counts its pairs (no lists): the
     // compact lists are sized from the counts and k_prep runs again into them.
     const bool sizing = new_geometry && !ctx->bin_force_cap;
+    if (sizing && ctx->sizing_profile) {
+        ctx->prof_t = t_call;
+        prof_mark(ctx, "set wait + buffers");
+    }
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
@@ -829,10 +1017,12 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bool cleared = false;
         const uint64_t entries = compact ? ctx->slot_pool : sizing ? 0u : (uint64_t)n_regions * fixed_cap;
         if ((rc = bin_buffers(ctx, fs, n_regions, entries, bins, bin_ctl, ps, cleared))) return rc;
+        if (sizing) prof_mark(ctx, "bin buffers (counter memset)");
         if (sizing) bins.list = nullptr;
         bins.tile_slots = n_regions;
         if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+        if (sizing) prof_mark(ctx, "fixed layout upload");
         // the fill plan's test hook (every region planned empty) is checked every frame
         arm_plan_check(fs, n_regions, bins, reuse, ctx->fill_plan == 2);
     }
@@ -845,13 +1035,21 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // pass above), slot offsets from them, and a re-run of k_prep into the
         // compact lists.
         ++ctx->hp_sizings;
+        prof_mark(ctx, "k_prep count pass");
         const auto t_sizing = HostClock::now();
-        std::vector<uint32_t> counts((size_t)n_regions * kCounterStride);
-        BinState st = {};
-        XRT_HIP(ctx, hipMemcpyAsync(counts.data(), bins.counts, counts.size() * sizeof(uint32_t),
-                                    hipMemcpyDeviceToHost, ps));
-        XRT_HIP(ctx, hipMemcpyAsync(&st, bin_ctl, sizeof st, hipMemcpyDeviceToHost, ps));
+        // every region's count (line-padded) and the BinState, into the pinned scratch
+        const size_t cbytes = (size_t)n_regions * kCounterStride * sizeof(uint32_t);
+        uint8_t* hs = nullptr;
+        if ((rc = sizing_scratch(ctx, cbytes + sizeof(BinState), hs))) return rc;
+        XRT_HIP(ctx, hipMemcpyAsync(hs, bins.counts, cbytes, hipMemcpyDeviceToHost, ps));
+        prof_mark(ctx, "count read-back: counts enqueued");
+        XRT_HIP(ctx, hipMemcpyAsync(hs + cbytes, bin_ctl, sizeof(BinState), hipMemcpyDeviceToHost, ps));
+        prof_mark(ctx, "count read-back: state enqueued");
         XRT_HIP(ctx, hipStreamSynchronize(ps));
+        prof_mark(ctx, "count read-back");
+        const uint32_t* counts = reinterpret_cast<const uint32_t*>(hs);
+        BinState st;
+        std::memcpy(&st, hs + cbytes, sizeof st);
         const std::vector<uint32_t>& fixed_region = ctx->fixed.slot_region;   // the counts' slots
         std::vector<uint32_t> count_of(n_regions);     // by region
         for (uint32_t s = 0; s < n_regions; ++s) count_of[fixed_region[s]] = counts[(size_t)s * kCounterStride];
@@ -892,7 +1090,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
             run += room;
         }
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
+        prof_mark(ctx, "plan (host)");
         if ((rc = upload_layout(ctx, ctx->compact_layout, rx, ry, std::move(slot_region), base, cap))) return rc;
+        prof_mark(ctx, "compact layout upload");
         ctx->acc_ms[1] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sizing).count();
         ctx->plan_tile_slots = tile_slots;
         ctx->plan_split_slots = split_slots;
@@ -906,7 +1106,9 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.tile_slots = n_regions;
         use_compact(ctx, n_regions, bins, fill_ok);
         arm_plan_check(fs, n_regions, bins, false, true);
+        prof_mark(ctx, "counter memset (re-run)");
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+        prof_mark(ctx, "k_prep into the compact lists");
     }
     // BINNED: one 8x8 tile per render wave, kTileWaves waves per workgroup, and
     // one workgroup per region of the fill plan
@@ -1155,9 +1357,90 @@ int enqueue_render(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, 
     return XRT_OK;
 }
 
+// One plane's device -> host copy of a host-buffer call.
+struct D2HCopy {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+
+// Copies `copies` (device -> the caller's host pages) behind the work already
+// on `stream`: kStageChunk pieces DMAed in order into the pinned ring on the
+// stream, each moved into the caller's pages by a copy thread once its DMA is
+// complete; a ring slot is reused once its previous piece has been moved.
+// Without copy threads (XRT_D2H_THREADS=0): pageable copies + synchronise.
+int d2h_copy(xrt_context* ctx, hipStream_t stream, const std::vector<D2HCopy>& copies)
+{
+    struct Piece {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t bytes;
+    };
+    std::vector<Piece> pieces;                         // at most kStageChunk, ending at 2-MB boundaries of dst
+    for (const D2HCopy& c : copies) {
+        size_t o = 0;
+        while (o < c.bytes) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(c.dst) + o;
+            const size_t len = std::min(kStageChunk - (size_t)(a % kStageChunk), c.bytes - o);
+            pieces.push_back({(uint8_t*)c.dst + o, (const uint8_t*)c.src + o, len});
+            o += len;
+        }
+    }
+    if (pieces.empty()) return XRT_OK;
+    if (!ctx->pool) {
+        for (const D2HCopy& c : copies)
+            if (c.bytes) XRT_HIP(ctx, hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost, stream));
+        XRT_HIP(ctx, hipStreamSynchronize(stream));
+        return XRT_OK;
+    }
+    const size_t n = pieces.size();
+    std::atomic<size_t> enqueued{0};                   // pieces whose DMA (and event) is enqueued
+    std::unique_ptr<std::atomic<uint8_t>[]> moved(new std::atomic<uint8_t>[n]);
+    for (size_t i = 0; i < n; ++i) moved[i].store(0);
+    std::atomic<int> failed{0};
+    ctx->pool->start(n, [&](size_t i) {
+        while (enqueued.load(std::memory_order_acquire) <= i) {
+            if (failed.load()) {
+                moved[i].store(1, std::memory_order_release);
+                return;
+            }
+            std::this_thread::yield();
+        }
+        if (hipEventSynchronize(ctx->stage_ev[i % kStageSlots]) != hipSuccess)
+            failed.store(1);
+        else
+            std::memcpy(pieces[i].dst, ctx->h_stage + (i % kStageSlots) * kStageChunk, pieces[i].bytes);
+        moved[i].store(1, std::memory_order_release);
+    });
+    hipError_t err = hipSuccess;
+    for (size_t i = 0; i < n; ++i) {
+        if (i >= kStageSlots)                          // the slot's previous piece has been moved
+            while (!moved[i - kStageSlots].load(std::memory_order_acquire)) std::this_thread::yield();
+        uint8_t* slot = ctx->h_stage + (i % kStageSlots) * kStageChunk;
+        err = hipMemcpyAsync(slot, pieces[i].src, pieces[i].bytes, hipMemcpyDeviceToHost, stream);
+        if (err == hipSuccess) err = hipEventRecord(ctx->stage_ev[i % kStageSlots], stream);
+        if (err != hipSuccess) {
+            failed.store(1);
+            break;
+        }
+        enqueued.store(i + 1, std::memory_order_release);
+    }
+    ctx->pool->wait();
+    if (err != hipSuccess) return fail(ctx, XRT_ERR_DEVICE, std::string("D2H copy: ") + hipGetErrorString(err));
+    if (failed.load()) return fail(ctx, XRT_ERR_DEVICE, "D2H copy: a staged piece failed");
+    return XRT_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int xrt_debug_destroy_ms(double ms[4])
+{
+    if (!ms) return XRT_ERR_ARGUMENT;
+    std::copy(g_destroy_ms, g_destroy_ms + 4, ms);
+    return XRT_OK;
+}
 
 int xrt_abi_version(void) { return XRT_ABI_VERSION; }
 
@@ -1185,6 +1468,8 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
+    const char* sp = std::getenv("XRT_SIZING_PROFILE");
+    ctx->sizing_profile = sp ? std::atoi(sp) : 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
@@ -1209,6 +1494,20 @@ int xrt_create(int device, xrt_context** out)
              hipEventCreate(&fs.ready) == hipSuccess &&
              hipEventCreate(&fs.done) == hipSuccess &&
              hipHostMalloc((void**)&fs.plan_flag, 2 * sizeof(uint32_t), hipHostMallocCoherent) == hipSuccess;
+    // the host-buffer entry points' stream, pinned D2H ring and copy threads
+    int threads = kD2HThreads;
+    if (const char* th = std::getenv("XRT_D2H_THREADS")) threads = std::max(0, std::atoi(th));
+    ok = ok && hipStreamCreateWithFlags(&ctx->host_stream, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&ctx->host_render_done, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&ctx->sizing_ev, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc((void**)&ctx->h_sizing, kSizingScratch, hipHostMallocDefault) == hipSuccess;
+    if (ok) ctx->h_sizing_cap = kSizingScratch;
+    if (ok && threads > 0) {
+        ok = hipHostMalloc((void**)&ctx->h_stage, kStageSlots * kStageChunk, hipHostMallocDefault) == hipSuccess;
+        for (hipEvent_t& e : ctx->stage_ev)
+            ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+        if (ok) ctx->pool.reset(new CopyPool(threads));
+    }
     if (!ok) {
         xrt_destroy(ctx);
         return fail(nullptr, XRT_ERR_DEVICE, "device allocation failed");
@@ -1235,7 +1534,16 @@ void xrt_destroy(xrt_context* ctx)
                      (unsigned long long)ctx->hp_overflow, (unsigned long long)ctx->hp_ahead_used,
                      (unsigned long long)ctx->hp_ahead_dropped, (unsigned long long)ctx->hp_launch_nowait);
     (void)hipSetDevice(ctx->device);
+    auto t = HostClock::now();
+    auto lap = [&](int k) {
+        const auto now = HostClock::now();
+        g_destroy_ms[k] = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
     (void)sync_context(ctx);
+    if (ctx->host_stream) (void)hipStreamSynchronize(ctx->host_stream);
+    lap(0);
+    ctx->pool.reset();
     (void)hipFree(ctx->d_tris);
     for (FrameSet& fs : ctx->sets) {
         (void)hipFree(fs.recs);
@@ -1251,7 +1559,6 @@ void xrt_destroy(xrt_context* ctx)
         for (hipEvent_t e : {fs.ready, fs.done})
             if (e) (void)hipEventDestroy(e);
     }
-    if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
     for (SlotLayout* L : {&ctx->fixed, &ctx->compact_layout}) {
         (void)hipFree(L->d_desc);
         (void)hipFree(L->d_rank);
@@ -1262,11 +1569,22 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_stats_partial);
     (void)hipFree(ctx->d_stats_done);
     (void)hipFree(ctx->d_stats_out);
-    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
-    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     for (auto& c : ctx->tchunks) (void)hipFree(c.p);
+    lap(1);
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->h_sizing) (void)hipHostFree(ctx->h_sizing);
+    lap(2);
+    if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
+    if (ctx->host_stream) (void)hipStreamDestroy(ctx->host_stream);
+    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->stage_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->host_render_done) (void)hipEventDestroy(ctx->host_render_done);
+    if (ctx->sizing_ev) (void)hipEventDestroy(ctx->sizing_ev);
     if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+    lap(3);
     delete ctx;
 }
 
@@ -1420,13 +1738,14 @@ int xrt_hole_fill(xrt_context* ctx, uint32_t width, uint32_t height, const float
     if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
     if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
     ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
-    XRT_HIP(ctx, hipMemcpy(ctx->d_lbuffer, lbuffer, n * sizeof(float), hipMemcpyHostToDevice));
+    XRT_HIP(ctx, hipMemcpyAsync(ctx->d_lbuffer, lbuffer, n * sizeof(float), hipMemcpyHostToDevice, ctx->host_stream));
     if ((rc = xrt_hole_fill_device(ctx, width, height, ctx->d_lbuffer, image ? ctx->d_image : nullptr,
-                                   image_u8 ? ctx->d_u8 : nullptr, nullptr)))
+                                   image_u8 ? ctx->d_u8 : nullptr, ctx->host_stream)))
         return rc;
-    if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
-    if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
-    return XRT_OK;
+    std::vector<D2HCopy> copies;
+    if (image) copies.push_back({image, ctx->d_image, n * sizeof(float)});
+    if (image_u8) copies.push_back({image_u8, ctx->d_u8, n});
+    return d2h_copy(ctx, ctx->host_stream, copies);
 }
 
 int xrt_render_signed(xrt_context* ctx, const xrt_camera* camera, float* image, float* lbuffer,
@@ -1443,15 +1762,19 @@ int xrt_render_signed(xrt_context* ctx, const xrt_camera* camera, float* image, 
     if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
     if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
     ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
-    if ((rc = enqueue_render(ctx, camera, 0, camera->height, nullptr, ctx->d_lbuffer, nullptr, nullptr))) return rc;
-    if ((rc = xrt_hole_fill_device(ctx, camera->width, camera->height, ctx->d_lbuffer,
-                                   image ? ctx->d_image : nullptr, image_u8 ? ctx->d_u8 : nullptr, nullptr)))
+    if ((rc = enqueue_render(ctx, camera, 0, camera->height, nullptr, ctx->d_lbuffer, nullptr, ctx->host_stream)))
         return rc;
+    if ((rc = xrt_hole_fill_device(ctx, camera->width, camera->height, ctx->d_lbuffer,
+                                   image ? ctx->d_image : nullptr, image_u8 ? ctx->d_u8 : nullptr,
+                                   ctx->host_stream)))
+        return rc;
+    std::vector<D2HCopy> copies;
     if (n) {
-        if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
-        if (lbuffer) XRT_HIP(ctx, hipMemcpy(lbuffer, ctx->d_lbuffer, n * sizeof(float), hipMemcpyDeviceToHost));
-        if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
+        if (image) copies.push_back({image, ctx->d_image, n * sizeof(float)});
+        if (lbuffer) copies.push_back({lbuffer, ctx->d_lbuffer, n * sizeof(float)});
+        if (image_u8) copies.push_back({image_u8, ctx->d_u8, n});
     }
+    if ((rc = d2h_copy(ctx, ctx->host_stream, copies))) return rc;
     xrt_stats local;
     return xrt_read_stats(ctx, stats ? stats : &local);
 }
@@ -1589,7 +1912,7 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     return XRT_OK;
 }
 
-int xrt_debug_host_call_ms(xrt_context* ctx, double ms[13])
+int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16])
 {
     if (!ctx || !ms) return XRT_ERR_ARGUMENT;
     std::copy(ctx->host_call_ms, ctx->host_call_ms + kHostCallFields, ms);
@@ -1658,6 +1981,57 @@ int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t 
     if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
     return enqueue_render(ctx, camera, row_begin, row_end, d_image, d_lbuffer, d_u8,
                           (hipStream_t)stream, true);
+}
+
+int xrt_render_frames_device(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin, uint32_t row_end,
+                             uint32_t n_frames, uint32_t n_sets, float* const* d_image, float* const* d_lbuffer,
+                             uint8_t* const* d_u8, void* const* streams)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (n_frames && !n_sets) return fail(ctx, XRT_ERR_ARGUMENT, "n_sets must be >= 1");
+    for (uint32_t k = 0; k < n_frames; ++k) {
+        const uint32_t s = k % n_sets;
+        int rc = enqueue_render(ctx, camera, row_begin, row_end, d_image ? d_image[s] : nullptr,
+                                d_lbuffer ? d_lbuffer[s] : nullptr, d_u8 ? d_u8[s] : nullptr,
+                                streams ? (hipStream_t)streams[s] : nullptr, true);
+        if (rc) return rc;
+    }
+    return XRT_OK;
+}
+
+int xrt_render_frames(xrt_context* ctx, const xrt_camera* camera, uint32_t row_begin, uint32_t row_end,
+                      uint32_t n_frames, float* image, float* lbuffer, uint8_t* image_u8, xrt_stats* stats,
+                      double* ms_per_frame)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    int rc = check_camera(ctx, camera, row_begin, row_end);
+    if (rc) return rc;
+    if (!n_frames) return fail(ctx, XRT_ERR_ARGUMENT, "n_frames must be >= 1");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t n = (size_t)(row_end - row_begin) * camera->width;
+    size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
+    if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_lbuffer, cap_l, n))) return rc;
+    if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
+    ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
+    float* di = image ? ctx->d_image : nullptr;
+    float* dl = lbuffer ? ctx->d_lbuffer : nullptr;
+    uint8_t* du = image_u8 ? ctx->d_u8 : nullptr;
+    void* st = ctx->host_stream;
+    const auto t0 = HostClock::now();
+    if ((rc = xrt_render_frames_device(ctx, camera, row_begin, row_end, n_frames, 1, &di, &dl, &du, &st))) return rc;
+    XRT_HIP(ctx, hipStreamSynchronize(ctx->host_stream));
+    if (ms_per_frame)
+        *ms_per_frame = std::chrono::duration<double, std::milli>(HostClock::now() - t0).count() / n_frames;
+    std::vector<D2HCopy> copies;
+    if (n) {
+        if (image) copies.push_back({image, ctx->d_image, n * sizeof(float)});
+        if (lbuffer) copies.push_back({lbuffer, ctx->d_lbuffer, n * sizeof(float)});
+        if (image_u8) copies.push_back({image_u8, ctx->d_u8, n});
+    }
+    if ((rc = d2h_copy(ctx, ctx->host_stream, copies))) return rc;
+    xrt_stats local;
+    return xrt_read_stats(ctx, stats ? stats : &local);
 }
 
 int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
@@ -1818,8 +2192,8 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
     };
     auto t = t0;
     std::fill(hc, hc + kHostCallFields, 0.0);
-    double acc0[5];
-    std::copy(ctx->acc_ms, ctx->acc_ms + 5, acc0);
+    double acc0[kAccFields];
+    std::copy(ctx->acc_ms, ctx->acc_ms + kAccFields, acc0);
     const size_t n = (size_t)(row_end - row_begin) * camera->width;
     size_t cap_f = ctx->stage_cap, cap_l = ctx->stage_cap, cap_u = ctx->stage_cap;
     if ((rc = ensure(ctx, ctx->d_image, cap_f, n))) return rc;
@@ -1827,26 +2201,31 @@ int xrt_render_rows(xrt_context* ctx, const xrt_camera* camera, uint32_t row_beg
     if ((rc = ensure(ctx, ctx->d_u8, cap_u, n))) return rc;
     ctx->stage_cap = std::min(cap_f, std::min(cap_l, cap_u));
     lap(0, t);
+    // the context's own non-blocking stream (not the null stream)
     rc = enqueue_render(ctx, camera, row_begin, row_end, image ? ctx->d_image : nullptr,
-                        lbuffer ? ctx->d_lbuffer : nullptr, image_u8 ? ctx->d_u8 : nullptr, nullptr);
+                        lbuffer ? ctx->d_lbuffer : nullptr, image_u8 ? ctx->d_u8 : nullptr, ctx->host_stream);
     if (rc) return rc;
+    XRT_HIP(ctx, hipEventRecord(ctx->host_render_done, ctx->host_stream));
     lap(1, t);
-    XRT_HIP(ctx, hipStreamSynchronize(nullptr));
+    XRT_HIP(ctx, hipEventSynchronize(ctx->host_render_done));
     lap(2, t);
+    std::vector<D2HCopy> copies;
     if (n) {
-        if (image) XRT_HIP(ctx, hipMemcpy(image, ctx->d_image, n * sizeof(float), hipMemcpyDeviceToHost));
-        lap(3, t);
-        if (lbuffer)
-            XRT_HIP(ctx, hipMemcpy(lbuffer, ctx->d_lbuffer, n * sizeof(float), hipMemcpyDeviceToHost));
-        lap(4, t);
-        if (image_u8) XRT_HIP(ctx, hipMemcpy(image_u8, ctx->d_u8, n, hipMemcpyDeviceToHost));
-        lap(5, t);
+        if (image) copies.push_back({image, ctx->d_image, n * sizeof(float)});
+        if (lbuffer) copies.push_back({lbuffer, ctx->d_lbuffer, n * sizeof(float)});
+        if (image_u8) copies.push_back({image_u8, ctx->d_u8, n});
     }
+    if ((rc = d2h_copy(ctx, ctx->host_stream, copies))) return rc;
+    lap(3, t);
+    double bytes = 0.0;
+    for (const D2HCopy& c : copies) bytes += (double)c.bytes;
+    hc[4] = ctx->pool ? (double)ctx->pool->size() : 0.0;
+    hc[5] = bytes / 1e6;
     xrt_stats local;
     rc = xrt_read_stats(ctx, stats ? stats : &local);
     lap(6, t);
     hc[7] = std::chrono::duration<double, std::milli>(t - t0).count();
-    for (int k = 0; k < 5; ++k) hc[8 + k] = ctx->acc_ms[k] - acc0[k];
+    for (int k = 0; k < kAccFields; ++k) hc[8 + k] = ctx->acc_ms[k] - acc0[k];
     return rc;
 }
 
@@ -1924,7 +2303,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     p.model = ctx->model;
     CullParams cp = make_cull_params(*camera);
     BinBuffers nobins = {};
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepWaves * kPrepTris - 1) / (kPrepWaves * kPrepTris))),
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepWaves * p.prep_tris - 1) / (kPrepWaves * p.prep_tris))),
                        dim3(kPrepThreads), 0, 0, ctx->d_tris,
                        (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());

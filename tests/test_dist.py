@@ -178,6 +178,110 @@ def test_balanced_bounds_optimal_small():
         assert got <= best * 1.001 + 1e-9, (trial, got, best, b)
 
 
+def _balanced_bounds_py(band_cost, band_bytes, n: int, link_bytes_per_us: float, height: int,
+                    band_rows: int = 32, unpack_us: float = 5.0):
+    """Pure-Python restatement of the balanced split (the round-4 bench implementation), a
+    cross-check of the C one (xrt_balanced_bounds) that both multi-GPU paths now share."""
+    cost = [float(c) for c in band_cost]
+    byts = [float(b) for b in band_bytes]
+    nb = len(cost)
+    if nb != len(byts) or nb == 0:
+        raise ValueError("band_cost and band_bytes must have one entry per band")
+    if n <= 1:
+        return [(0, height)]
+    if nb < n:
+        raise ValueError("fewer bands than ranks")
+    link = max(float(link_bytes_per_us), 1e-9)
+    pre_c = [0.0]
+    pre_b = [0.0]
+    for c, b in zip(cost, byts):
+        pre_c.append(pre_c[-1] + c)
+        pre_b.append(pre_b[-1] + b)
+
+    def sender_cost(i, j):            # bands [i, j) on one sender
+        return max(pre_c[j] - pre_c[i], (pre_b[j] - pre_b[i]) / link)
+
+    def pieces(i, j, step):           # fewest senders covering [i, j) within step (greedy); None: impossible
+        k, a = 0, i
+        while a < j:
+            b = a + 1
+            if sender_cost(a, b) > step:
+                return None
+            while b < j and sender_cost(a, b + 1) <= step:
+                b += 1
+            k, a = k + 1, b
+        return k
+
+    def plan(step):                   # (a, b): the root's run of bands, or None
+        for a in range(nb):
+            # the longest run from a within the step that leaves a band for every sender
+            b = None
+            for e in range(nb, a, -1):
+                if a + (nb - e) >= n - 1 and pre_c[e] - pre_c[a] + unpack_us <= step:
+                    b = e
+                    break
+            if b is None:
+                continue
+            ka, kb = pieces(0, a, step), pieces(b, nb, step)
+            if ka is not None and kb is not None and ka + kb <= n - 1:
+                return a, b           # the senders left over split pieces (never raises the step)
+        return None
+
+    lo, hi = 0.0, pre_c[nb] + unpack_us + pre_b[nb] / link
+    root = plan(hi)
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        r = plan(mid)
+        if r is None:
+            lo = mid
+        else:
+            hi, root = mid, r
+    a, b = root
+    # senders: greedy pieces within the step found, then split until n - 1 pieces
+    step = hi
+
+    def split(i, j):
+        out, s0 = [], i
+        while s0 < j:
+            e = s0 + 1
+            while e < j and sender_cost(s0, e + 1) <= step:
+                e += 1
+            out.append([s0, e])
+            s0 = e
+        return out
+    above, below = split(0, a), split(b, nb)
+    while len(above) + len(below) < n - 1:
+        cand = [(sender_cost(x, y), k, side) for side, lst in ((0, above), (1, below))
+                for k, (x, y) in enumerate(lst) if y - x >= 2]
+        if not cand:
+            raise ValueError("cannot give every rank a band")
+        _, k, side = max(cand)
+        lst = above if side == 0 else below
+        x, y = lst[k]
+        m = (x + y) // 2
+        lst[k:k + 1] = [[x, m], [m, y]]
+    rows = lambda band: min(band * band_rows, height)                        # noqa: E731
+    return [(rows(a), rows(b))] + [(rows(x), rows(y)) for x, y in above + below]
+
+
+def test_balanced_bounds_c_equals_python_restatement():
+    """The C split (xrt_balanced_bounds, used by xrt_render_rows_multi and, through
+    strips.balanced_bounds, by bench.py) gives the same strips as the pure-Python
+    restatement, on random band models of 4-300 bands and 2-8 ranks."""
+    from simpleraytracing_amd.strips import balanced_bounds
+    rng = np.random.default_rng(11)
+    for trial in range(60):
+        nb = int(rng.integers(4, 300))
+        n = int(rng.integers(2, min(nb, 8) + 1))
+        cost = rng.uniform(0.0, 10.0, nb) * (rng.uniform(size=nb) > 0.2)
+        byts = rng.uniform(0.0, 3e5, nb) * (rng.uniform(size=nb) > 0.3)
+        link = float(rng.uniform(1e3, 2e5))
+        H = 32 * nb - int(rng.integers(0, 31))
+        want = _balanced_bounds_py(cost, byts, n, link, H, unpack_us=5.0)
+        got = balanced_bounds(cost, byts, n, link, H, unpack_us=5.0)
+        assert [tuple(x) for x in got] == [tuple(x) for x in want], (trial, got, want)
+
+
 def _link_worker(rank, world, port, out_path):
     import sys
     sys.path.insert(0, ROOT)

@@ -963,6 +963,104 @@ def test_multi_rccl_gather_one_rank(dragon, devices, W, H):
                     assert np.array_equal(bits(x), bits(y))
 
 
+@pytest.mark.parametrize("W,H,n,link", [(4096, 4096, 8, 0.0), (1000, 777, 3, 3.0e4), (512, 512, 4, 1.0e3)])
+def test_multi_balanced_split_rccl_one_rank(dragon, W, H, n, link):
+    """xrt_render_rows_multi with the balanced split (the default): one GPU listed
+    n times, gathered through a one-rank RCCL communicator -- 4096^2 in 8
+    strips is BASELINE configs[3]'s split, planned by the product path itself
+    (device 0's full-frame model, the link measured or given).  The strips are
+    band-aligned, cover the frame, device 0's run may sit anywhere; every frame
+    is bit-equal to one device's frame; the equal split (the reference's rule)
+    still gives the reference's strips and the same frame."""
+    from simpleraytracing_amd.strips import strip_bounds
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        ref = one.render_rows(cam)
+    with xrt.MultiContext([0] * n) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        m.set_gather(xrt.XRT_GATHER_RCCL)
+        m.set_split(xrt.XRT_SPLIT_BALANCED, link)
+        bounds, info = m.plan(cam)
+        assert len(bounds) == n and all(e > b for b, e in bounds)
+        spans = sorted(bounds)
+        assert spans[0][0] == 0 and spans[-1][1] == H and all(b % 32 == 0 for b, _ in spans)
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(n - 1))
+        assert [b for b, _ in bounds[1:]] == sorted(b for b, _ in bounds[1:])     # senders in frame order
+        assert info["frame_span_us"] > 0 and info["predicted_step_us"] > 0
+        assert info["link_bytes_per_us"] == link if link else info["link_bytes_per_us"] > 0
+        assert m.plan(cam)[0] == bounds                        # planned once per geometry
+        for _ in range(3):                                     # the strip buffers rotate
+            got = m.render(cam)
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y))
+            assert got[3].hit_rays == ref[3].hit_rays and got[3].odd_rays == ref[3].odd_rays
+        m.set_split(xrt.XRT_SPLIT_EQUAL)
+        assert m.plan(cam)[0] == [strip_bounds(H, n, g) for g in range(n)]
+        got = m.render(cam)
+        for x, y in zip(got[:3], ref[:3]):
+            assert np.array_equal(bits(x), bits(y))
+
+
+def test_fresh_context_after_two_stream_loop(dragon):
+    """Round 4 saw a fresh context's first host-buffer render wait 13.6-22.7 ms
+    (in its layout upload's synchronisations) right after a frames-in-flight
+    loop on two streams.  Here, run once, the same sequence: 400 frames of
+    2048^2 alternating two streams and two plane sets, then a new context's first
+    xrt_render_rows (list sizing included) -- enqueued within 3 ms, its
+    synchronisations short, and its planes equal to the loop's frames."""
+    import torch
+    W = H = 2048
+    dev = torch.device("cuda", 0)
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    sets = [(torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+             torch.empty(W * H, dtype=torch.uint8, device=dev)) for _ in streams]
+    with xrt.Context(0) as c:
+        c.upload_mesh(dragon)
+        for k in range(400):
+            img, lb, u8 = sets[k % 2]
+            c.render_rows_device(cam, 0, H, img.data_ptr(), lb.data_ptr(), u8.data_ptr(), streams[k % 2].cuda_stream)
+        torch.cuda.synchronize(dev)
+        with xrt.Context(0) as fresh:
+            fresh.upload_mesh(dragon)
+            got = fresh.render_rows(cam)
+            hc = fresh.host_call_ms()
+            again = fresh.render_rows(cam)
+    print("first host-buffer call after the loop:", hc)
+    assert hc["enqueue"] <= 3.0, hc
+    assert hc["of_which_device_sync"] <= 1.0, hc
+    for planes in sets:
+        for x, y in zip(planes, got[:3]):
+            assert np.array_equal(bits(x.cpu().numpy()), bits(y))
+    for x, y in zip(again[:3], got[:3]):
+        assert np.array_equal(bits(x), bits(y))
+
+
+def test_host_buffer_d2h_pieces_exact(dragon):
+    """The pinned-ring D2H of the host-buffer entry points (1-MB pieces, 32 ring
+    slots, copy threads): frames whose planes span many ring rounds (1024 x
+    1531, 3000 x 2000) and a strip that is not a multiple of a piece arrive
+    exactly -- equal to the device planes of the same frame copied by torch."""
+    import torch
+    dev = torch.device("cuda", 0)
+    with xrt.Context(0) as c:
+        c.upload_mesh(dragon)
+        for W, H, r0, r1 in [(1024, 1531, 0, 1531), (3000, 2000, 0, 2000), (777, 555, 13, 500)]:
+            cam = xrt.camera_for_mesh(dragon, W, H)
+            n = (r1 - r0) * W
+            planes = (torch.empty(n, device=dev), torch.empty(n, device=dev), torch.empty(n, dtype=torch.uint8,
+                                                                                           device=dev))
+            c.render_rows_device(cam, r0, r1, *(p.data_ptr() for p in planes), 0)
+            torch.cuda.synchronize(dev)
+            got = c.render_rows(cam, r0, r1)
+            for x, y in zip(planes, got[:3]):
+                assert np.array_equal(bits(x.cpu().numpy()), bits(y)), (W, H)
+            assert c.host_call_ms()["d2h_mb"] == pytest.approx(9 * n / 1e6)
+
+
 def test_multi_device_pipelined(dragon):
     """xrt_render_rows_multi_device: frames enqueued back to back into torch
     device planes (the next frame's strips render while the last one's gather is
@@ -1081,22 +1179,28 @@ def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
         assert np.array_equal(x.cpu().numpy().view(np.uint8), y.cpu().numpy().view(np.uint8))
 
 
-@pytest.mark.parametrize("transit,ranks,share", [("packed", 2, "auto"), ("dense", 2, "auto"),
-                                                  ("packed", 3, "equal"), ("dense", 3, "0.5"),
-                                                  ("packed", 3, "balanced"), ("dense", 2, "balanced"),
-                                                  ("packed", 4, "balanced")])
-def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share):
+@pytest.mark.parametrize("transit,ranks,share,size", [("packed", 2, "auto", 512), ("dense", 2, "auto", 512),
+                                                       ("packed", 3, "equal", 512), ("dense", 3, "0.5", 512),
+                                                       ("packed", 3, "balanced", 512), ("dense", 2, "balanced", 512),
+                                                       ("packed", 4, "balanced", 512),
+                                                       ("packed", 8, "balanced", 4096)])
+def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
     """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
-    packed by region or dense --, expanded there) with 2 ranks on the one GPU
+    packed by region or dense --, expanded there) with 2-8 ranks on the one GPU
     (gloo, host-staged): the gathered frame is bit-equal to rank 0's
-    single-device render."""
+    single-device render.  The 8-rank case is BASELINE configs[3]'s real split
+    (4096^2, 8 strips, balanced, packed), and it also runs the bench's
+    capi_multi leg: the C ABI's xrt_render_rows_multi_device over device 0
+    listed 8 times (one-rank RCCL), bit-equal as well."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     port = 29500 + (os.getpid() % 1000) + (7 if transit == "dense" else 0) + 13 * ranks
+    capi = ranks == 8
     cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(ranks), "--dist-backend", "gloo", "--same-device", "--size", "512", "512",
-           "--steps", "4", "--warmup", "1", "--transit", transit, "--kernel", "binned", "--root-share", share]
+           "--gpus", str(ranks), "--dist-backend", "gloo", "--same-device", "--size", str(size), str(size),
+           "--steps", "4", "--warmup", "1", "--transit", transit, "--kernel", "binned", "--root-share", share,
+           "--loaded-ms", "0", "--capi-multi", "auto" if capi else "off"]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
     if r.returncode != 0:
         print(r.stderr[-6000:])
@@ -1107,20 +1211,76 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share):
     assert d["gather_check"]["bit_exact_vs_single_device_frame"] is True
     g = d["gather_check"]
     rows = g["strip_rows"]
-    assert sum(rows) == 512 and len(rows) == ranks
+    assert sum(rows) == size and len(rows) == ranks
+    if capi:
+        c = d["capi_multi"]
+        assert "error" not in c, c
+        assert c["bit_exact_vs_single_device_frame"] is True and c["devices"] == [0] * 8
+        assert sum(c["strip_rows"]) == size and c["plan"]["predicted_step_us"] > 0
+    else:
+        assert "capi_multi" not in d
     if share == "equal":
         assert max(rows) - min(rows) <= 1
     elif share == "balanced":                     # band-aligned strips, the root's anywhere in the frame
         spans = sorted(map(tuple, g["strips"]))
-        assert spans[0][0] == 0 and spans[-1][1] == 512 and all(s0 % 32 == 0 for s0, _ in spans)
+        assert spans[0][0] == 0 and spans[-1][1] == size and all(s0 % 32 == 0 for s0, _ in spans)
         assert all(spans[i][1] == spans[i + 1][0] for i in range(ranks - 1))
         assert g["split"]["link_bytes_per_us"] > 0 and g["split"]["predicted_step_us"] > 0
     else:
-        assert rows[0] > 512 // ranks
+        assert rows[0] > size // ranks
     if transit == "packed":
         assert g["bytes_gathered_per_step"] < g["dense_bytes_per_step"]
     else:
         assert g["bytes_gathered_per_step"] == g["dense_bytes_per_step"]
+
+
+def test_render_frames_batch_equals_single_calls(dragon):
+    """xrt_render_frames_device: 7 frames of one geometry in ONE call, alternating
+    two plane sets on two streams (each frame prepared and rendered in full) --
+    every set's last frame bit-equal to a single xrt_render_rows; the
+    host-buffer xrt_render_frames likewise, with its per-frame device time."""
+    import torch
+    dev = torch.device("cuda", 0)
+    for W, H, r0, r1 in [(1024, 1024, 0, 1024), (640, 480, 100, 380)]:
+        cam = xrt.camera_for_mesh(dragon, W, H)
+        n = (r1 - r0) * W
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        sets = [(torch.full((n,), -1.0, device=dev), torch.full((n,), -1.0, device=dev),
+                 torch.zeros(n, dtype=torch.uint8, device=dev), s) for s in streams]
+        with xrt.Context(0) as c:
+            c.upload_mesh(dragon)
+            ref = c.render_rows(cam, r0, r1)
+            c.render_frames_device(cam, r0, r1, 7, [(a.data_ptr(), b.data_ptr(), u.data_ptr(), s.cuda_stream)
+                                                    for a, b, u, s in sets])
+            torch.cuda.synchronize(dev)
+            for a, b, u, _ in sets:
+                for x, y in zip((a, b, u), ref[:3]):
+                    assert np.array_equal(bits(x.cpu().numpy()), bits(y)), (W, H)
+            img, lb, u8, st, ms = c.render_frames(cam, 5, r0, r1)
+        for x, y in zip((img, lb, u8), ref[:3]):
+            assert np.array_equal(bits(x), bits(y))
+        assert st.hit_rays == ref[3].hit_rays and ms > 0
+
+
+def test_cli_rows_and_batch(tmp_path):
+    """xrt_main --rows A:B writes only the strip's text rows; --batch N renders the
+    frame N times back to back (xrt_render_frames) and writes the last -- the
+    golden text's rows either way."""
+    exe = os.path.join(ROOT, "simpleraytracing_amd", "lib", "xrt_main")
+    (tmp_path / "out").mkdir()
+    golden = open(os.path.join(GOLDEN, "dragon-128x128-serial.txt"), "rb").read().split(b"\n")
+    for extra, name, want in [(["--rows", "32:96"], "r.txt", b"\n".join(golden[32:96])),
+                              (["--batch", "3", "--time"], "b.txt", b"\n".join(golden)),
+                              (["--rows", "0:17", "--batch", "2"], "rb.txt", b"\n".join(golden[0:17]))]:
+        r = subprocess.run([exe, "-s", "128", "128", "-i", DRAGON, "-f", name, *extra], capture_output=True,
+                           text=True, cwd=tmp_path, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert (tmp_path / "out" / name).read_bytes() == want, extra
+        if "--time" in extra:
+            assert "device time per frame" in r.stdout
+    r = subprocess.run([exe, "-s", "128", "128", "-i", DRAGON, "--rows", "90:40"], capture_output=True, text=True,
+                       cwd=tmp_path, timeout=60)
+    assert r.returncode == 1 and "ERROR" in r.stderr
 
 
 def test_cli_multi_gpu_golden_text(tmp_path):

@@ -79,6 +79,28 @@ def test_render_rows_vs_reference_classes(REF, dragon):
     assert np.array_equal(bits(lb), bits(lb2))
 
 
+def test_reference_spans_threaded_vs_oracle(REF, dragon):
+    """bench.py's "reference" CPU baseline: spans of rows over one shared mesh
+    of the reference's classes on several threads equal the oracle's rows."""
+    W, H = 64, 56
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    rows = [0, 7, 21, 28, 40, 55]
+    img, lb, u8, nh, odd = oracle.render_row_list(dragon, cam, W, H, np.array(rows, np.uint32))
+    r_img, r_lb, r_odd = oracle.ref_render_spans(dragon, cam, W, H, rows, 0, W, threads=4)
+    assert np.array_equal(bits(r_img.ravel()), bits(img)) and np.array_equal(bits(r_lb.ravel()), bits(lb))
+    assert r_odd == odd
+    assert np.array_equal(oracle.lut_u8_array(r_img.ravel()), u8)
+    s_img, s_lb, _ = oracle.ref_render_spans(dragon, cam, W, H, rows, 17, 45, threads=3)
+    assert np.array_equal(bits(s_img), bits(r_img[:, 17:45])) and np.array_equal(bits(s_lb), bits(r_lb[:, 17:45]))
+
+
+def test_lut_array_equals_scalar_formula():
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.uniform(-3.0, 90.0, 20000).astype(np.float32),
+                        np.array([np.nan, np.inf, -np.inf, 0.0, -0.0, 80.0, 0.15686275, 40.0], np.float32)])
+    assert np.array_equal(oracle.lut_u8_array(v), np.array([oracle.lut_u8(x) for x in v], np.uint8))
+
+
 def test_lut_formula():
     assert oracle.lut_u8(80.0) == 255
     assert oracle.lut_u8(0.0) == 0
