@@ -179,6 +179,11 @@ int xrt_render_rows_device(xrt_context* ctx, const xrt_camera* camera, uint32_t 
                            uint32_t row_end, float* d_image, float* d_lbuffer,
                            uint8_t* d_image_u8, void* stream);
 
+/*
+ * Counters and kernel time of the last render.  Enqueues a small reduction
+ * kernel (k_reduce_stats) on that render's stream and waits for it: call it
+ * after a sequence of frames, not between frames in flight.
+ */
 int xrt_read_stats(xrt_context* ctx, xrt_stats* stats);
 
 /*
@@ -212,6 +217,9 @@ int xrt_render_frames(xrt_context* ctx, const xrt_camera* camera, uint32_t row_b
 
 /*
  * Kernel timing over a region of many renders without host synchronisation.
+ * A begin while a region is open ends that region first (its results are
+ * dropped).  The record space is sized from the context's last frame, and
+ * from the region's first frame when that is larger.
  * Every render's waves store their s_memrealtime start and end beside their
  * statistics records (xrt_stats::kernel_ms is the last frame's span: last end -
  * first start).  After xrt_timing_begin, every render keeps its records apart

@@ -152,6 +152,14 @@ void xrt_host_mt_check(const float* det, const float* a, const float* b, const f
 int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16]);
 
 /*
+ * Diagnostics: [0] binned frames rendered with a tile plan (tiles that had no
+ * survivor in an earlier frame of the same geometry store their misses without
+ * reading the region's list), [1] tile plans taken.
+ * XRT_TILE_PLAN=0 in the environment at xrt_create turns the plan off.
+ */
+int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2]);
+
+/*
  * Diagnostics: the phases of the last xrt_destroy, ms: [0] waiting for the
  * context's own work, [1] device frees, [2] pinned host frees, [3] streams and
  * events destroyed.

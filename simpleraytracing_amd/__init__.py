@@ -248,6 +248,12 @@ class Context:
                     "xrt_debug_block_records")
         return out
 
+    def tile_plan_counters(self) -> dict:
+        """Binned frames rendered with a tile plan, tile plans taken (xrt_debug_tile_plan)."""
+        c = (ctypes.c_uint64 * 2)()
+        self._check(self._lib.xrt_debug_tile_plan(self._ctx, c), "xrt_debug_tile_plan")
+        return {"frames": int(c[0]), "plans": int(c[1])}
+
     def pipeline_counters(self) -> dict:
         """Frames rendered from a preparation made ahead, preparations dropped, renders
         launched with no wait, renders launched after a host wait (xrt_debug_pipeline_counters)."""

@@ -148,6 +148,7 @@ XRT_SYMBOLS = {
     "xrt_debug_pipeline_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_host_call_ms": (ctypes.c_int, [_CtxP, _dp]),
     "xrt_debug_destroy_ms": (ctypes.c_int, [_dp]),
+    "xrt_debug_tile_plan": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_wave_times": (ctypes.c_int, [_CtxP, _u32, ctypes.POINTER(_u32), _u64, ctypes.POINTER(_u64)]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),

@@ -1335,6 +1335,13 @@ constexpr uint32_t kBinQueue = XRT_BIN_QUEUE;  // passing (region, triangle) pai
 #endif
 constexpr uint32_t kRankCache = XRT_PREP_RANK_LDS;
 static_assert(kRankCache % 64u == 0u, "whole DMA rounds");
+// k_prep's commit through buffer instructions (range-checked, no per-lane
+// branches around the memory ops; 0: plain guarded loads and atomics)
+#ifndef XRT_PREP_BUFFER_OPS
+#define XRT_PREP_BUFFER_OPS 1
+#endif
+constexpr int kBufferWord3 = 0x00020000;          // raw buffer resource, gfx9 family (32-bit elements)
+constexpr uint32_t kBufferOut = 0x80000000u;      // an offset past every buffer: no-op access
 
 // Counters and lists are indexed by launch slot, not by region: the render
 // wave of slot s loads its count and list without first looking up which
@@ -1371,7 +1378,14 @@ __device__ __forceinline__ const_ptr<T> as_const(const T* p)
 // (x, y) = (xy & 0xFFFF, xy >> 16).  A tile wave reads it with ONE
 // s_load_dwordx4 beside its count -- no dependent reads before its DMA.
 struct SlotDesc {
-    uint32_t base, cap, xy, pad;
+    uint32_t base, cap, xy;
+    // Tile plan: bit t = tile t of the region had a survivor in the frame the
+    // plan was taken from (k_tile_plan; 0xFFFF = every tile live).  The cull of
+    // a frame geometry is deterministic -- the same footprints join the same
+    // region lists and pass the same tiles -- so a tile without a survivor in
+    // one frame has none in any frame of that geometry, and the render stores
+    // its misses without reading its region's list (BinBuffers::tile_plan).
+    uint32_t live;
 };
 static_assert(sizeof(SlotDesc) == 16, "SlotDesc must be 16 bytes");
 
@@ -1396,6 +1410,9 @@ struct BinBuffers {
     // or a triangle into the global list, [1] = 1 when a region's count passes
     // its list's capacity.  Null: nothing to check.
     uint32_t* plan_miss;
+    // 1: this frame's geometry is the one its layout's tile plan was taken for
+    // (SlotDesc::live may skip tiles); 0: every tile renders.
+    uint32_t tile_plan;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -1405,7 +1422,7 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 // statement, so the compiler cannot put the count load behind a branch that
 // consumes the description (two serial round trips).  slot is wave-uniform.
 __device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot, uint32_t& count, uint32_t& base,
-                                          uint32_t& cap, uint32_t& xy)
+                                          uint32_t& cap, uint32_t& xy, uint32_t& live)
 {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t* count_addr = bins.counts + (size_t)slot * kCounterStride;
@@ -1422,6 +1439,7 @@ __device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot,
     base = d.x;
     cap = d.y;
     xy = d.z;
+    live = d.w;
 }
 
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
@@ -1632,6 +1650,16 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     // No lists (the sizing pass of a new geometry, DESIGN.md "List sizing"):
     // the pairs are counted, nothing is stored, nothing can overflow.
     const uint32_t count_only = wave_uniform(bins.list == nullptr ? 1u : 0u);
+#if XRT_PREP_BUFFER_OPS
+    // the commit's tables as buffers (range-checked: kBufferOut is past all of them)
+    const uint32_t n_regions = bins.regions_x * bins.regions_y;
+    const __amdgpu_buffer_rsrc_t r_rank =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bins.rank), 0, (int)(n_regions * 4u), kBufferWord3);
+    const __amdgpu_buffer_rsrc_t r_cnt =
+        __builtin_amdgcn_make_buffer_rsrc(bins.counts, 0, (int)(n_regions * kCounterStride * 4u), kBufferWord3);
+    const __amdgpu_buffer_rsrc_t r_desc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<SlotDesc*>(bins.desc), 0, (int)(n_regions * (uint32_t)sizeof(SlotDesc)), kBufferWord3);
+#endif
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
     bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
@@ -1644,6 +1672,33 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 #endif
         for (uint32_t base = 0; base < queued; base += 64u * kBinBatch) {
             uint32_t reg[kBinBatch], own[kBinBatch], slot[kBinBatch];
+#if XRT_PREP_BUFFER_OPS
+            // Buffer loads and atomics with an out-of-range offset for the lanes
+            // without a pair (a load returns 0, an atomic does nothing): no
+            // exec-masked branch around each memory op, so the round's four
+            // slot loads issue back to back, then its four count atomics and four
+            // list descriptions -- two memory round trips a round.  (The guarded
+            // form compiled to a wait after every load and every atomic: eight.)
+            bool val[kBinBatch];
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
+                const uint32_t q = base + b * 64u + lane;
+                val[b] = q < queued;
+                const uint32_t qq = q < kBinQueue ? q : kBinQueue - 1u;   // in the array; ignored unless val
+                reg[b] = s_qreg[wave][qq];
+                own[b] = s_qown[wave][qq];
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
+#if XRT_PREP_RANK_LDS
+                if (cached) reg[b] = val[b] ? s_rank[wave][reg[b]] : kEmpty;
+                else
+#endif
+                reg[b] = __builtin_amdgcn_raw_buffer_load_b32(r_rank, val[b] ? reg[b] * 4u : kBufferOut, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) reg[b] = val[b] ? reg[b] : kEmpty;
+#else
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 const uint32_t q = base + b * 64u + lane;
@@ -1658,12 +1713,26 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                     own[b] = s_qown[wave][q];
                 }
             }
+#endif
             bool planned_empty = false;            // a pair for a region the fill plan fills
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) planned_empty |= reg[b] != kEmpty && reg[b] >= bins.tile_slots;
             if (__builtin_expect(bins.plan_miss != nullptr && __ballot(planned_empty) != 0ull, 0) && lane == 0)
                 *bins.plan_miss = 1u;
             uint32_t lbase[kBinBatch], lcap[kBinBatch];
+#if XRT_PREP_BUFFER_OPS
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b)
+                slot[b] = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+                    1, r_cnt, reg[b] != kEmpty ? reg[b] * (kCounterStride * 4u) : kBufferOut, 0, 0);
+#pragma unroll
+            for (uint32_t b = 0; b < kBinBatch; ++b) {
+                const auto bc = __builtin_amdgcn_raw_buffer_load_b64(
+                    r_desc, reg[b] != kEmpty && count_only == 0u ? reg[b] * (uint32_t)sizeof(SlotDesc) : kBufferOut, 0, 0);
+                lbase[b] = bc[0];
+                lcap[b] = bc[1];
+            }
+#else
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
@@ -1672,6 +1741,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 lbase[b] = bc.x;
                 lcap[b] = bc.y;
             }
+#endif
             if (count_only) continue;              // the sizing pass: counts only
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
@@ -1917,8 +1987,8 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
 {
     const uint32_t lane = threadIdx.x & 63u;
     // the slot's count (k_prep) and description (host): two scalar loads in flight together
-    uint32_t n_local, d_base, d_cap, d_xy;
-    load_slot(bins, slot, n_local, d_base, d_cap, d_xy);
+    uint32_t n_local, d_base, d_cap, d_xy, d_live;
+    load_slot(bins, slot, n_local, d_base, d_cap, d_xy, d_live);
     const uint32_t reg_x = d_xy & 0xFFFFu, reg_y = d_xy >> 16;
     const RegionEntry* __restrict__ local = bins.list + d_base;
     const RegionEntry* __restrict__ glob = bins.global_list;
@@ -1943,6 +2013,9 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
         if (split != kSplitNone) __syncthreads();  // the pair's one barrier (workgroup-uniform count)
         return;
     }
+    // a tile the geometry's tile plan found without survivors: its misses,
+    // without reading the region's list (exact: SlotDesc::live)
+    const bool planned_dead = !kSigned && bins.tile_plan && split == kSplitNone && !((d_live >> tile) & 1u);
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction
@@ -1954,7 +2027,7 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
     typename std::conditional<kSigned, SignedHits, HitList>::type hl;
     hl.init();
     uint32_t tests = 0;
-    for (uint32_t base = 0; base < n_cand; base += kBinStage) {
+    for (uint32_t base = 0; base < (planned_dead ? 0u : n_cand); base += kBinStage) {
         // the round's footprints, kRoundSlots per lane, all loads in flight together
         float4 f[kRoundSlots][4];
         uint32_t id[kRoundSlots];
@@ -2155,6 +2228,26 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
+}
+
+// ---------------------------------------------------------------------------
+// k_tile_plan: a geometry's tile plan (SlotDesc::live) from the statistics
+// records of one of its binned renders -- bit t of slot s = tile t tested a
+// survivor (record s * 16 + t).  Slots [first, end): the tile regions past the
+// split ones (a split tile's two waves keep one record, every split tile
+// stays live).  Renders in flight may read `live` while it is written: either
+// value is exact for the geometry.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tile_plan(const BlockStats* __restrict__ recs, SlotDesc* __restrict__ desc,
+                                                  uint32_t first, uint32_t end)
+{
+    const uint32_t s = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= end) return;
+    uint32_t live = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kWavesPerRegion; ++t)
+        live |= (recs[(size_t)s * kWavesPerRegion + t].tile_tests != 0u ? 1u : 0u) << t;
+    desc[s].live = live;
 }
 
 // ---------------------------------------------------------------------------

@@ -260,6 +260,9 @@ struct SlotLayout {
 // waits for any (xrt_render_rows_multi).
 struct PendingFrame {
     FrameSet* fs = nullptr;
+    // the frame renders the current geometry (bin_key) over its compact
+    // layout and fill plan: its records can give the tile plan
+    bool plan_source = false;
     hipStream_t stream = nullptr;
     hipEvent_t prep_done = nullptr;    // k_prep complete (prep stream)
     // The host waits for prep_done and reads k_prep's check before the launch
@@ -315,6 +318,12 @@ struct xrt_context {
     uint32_t split_min = kSplitAuto;   // kSplitAuto: the rule above
     uint32_t wave_slots = 0;           // the device's CUs x 32 (render waves resident at full occupancy)
     bool plan_valid = false;
+    // Tile plan (SlotDesc::live): 0 = the compact layout's tiles all live (as
+    // uploaded), 1 = k_tile_plan ran after a render of the current geometry
+    // (bin_key) with its fill plan.  XRT_TILE_PLAN=0 turns it off.
+    bool tile_plan_enabled = true;
+    int tile_plan_state = 0;
+    uint64_t hp_tile_plan_frames = 0, hp_tile_plans = 0;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
     uint64_t packed_cap = 0;           // xrt_set_transit_layout: the packed L-buffer's floats (0: row-major)
 
@@ -810,7 +819,7 @@ int upload_layout(xrt_context* ctx, SlotLayout& L, uint32_t rx, uint32_t ry, std
     std::vector<uint32_t> rank(n);
     for (size_t s = 0; s < n; ++s) {
         const uint32_t r = slot_region[s];
-        desc[s] = SlotDesc{base[s], cap[s], (r % rx) | ((r / rx) << 16), 0u};
+        desc[s] = SlotDesc{base[s], cap[s], (r % rx) | ((r / rx) << 16), 0xFFFFu};   // every tile live
         rank[r] = (uint32_t)s;
     }
     // Frames in flight may read the old layout: wait for them, but only when
@@ -1022,6 +1031,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.tile_slots = n_regions;
         if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+        bins.tile_plan = compact && fill_ok && !reuse && !sizing && ctx->plan_valid && ctx->tile_plan_state == 1 ? 1u : 0u;
         if (sizing) prof_mark(ctx, "fixed layout upload");
         // the fill plan's test hook (every region planned empty) is checked every frame
         arm_plan_check(fs, n_regions, bins, reuse, ctx->fill_plan == 2);
@@ -1092,6 +1102,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if (run > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "region lists exceed 2^32 entries");
         prof_mark(ctx, "plan (host)");
         if ((rc = upload_layout(ctx, ctx->compact_layout, rx, ry, std::move(slot_region), base, cap))) return rc;
+        ctx->tile_plan_state = 0;                  // the new layout's tiles are all live
         prof_mark(ctx, "compact layout upload");
         ctx->acc_ms[1] += std::chrono::duration<double, std::milli>(HostClock::now() - t_sizing).count();
         ctx->plan_tile_slots = tile_slots;
@@ -1124,6 +1135,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     fs.binned = binned;
     out.block_stats = fs.block_stats;
     pf.fs = &fs;
+    pf.plan_source = binned && fill_ok && !reuse && ctx->compact && ctx->plan_valid && !ctx->bin_force_cap &&
+                     bins.desc == ctx->compact_layout.d_desc && bins.tile_slots == ctx->plan_tile_slots;
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
     pf.host_wait = bins.plan_miss != nullptr;
@@ -1218,6 +1231,11 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         // the next frame re-sizes its lists.
         ++(fs.plan_flag[1] != 0u ? ctx->hp_overflow : ctx->hp_plan_miss);
         bins.tile_slots = rx * ry;
+        bins.tile_plan = 0u;
+        pf.plan_source = false;
+        // an overflowed list renders its region from the whole mesh: as ordinary
+        // tiles (split tiles only ever merge list-rendered halves)
+        if (fs.plan_flag[1] != 0u) bins.split_slots = 0u;
         grid = dim3(kWavesPerRegion / kTileWaves * (bins.tile_slots + bins.split_slots));
         ctx->bin_key_valid = false;
     }
@@ -1237,6 +1255,20 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     out.wave_times = fs.times;
     hipEvent_t t0 = nullptr, t1 = fs.done;
     const uint64_t frame_in_region = ctx->timing ? ctx->timed_frames++ : 0;
+    if (ctx->timing && rows > 0 && frame_in_region == 0 &&
+        ctx->timing_space < std::min(kTimingRecords, kTimingFrames * (size_t)fs.n_blocks)) {
+        // the region's first frame is larger than the space xrt_timing_begin
+        // sized from the context's previous frame (or there was none): room for
+        // kTimingFrames of these, before any record of the region is kept
+        const size_t space = std::min(kTimingRecords, kTimingFrames * (size_t)fs.n_blocks);
+        XRT_HIP(ctx, hipStreamSynchronize(stream));
+        for (auto& c : ctx->tchunks) (void)hipFree(c.p);
+        ctx->tchunks.clear();
+        xrt_context::TimesChunk c = {nullptr, space, 0};
+        XRT_HIP(ctx, hipMalloc(&c.p, space * sizeof(uint2)));
+        ctx->tchunks.push_back(c);
+        ctx->timing_space = space;
+    }
     if (ctx->timing && rows > 0 && ctx->timed_records + fs.n_blocks <= ctx->timing_space) {
         ctx->timed_records += fs.n_blocks;
         uint2* slot = nullptr;
@@ -1275,6 +1307,19 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         if (ctx->host_profile) ctx->hp_lrender += seconds_since(t_launch);
         fs.done_ev = t1;
         fs.done_valid = true;
+        if (binned && bins.tile_plan) ++ctx->hp_tile_plan_frames;
+        // The geometry's tile plan from this render's records, once (behind
+        // the render on its stream; frames in flight read either value, both
+        // exact for the geometry).
+        if (binned && !sgn && pf.plan_source && ctx->tile_plan_enabled && ctx->tile_plan_state == 0 &&
+            bins.tile_slots > bins.split_slots) {
+            const uint32_t n = bins.tile_slots - bins.split_slots;
+            hipLaunchKernelGGL(k_tile_plan, dim3((n + 255) / 256), dim3(256), 0, stream, fs.block_stats,
+                               ctx->compact_layout.d_desc, bins.split_slots, bins.tile_slots);
+            XRT_HIP(ctx, hipGetLastError());
+            ctx->tile_plan_state = 1;
+            ++ctx->hp_tile_plans;
+        }
     }
     if (ctx->host_profile) {
         ctx->hp_total += seconds_since(t_call);
@@ -1468,6 +1513,7 @@ int xrt_create(int device, xrt_context** out)
     ctx->device = device;
     const char* hp = std::getenv("XRT_HOST_PROFILE");
     ctx->host_profile = hp && std::atoi(hp) != 0;
+    if (const char* tp = std::getenv("XRT_TILE_PLAN")) ctx->tile_plan_enabled = std::atoi(tp) != 0;
     const char* sp = std::getenv("XRT_SIZING_PROFILE");
     ctx->sizing_profile = sp ? std::atoi(sp) : 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -1919,6 +1965,14 @@ int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16])
     return XRT_OK;
 }
 
+int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2])
+{
+    if (!ctx || !counters) return XRT_ERR_ARGUMENT;
+    counters[0] = ctx->hp_tile_plan_frames;
+    counters[1] = ctx->hp_tile_plans;
+    return XRT_OK;
+}
+
 int xrt_debug_pipeline_counters(xrt_context* ctx, uint64_t counters[4])
 {
     if (!ctx || !counters) return XRT_ERR_ARGUMENT;
@@ -2081,6 +2135,11 @@ int xrt_read_stats(xrt_context* ctx, xrt_stats* stats)
 int xrt_timing_begin(xrt_context* ctx)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
+    if (ctx->timing) {                 // a region still open: end it (its results are dropped)
+        double ms = 0.0;
+        uint64_t n = 0;
+        if (int rc = xrt_timing_end(ctx, &ms, &n)) return rc;
+    }
     // Frames in flight may mark their completion with events of the previous
     // timed region, which this one re-records: wait for them first.
     for (FrameSet& fs : ctx->sets) {

@@ -1061,6 +1061,96 @@ def test_host_buffer_d2h_pieces_exact(dragon):
             assert c.host_call_ms()["d2h_mb"] == pytest.approx(9 * n / 1e6)
 
 
+@pytest.mark.parametrize("W,H,r0,r1", [(2048, 2048, 0, 2048), (1000, 777, 0, 777), (4096, 4096, 1024, 2080),
+                                       (333, 517, 100, 400)])
+def test_tile_plan_frames_exact(dragon, W, H, r0, r1):
+    """The tile plan (SlotDesc::live from one render's records): later frames of
+    the same geometry store the misses of the tiles that had no survivor
+    without reading their region's list -- every such frame bit-equal to a
+    brute-force render; a camera change re-plans, and the old plan is not used."""
+    cams = [xrt.camera_for_mesh(dragon, W, H), xrt.camera_from_bbox(*oracle.bbox(dragon[:7000]), W, H)]
+    with xrt.Context(0) as brute:
+        brute.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        brute.upload_mesh(dragon)
+        refs = [brute.render_rows(c, r0, r1) for c in cams]
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        for k in range(8):
+            ci = (k // 4) % 2
+            got = c.render_rows(cams[ci], r0, r1)
+            for x, y in zip(got[:3], refs[ci][:3]):
+                assert np.array_equal(bits(x), bits(y)), (k, ci)
+        counters = c.tile_plan_counters()
+    assert counters["plans"] == 2 and counters["frames"] >= 4, counters
+
+
+def test_split_tiles_with_packed_transit_exact(dragon, monkeypatch):
+    """Split tiles (XRT_SPLIT_MIN=1: every non-empty region) rendered straight
+    into the packed transit layout of a strip (xrt_set_transit_layout) and
+    unpacked: equal to the strip's direct render (round-4 advice: the split
+    halves' merge was pinned only for row-major planes)."""
+    import torch
+    monkeypatch.setenv("XRT_SPLIT_MIN", "1")
+    W, H, r0, r1 = 1024, 1024, 256, 768
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    rows = r1 - r0
+    dev = torch.device("cuda", 0)
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        ref = c.render_rows(cam, r0, r1)
+        stream = torch.cuda.current_stream(dev)
+        c.set_miss_code(xrt._abi.XRT_MISS_TRANSIT)
+        lb = torch.zeros(W * rows, device=dev)
+        c.render_rows_device(cam, r0, r1, 0, lb.data_ptr(), 0, stream.cuda_stream)
+        rmap, n_packed = c.plan_region_map(W, rows)
+        packed = torch.full((max(n_packed, 1) * 1024,), -3.0, device=dev)
+        c.set_transit_layout(packed.numel())
+        for _ in range(3):                            # the sizing frame's plan, then steady frames
+            c.render_rows_device(cam, r0, r1, 0, packed.data_ptr(), 0, stream.cuda_stream)
+        c.set_transit_layout(0)
+        c.set_miss_code(0)
+        d_map = torch.from_numpy(rmap.view(np.int32)).to(dev)
+        out = [torch.zeros(W * rows, device=dev), torch.zeros(W * rows, device=dev),
+               torch.zeros(W * rows, dtype=torch.uint8, device=dev)]
+        c.unpack_regions_device(W, rows, d_map.data_ptr(), packed.data_ptr(), out[0].data_ptr(), out[1].data_ptr(),
+                                out[2].data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+    assert n_packed < len(rmap)
+    assert np.array_equal(bits(out[1].cpu().numpy()), bits(ref[0]))
+    assert np.array_equal(bits(out[0].cpu().numpy()), bits(ref[1]))
+    assert np.array_equal(out[2].cpu().numpy(), ref[2])
+
+
+def test_timing_region_before_any_frame_and_twice(dragon):
+    """xrt_timing_begin on a fresh context (no frame yet to size the record
+    space from) keeps every frame of a region of 2048^2 frames; a second begin
+    while a region is open ends it first."""
+    import torch
+    W = H = 2048
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    dev = torch.device("cuda", 0)
+    planes = [torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+              torch.empty(W * H, dtype=torch.uint8, device=dev)]
+    with xrt.Context(0) as c:
+        c.upload_mesh(dragon)
+        c.timing_begin()
+        for _ in range(40):
+            c.render_rows_device(cam, 0, H, *(p.data_ptr() for p in planes), 0)
+        ms, n = c.timing_end()
+        assert n == 40 and ms > 0
+        c.timing_begin()
+        for _ in range(3):
+            c.render_rows_device(cam, 0, H, *(p.data_ptr() for p in planes), 0)
+        c.timing_begin()                              # the open region ends, a new one starts
+        for _ in range(5):
+            c.render_rows_device(cam, 0, H, *(p.data_ptr() for p in planes), 0)
+        ms2, n2 = c.timing_end()
+        assert n2 == 5 and ms2 > 0
+        assert c.read_stats().kernel_ms > 0
+
+
 def test_multi_device_pipelined(dragon):
     """xrt_render_rows_multi_device: frames enqueued back to back into torch
     device planes (the next frame's strips render while the last one's gather is

@@ -39,7 +39,7 @@ for c in "${CONFIGS[@]}"; do
     timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/${name}_pmc/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --ramp-ms 0 --no-timing-check $base $short > /dev/null 2> $OUT/${name}_pmc$i.err || exit 1
   done
   python3 tools/pmc_summary.py $OUT/${name}_pmc > $OUT/pmc_summary_${name}.txt || exit 1
-  python3 tools/make_traffic_json.py $OUT/${name}_pmc/summary.json "binned:$key" --kernel "k_render_binned<false>" > /dev/null || exit 1
+  python3 tools/make_traffic_json.py $OUT/${name}_pmc/summary.json "binned:$key" --kernel "k_render_binned<false>" --source-as profiles/$TAG/pmc_summary_${name}.json > /dev/null || exit 1
   echo "[$name] bench"
   timeout -k 10 300 python bench.py --no-cpu-baseline $args > $OUT/bench_${name}.json 2> $OUT/bench_${name}.err || exit 1
   python3 -c "import json; d=json.load(open('$OUT/bench_${name}.json')); r=d['roofline']; print('$name', 'Mrays/s %.0f'%d['value'], 'ms/step %.4f'%d['ms_per_step'], 'kernel_ms %.4f'%r['avg_kernel_ms'], r['bound'], 'frac %.3f'%r['frac'])"

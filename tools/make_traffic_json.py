@@ -17,7 +17,11 @@ import os
 import sys
 
 src, key = sys.argv[1], sys.argv[2]
-kname = sys.argv[4] if len(sys.argv) > 4 and sys.argv[3] == "--kernel" else "k_render_" + key.split(":")[0]
+opts = dict(zip(sys.argv[3::2], sys.argv[4::2]))
+kname = opts.get("--kernel", "k_render_" + key.split(":")[0])
+# --source-as: the tracked copy the record cites (profiles/<round>/pmc_summary_<config>.json),
+# where the summary is copied from gpurun_out/ (scratch) after the run
+source = opts.get("--source-as", os.path.relpath(src))
 summ = json.load(open(src))
 row = next(v for k, v in summ.items() if k.endswith("::" + kname))
 out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
@@ -36,7 +40,7 @@ data[key] = {
     "valu_wave_instr_per_launch": row.get("SQ_INSTS_VALU"),
     "salu_instr_per_launch": row.get("SQ_INSTS_SALU"),
     "waves_per_launch": row.get("SQ_WAVES"),
-    "source": os.path.relpath(src),
+    "source": source,
 }
 json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
 print(json.dumps(data[key]))
