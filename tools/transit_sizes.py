@@ -9,18 +9,19 @@ largest sender transfer) -- the gather of frame k overlaps the render of frame
 k+1, each sender has its own link into rank 0 (DESIGN.md "Multi-GPU").
 
     python tools/transit_sizes.py [--size W H] [--tile-mesh n] [--ranks 1 2 4 8] [--link-gbs 64 128]
-                                  [--splits weighted equal balanced]
+                                  [--splits weighted equal balanced capi] [--ramp-ms 50]
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def strip_time_ms(xrt, torch, tris, cam, r0, r1, W, frames, miss_code):
+def strip_time_ms(xrt, torch, tris, cam, r0, r1, W, frames, miss_code, ramp_ms=0.0):
     dev = torch.device("cuda", 0)
     with xrt.Context(0) as ctx:
         ctx.upload_mesh(tris)
@@ -34,13 +35,20 @@ def strip_time_ms(xrt, torch, tris, cam, r0, r1, W, frames, miss_code):
         for _ in range(5):
             ctx.render_rows_device(cam, r0, r1, *args, 0)
         torch.cuda.synchronize()
+        if ramp_ms > 0:                     # loaded clocks (DESIGN.md "Measurement"): keep the GPU busy first
+            t0 = time.perf_counter()
+            while (time.perf_counter() - t0) * 1e3 < ramp_ms:
+                for _ in range(20):
+                    ctx.render_rows_device(cam, r0, r1, *args, 0)
+                torch.cuda.synchronize()
         ctx.timing_begin()
         for _ in range(frames):
             ctx.render_rows_device(cam, r0, r1, *args, 0)
         torch.cuda.synchronize()
         ms, n = ctx.timing_end()
         _, n_packed = ctx.plan_region_map(W, r1 - r0)
-    return ms / max(n, 1), n_packed
+        hit_rays = ctx.read_stats().hit_rays
+    return ms / max(n, 1), n_packed, hit_rays
 
 
 def main():
@@ -50,7 +58,10 @@ def main():
     ap.add_argument("--link-gbs", type=float, nargs="+", default=[64.0, 128.0])
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--tile-mesh", type=int, default=1, help="n x n tiled copies (7 = BASELINE configs[4])")
-    ap.add_argument("--splits", nargs="+", default=["weighted", "equal", "balanced"])
+    ap.add_argument("--splits", nargs="+", default=["weighted", "equal", "balanced", "capi"],
+                    help="balanced: bench.py's band model through strips.balanced_bounds; capi: the strips the C "
+                         "ABI's xrt_multi_plan picks itself (its own frame model), both per --link-gbs")
+    ap.add_argument("--ramp-ms", type=float, default=50.0, help="GPU kept busy with the strip before timing it")
     args = ap.parse_args()
     import torch
     import simpleraytracing_amd as xrt
@@ -68,22 +79,37 @@ def main():
     splits = [s for s in ("weighted", "equal") if s in args.splits]
     if "balanced" in args.splits:
         splits += [f"balanced@{g:g}" for g in args.link_gbs]
+    if "capi" in args.splits:
+        splits += [f"capi@{g:g}" for g in args.link_gbs]
     for split in splits:
         for n in args.ranks:
             if split != "weighted" and n == 1:
                 continue
             share0 = root_share(n)
+            plan = None
             if split.startswith("balanced@"):
                 link = float(split.split("@")[1]) * 1e3           # GB/s -> bytes/us
                 bounds = balanced_bounds(band_cost, band_bytes, n, link, H)
+            elif split.startswith("capi@"):                       # the product path's own plan
+                link = float(split.split("@")[1]) * 1e3
+                with xrt.MultiContext([0] * n) as m:
+                    m.set_kernel(xrt.XRT_KERNEL_BINNED)
+                    m.upload_mesh(tris)
+                    m.set_split(xrt.XRT_SPLIT_BALANCED, link)
+                    bounds, plan = m.plan(cam)
             else:
                 bounds = [weighted_bounds(H, n, g, share0) if split == "weighted" else strip_bounds(H, n, g)
                           for g in range(n)]
             ranks = []
             for g, (r0, r1) in enumerate(bounds):
-                ms, n_packed = strip_time_ms(xrt, torch, tris, cam, r0, r1, W, args.frames, miss_code=g > 0)
+                ms, n_packed, hit_rays = strip_time_ms(xrt, torch, tris, cam, r0, r1, W, args.frames,
+                                                       miss_code=g > 0, ramp_ms=args.ramp_ms)
+                # hit_only_bytes: what a hit-only transit would send (a 64-bit mask per 8x8 tile of the
+                # packed regions + 4 B per hit pixel) -- an estimate, not a built layout
                 ranks.append({"rows": r1 - r0, "render_us": round(ms * 1e3, 2),
-                              "packed_bytes": 4096 * n_packed if g else 0, "dense_bytes": 4 * (r1 - r0) * W if g else 0})
+                              "packed_bytes": 4096 * n_packed if g else 0, "dense_bytes": 4 * (r1 - r0) * W if g else 0,
+                              "hit_rays": hit_rays,
+                              "hit_only_bytes": 4 * hit_rays + 8 * 16 * n_packed if g else 0})
             senders = ranks[1:]
             unpack_us = 0.0 if n == 1 else 5.0       # one k_unpack_blocks launch (measured ~5 us at 4096^2)
             pred = {}
@@ -93,8 +119,8 @@ def main():
                            transfer)
                 pred[f"{gbs:g}GBs"] = {"step_us": round(step, 1), "transfer_us": round(transfer, 1),
                                        "mrays_s": round(W * H / step, 0) if step else None}
-            out[f"{split}_{n}"] = {"ranks": ranks, "bounds": bounds, "predicted": pred}
-    print(json.dumps({"image": [W, H], "triangles": len(tris), "splits": out}))
+            out[f"{split}_{n}"] = {"ranks": ranks, "bounds": bounds, "predicted": pred, "plan": plan}
+    print(json.dumps({"image": [W, H], "triangles": len(tris), "ramp_ms": args.ramp_ms, "splits": out}))
 
 
 if __name__ == "__main__":
