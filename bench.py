@@ -77,9 +77,10 @@ def parse():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
                          "N ranks on fewer GPUs")
-    ap.add_argument("--transit", choices=["packed", "dense"], default="packed",
-                    help="strips mode: send the regions the strip's fill plan did not fill (packed) or the "
-                         "whole L-buffer strip (dense)")
+    ap.add_argument("--transit", choices=["hits", "packed", "dense"], default="hits",
+                    help="strips mode: send per tile of the strip's fill plan a hit mask and the hit rays' L "
+                         "values (hits), the regions the fill plan did not fill (packed) or the whole L-buffer "
+                         "strip (dense)")
     ap.add_argument("--root-share", default="balanced",
                     help="strips mode: 'balanced' (default): strips from the frame's measured per-band render "
                          "cost and packed bytes and the measured link rate (strips.balanced_bounds); or the "
@@ -296,11 +297,12 @@ def end_to_end(args, W, H, device_index, kernel):
     return out
 
 
-def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32):
+def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32, transit="packed"):
     """Inputs of strips.balanced_bounds from one binned render of the whole frame
     (rank 0, untimed): per band of 32 rows, its share of the render (the waves'
     in-kernel timing records, scaled to the frame's span, in us) and the bytes
-    its packed strip sends (a 32x32 block per region the fill plan leaves)."""
+    its strip sends -- packed: a 32x32 block per region the fill plan leaves;
+    hits: per such region 16 tile masks (8 B each) and 4 B per hit ray."""
     import numpy as np
     dev = torch.device("cuda", device_index)
     img = torch.empty(W * H, dtype=torch.float32, device=dev)
@@ -316,6 +318,7 @@ def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32):
         t = c.wave_times().astype(np.int64)
         span_us = c.read_stats().kernel_ms * 1e3
         rmap, n_packed = c.plan_region_map(W, H)
+        tile_hits = c.plan_hit_layout()[0] if transit == "hits" else None
     rx, ry = -(-W // 32), -(-H // 32)
     dur = ((t[:, 1] - t[:, 0]) % 2**32).astype(np.float64)         # ticks, per statistics record
     per_slot = dur.reshape(-1, 16).sum(axis=1)                       # 16 records per region slot
@@ -326,7 +329,13 @@ def band_model(xrt, torch, tris, cam, W, H, device_index, band_rows=32):
         region_cost[~unfilled] = per_slot[n_packed:].sum() / (~unfilled).sum()
     band_wave = region_cost.reshape(ry, rx).sum(axis=1)
     band_cost = band_wave / max(band_wave.sum(), 1e-9) * span_us
-    band_bytes = 4096.0 * unfilled.reshape(ry, rx).sum(axis=1)
+    if tile_hits is not None:
+        region_bytes = np.zeros(rx * ry)
+        slot_bytes = 128.0 + 4.0 * tile_hits.reshape(-1, 16).sum(axis=1)
+        region_bytes[unfilled] = slot_bytes[rmap[unfilled].astype(np.int64)]
+        band_bytes = region_bytes.reshape(ry, rx).sum(axis=1)
+    else:
+        band_bytes = 4096.0 * unfilled.reshape(ry, rx).sum(axis=1)
     return band_cost, band_bytes, span_us
 
 
@@ -551,6 +560,8 @@ def capi_multi_only(args) -> int:
         if distinct == 1 and len(devices) > 1:
             m.set_gather(xrt.XRT_GATHER_RCCL)          # one-rank communicator: the RCCL calls on one GPU
         m.set_split(xrt.XRT_SPLIT_BALANCED if args.capi_split == "balanced" else xrt.XRT_SPLIT_EQUAL)
+        # (--transit dense has no C-ABI counterpart: the blocks of the fill plan)
+        m.set_transit(xrt.XRT_TRANSIT_HITS if args.transit == "hits" else xrt.XRT_TRANSIT_PACKED)
         t_p = time.perf_counter()
         bounds, info = m.plan(cam)
         plan_ms = (time.perf_counter() - t_p) * 1e3
@@ -568,6 +579,7 @@ def capi_multi_only(args) -> int:
         s.synchronize()
         dt = time.perf_counter() - t0
         st = m.read_stats()
+        transit = m.transit_stats()
     ok = (np.array_equal(img.cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
           and np.array_equal(lb.cpu().numpy().view(np.uint32), ref[1].view(np.uint32))
           and np.array_equal(u8.cpu().numpy(), ref[2]))
@@ -578,7 +590,9 @@ def capi_multi_only(args) -> int:
            "split": args.capi_split, "strips": bounds, "strip_rows": [e - b for b, e in bounds],
            "plan": info, "plan_ms": plan_ms, "steps": args.steps, "warmup": max(args.warmup, 1),
            "ms_per_step": dt / args.steps * 1e3, "value": W * H * args.steps / dt / 1e6, "unit": "Mrays/s",
-           "hit_rays": st.hit_rays, "bit_exact_vs_single_device_frame": bool(ok)}
+           "hit_rays": st.hit_rays, "transit": "hits" if args.transit == "hits" else "packed",
+           "bytes_gathered_per_step": transit["last_bytes"], "transit_frames": transit,
+           "bit_exact_vs_single_device_frame": bool(ok and transit["bad"] == 0)}
     print(json.dumps(out), flush=True)
     return 0
 
@@ -590,7 +604,8 @@ def capi_multi_isolated(args, W, H, devices, timeout_s=100):
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--capi-only", "--capi-devices", ",".join(map(str, devices)),
            "--size", str(W), str(H), "--mesh", args.mesh, "--tile-mesh", str(args.tile_mesh), "--kernel", args.kernel,
-           "--steps", str(args.steps), "--warmup", str(args.warmup), "--capi-split", args.capi_split]
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--capi-split", args.capi_split,
+           "--transit", args.transit]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
     except subprocess.TimeoutExpired:
@@ -612,8 +627,8 @@ def main():
 
     import simpleraytracing_amd as xrt
     from simpleraytracing_amd.scenes import orbit_camera, tiled_mesh
-    from simpleraytracing_amd.strips import (balanced_bounds, gather_step_us, root_share, strip_bounds,
-                                             unpack_descriptors, weighted_bounds)
+    from simpleraytracing_amd.strips import (balanced_bounds, gather_step_us, hit_descriptors, root_share,
+                                             strip_bounds, unpack_descriptors, weighted_bounds)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -676,7 +691,8 @@ def main():
         link = measure_link(dist, torch, world, rank, dev, nccl)
         flat = torch.zeros(2 * world, dtype=torch.int64, device=dev if nccl else "cpu")
         if rank == 0:
-            band_cost, band_bytes, span_us = band_model(xrt, torch, tris, cam, W, H, device_index)
+            band_cost, band_bytes, span_us = band_model(xrt, torch, tris, cam, W, H, device_index,
+                                                        transit=args.transit)
             b = balanced_bounds(band_cost, band_bytes, world, link, H, unpack_us=5.0)
             flat.copy_(torch.tensor([v for be in b for v in be], dtype=torch.int64))
             split_info = {"link_bytes_per_us": link, "frame_span_us": span_us,
@@ -706,7 +722,8 @@ def main():
     # its frame's L plane and expands the image and u8 planes from them
     # (xrt_expand_rows_device) -- frame k's gather overlaps frame k+1's render.
     root = rank == 0 or not strips
-    packed = gathering and args.transit == "packed"
+    hits = gathering and args.transit == "hits"
+    packed = gathering and args.transit in ("packed", "hits")     # the hit layout travels by the fill plan too
     # Frames in flight (frames mode): frame k renders on stream k % F into its
     # own planes, so consecutive renders are not serialised by one stream -- a
     # frame's first waves start while the previous frame's last ones run.  The
@@ -737,37 +754,66 @@ def main():
     # its fill plan did not fill (those hold only misses).  The map of each
     # strip is a function of its geometry: one untimed frame sizes it, and the
     # senders send their maps to rank 0 once.
+    # Hit transit (--transit hits): per tile of the fill plan a 64-bit hit mask,
+    # then the hit rays' L values; the hit counts are a function of the
+    # geometry too (xrt_plan_hit_layout), so the senders send them once with
+    # their maps and rank 0 builds one set of unpack descriptors.
     if packed:
         if not root:
             ctx.render_rows_device(cam, r0, r1, 0, tbufs[0].data_ptr(), 0, stream.cuda_stream)
             rmap, n_packed = ctx.plan_region_map(W, r1 - r0)
             expect_fill = len(rmap) - n_packed
             d_map = torch.from_numpy(rmap.view(np.int32)).to(dev)
-            pbufs = [torch.zeros(max(n_packed, 1) * 1024, dtype=torch.float32, device=dev) for _ in range(2)]
-            # later frames render their L-buffer straight into the packed layout
-            if expect_fill:
-                ctx.set_transit_layout(pbufs[0].numel())
-            meta = torch.tensor([n_packed], dtype=torch.int64)
+            words = 0
+            if hits:
+                tile_hits, words = ctx.plan_hit_layout()
+                # the message, and room for one tile's hits past it (xrt.h)
+                hbufs = [torch.zeros(max(words, 4) + 64, dtype=torch.float32, device=dev) for _ in range(2)]
+                pbufs = [hb[:max(words, 4)] for hb in hbufs]
+                ctx.set_transit_hits(hbufs[0].numel())
+            else:
+                pbufs = [torch.zeros(max(n_packed, 1) * 1024, dtype=torch.float32, device=dev) for _ in range(2)]
+                # later frames render their L-buffer straight into the packed layout
+                if expect_fill:
+                    ctx.set_transit_layout(pbufs[0].numel())
+            meta = torch.tensor([n_packed, words], dtype=torch.int64)
             dist.send(meta.to(dev) if nccl else meta, dst=0)
             dist.send(d_map if nccl else d_map.cpu(), dst=0)
+            if hits:
+                th = torch.from_numpy(tile_hits.view(np.int32))
+                if th.numel():
+                    dist.send(th.to(dev) if nccl else th, dst=0)
         else:
             # every sender's blocks back to back in one buffer, one unpack launch
-            maps, counts = [], []
+            maps, counts, plans = [], [], []
             for g, (b, e) in enumerate(bounds):
                 if not g:
                     continue
-                meta = torch.zeros(1, dtype=torch.int64, device=dev if nccl else "cpu")
+                meta = torch.zeros(2, dtype=torch.int64, device=dev if nccl else "cpu")
                 dist.recv(meta, src=g)
                 n_regions = -(-W // 32) * -(-(e - b) // 32)
                 m = torch.zeros(n_regions, dtype=torch.int32, device=dev if nccl else "cpu")
                 dist.recv(m, src=g)
                 maps.append(m.cpu().numpy().view(np.uint32))
-                counts.append(int(meta.item()))
-            desc, bases, total = unpack_descriptors(W, bounds[1:], maps)
+                counts.append(int(meta[0].item()))
+                if hits:
+                    th = torch.zeros(16 * counts[-1], dtype=torch.int32, device=dev if nccl else "cpu")
+                    if th.numel():
+                        dist.recv(th, src=g)
+                    plans.append(th.cpu().numpy().view(np.uint32))
+            if hits:
+                desc, tdesc, bases, msg_words, total = hit_descriptors(W, bounds[1:], maps, plans)
+                d_tdesc = torch.from_numpy(tdesc.reshape(-1).view(np.int32)).to(dev)
+                d_bad = torch.zeros(1, dtype=torch.int32, device=dev)
+                rbuf = torch.zeros(max(total, 4), dtype=torch.float32, device=dev)
+                segs = {g + 1: rbuf[bases[g]:bases[g] + msg_words[g]] for g in range(world - 1)}
+            else:
+                desc, bases, total = unpack_descriptors(W, bounds[1:], maps)
+                rbuf = torch.zeros(max(total, 1) * 1024, dtype=torch.float32, device=dev)
+                segs = {g + 1: rbuf[bases[g] * 1024:(bases[g] + max(counts[g], 1)) * 1024]
+                        for g in range(world - 1)}
             d_desc = torch.from_numpy(desc.reshape(-1).view(np.int32)).to(dev)
             n_desc = len(desc)
-            rbuf = torch.zeros(max(total, 1) * 1024, dtype=torch.float32, device=dev)
-            segs = {g + 1: rbuf[bases[g] * 1024:(bases[g] + max(counts[g], 1)) * 1024] for g in range(world - 1)}
 
     def send_strip(t):
         if nccl:
@@ -794,7 +840,10 @@ def main():
                 host = torch.empty(t.numel(), dtype=torch.float32)
                 dist.recv(host, src=g)
                 t.copy_(host, non_blocking=False)
-        if packed:
+        if hits:
+            ctx.unpack_hits_device(W, n_desc, d_desc.data_ptr(), d_tdesc.data_ptr(), rbuf.data_ptr(), lb.data_ptr(),
+                                   img.data_ptr(), u8.data_ptr(), d_bad.data_ptr(), stream.cuda_stream)
+        elif packed:
             ctx.unpack_blocks_device(W, n_desc, d_desc.data_ptr(), rbuf.data_ptr(), lb.data_ptr(), img.data_ptr(),
                                      u8.data_ptr(), stream.cuda_stream)
         else:                                 # the received rows, above and below the root's strip
@@ -828,7 +877,7 @@ def main():
             b = k % 2
             if pending[b] is not None:
                 pending[b].wait()             # the send of frame k-2 has read this buffer
-            if packed and expect_fill:        # the render writes the packed blocks itself
+            if hits or (packed and expect_fill):   # the render writes the message itself
                 ctx.render_rows_device(cam, r0, r1, 0, pbufs[b].data_ptr(), 0, stream.cuda_stream)
                 if ctx.fill_regions() != expect_fill:   # the map assumes this frame filled them
                     raise RuntimeError(f"rank {rank}: the strip's fill plan did not hold for frame {k}")
@@ -963,13 +1012,17 @@ def main():
     if gathering and rank == 0:
         full = ctx.render_rows(cam)
         ok = planes_equal((img.cpu().numpy(), lb.cpu().numpy(), u8.cpu().numpy()), full)
+        if hits and int(d_bad.item()) != 0:   # a mask disagreed with its sender's plan
+            ok = False
         if os.environ.get("XRT_BENCH_CORRUPT_GATHER") == "1":    # test hook: a wrong strip must fail the job
             ok = False
-        moved = 4096 * sum(max(c, 1) for c in counts) if packed else 4 * rest
+        moved = (4 * sum(msg_words) if hits else 4096 * sum(max(c, 1) for c in counts)) if packed else 4 * rest
         gather = {"bit_exact_vs_single_device_frame": bool(ok),
                   "bytes_gathered_per_step": moved, "dense_bytes_per_step": 4 * rest,
-                  "transit": ("L-buffer strips, misses as XRT_MISS_TRANSIT, packed by region (the regions "
-                              "each strip's fill plan filled stay behind)") if packed
+                  "transit": ("per tile of each strip's fill plan a 64-bit hit mask, then the hit rays' L values "
+                              "(xrt_set_transit_hits)") if hits
+                  else ("L-buffer strips, misses as XRT_MISS_TRANSIT, packed by region (the regions "
+                        "each strip's fill plan filled stay behind)") if packed
                   else "L-buffer strips, misses as XRT_MISS_TRANSIT",
                   "strip_rows": [e - b for b, e in bounds], "strips": bounds, "root_share": share0,
                   "split": split_info or ("balanced" if balanced else args.root_share)}

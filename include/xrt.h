@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 4
+#define XRT_ABI_VERSION 5
 
 typedef enum xrt_status {
     XRT_OK = 0,
@@ -366,6 +366,20 @@ int xrt_multi_read_stats(xrt_multi* m, xrt_stats* stats);
 int xrt_multi_set_gather(xrt_multi* m, int mode);
 
 /*
+ * What a sender's strip sends to device 0 (attenuation model).
+ * XRT_TRANSIT_HITS (the default): once a strip geometry repeats (the same
+ * camera, rows, mesh and kernel as the sender's previous frame), per 8x8 tile
+ * of the regions its fill plan leaves a 64-bit hit mask and the hit rays' L
+ * values, rendered straight into that layout (xrt_set_transit_hits; the plan
+ * is made once per geometry, synchronously); a frame of a new geometry sends
+ * the packed layout.  XRT_TRANSIT_PACKED: always the 32x32 blocks of the
+ * regions the fill plan leaves (xrt_set_transit_layout's layout).
+ */
+#define XRT_TRANSIT_PACKED 0
+#define XRT_TRANSIT_HITS 1
+int xrt_multi_set_transit(xrt_multi* m, int mode);
+
+/*
  * How the rows are split over the devices.
  *   XRT_SPLIT_EQUAL     rows_per = H / n, the remainder going to the first
  *                       strips, strip g = device g in frame order -- the
@@ -459,6 +473,45 @@ int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats);
  */
 int xrt_unpack_blocks_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
                              const float* d_packed, float* d_lbuffer, float* d_image, uint8_t* d_u8, void* stream);
+
+/* --- hit transit (multi-GPU gathers) ------------------------------------- */
+
+/*
+ * Hit-only strips: a strip's message holds, per tile of its fill plan (8x8
+ * pixels; tile t of tile slot s is tile i = 16 s + t), a 64-bit mask of the
+ * tile's rays that hit mesh 0 (bit 8 y + x for pixel (x, y) of the tile) at
+ * 32-bit words [2i, 2i + 2), then the hit rays' L values -- tile by tile, in
+ * bit order -- from word 2 n_tiles.  A miss is an unset bit (its L is +inf,
+ * image 80, u8 255); the filled regions send nothing.  The per-tile hit counts
+ * are a function of the strip's geometry, like the fill plan.
+ *
+ * xrt_plan_hit_layout: the hit plan of the last frame's geometry, from that
+ * frame's records (it must be a BINNED render of that geometry over its fill
+ * plan: typically the geometry's first frame, row-major).  *n_tiles = 16 x
+ * the plan's tile slots, *words = the message's words (2 n_tiles + hits);
+ * tile_hits (nullable, `capacity` entries) receives each tile's hit count.
+ * Synchronous.  The tiles' order is xrt_plan_region_map's: tile slot s is
+ * packed region s.
+ * xrt_set_transit_hits: renders of this context write the hit layout into
+ * d_lbuffer (capacity_words >= *words + 64), instead of the packed
+ * (xrt_set_transit_layout) or row-major layout; 0 turns it off.  For BINNED
+ * attenuation renders of the L-buffer only; a frame of another geometry than
+ * the plan's, or whose fill plan does not hold, is not rendered and returns
+ * XRT_ERR_OVERFLOW.
+ * xrt_unpack_hits_device: many strips' messages in one launch on the receiver
+ * -- d_desc as xrt_unpack_blocks_device's, its last word the index in d_tdesc
+ * of the region's first tile descriptor (or 0xFFFFFFFF: a filled region);
+ * d_tdesc holds 4 u32 per tile: the word of its mask in d_msg, the word of its
+ * first hit value, its planned hit count, 0.  A mask whose count is not the
+ * planned one sets *d_bad (nullable) to 1.  d_desc, d_tdesc 16-B aligned;
+ * d_msg 8-B aligned.
+ */
+int xrt_plan_hit_layout(xrt_context* ctx, uint32_t* tile_hits, uint64_t capacity, uint64_t* n_tiles,
+                        uint64_t* words);
+int xrt_set_transit_hits(xrt_context* ctx, uint64_t capacity_words);
+int xrt_unpack_hits_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
+                           const uint32_t* d_tdesc, const uint32_t* d_msg, float* d_lbuffer, float* d_image,
+                           uint8_t* d_u8, uint32_t* d_bad, void* stream);
 
 /*
  * Test hooks, device probes and diagnostics: include/xrt_debug.h (not part of

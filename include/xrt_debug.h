@@ -166,6 +166,14 @@ int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2]);
  */
 int xrt_debug_destroy_ms(double ms[4]);
 
+/*
+ * Diagnostics of a multi context's transit (xrt_multi_set_transit): [0]
+ * frames whose strips travelled in the hit layout, [1] frames that travelled
+ * packed, [2] bytes the last frame sent into device 0, [3] 1 when a received
+ * hit mask disagreed with its sender's plan (waits for the last gather).
+ */
+int xrt_multi_transit_stats(xrt_multi* m, uint64_t out[4]);
+
 #ifdef __cplusplus
 }
 #endif

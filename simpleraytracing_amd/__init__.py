@@ -21,14 +21,14 @@ from . import _abi
 from ._abi import (Camera, Stats, XRT_KERNEL_AUTO, XRT_KERNEL_BINNED,  # noqa: F401
                    XRT_KERNEL_BRUTE, XRT_KERNEL_TILED, XRT_MISS_TRANSIT, XRT_MODEL_ATTENUATION,
                    XRT_MODEL_SIGNED, XRT_GATHER_AUTO, XRT_GATHER_COPY, XRT_GATHER_RCCL, XRT_SPLIT_EQUAL,
-                   XRT_SPLIT_BALANCED)
+                   XRT_SPLIT_BALANCED, XRT_TRANSIT_HITS, XRT_TRANSIT_PACKED)
 
 __all__ = [
     "Camera", "Stats", "Context", "MultiContext", "XrtError", "load_ply", "mesh_bbox", "camera_from_bbox",
     "camera_for_mesh", "device_count", "XRT_KERNEL_AUTO", "XRT_KERNEL_BRUTE", "XRT_KERNEL_TILED",
     "XRT_KERNEL_BINNED", "XRT_MISS_TRANSIT", "load_meshes", "scene_bbox", "camera_for_scene",
     "XRT_MODEL_ATTENUATION", "XRT_MODEL_SIGNED", "XRT_GATHER_AUTO", "XRT_GATHER_COPY", "XRT_GATHER_RCCL",
-    "XRT_SPLIT_EQUAL", "XRT_SPLIT_BALANCED",
+    "XRT_SPLIT_EQUAL", "XRT_SPLIT_BALANCED", "XRT_TRANSIT_HITS", "XRT_TRANSIT_PACKED",
 ]
 
 
@@ -383,6 +383,29 @@ class Context:
                                                        d_lbuffer or None, d_image or None, d_u8 or None,
                                                        stream or None), "xrt_unpack_blocks_device")
 
+    def plan_hit_layout(self):
+        """(tile_hits, words) of the last frame's geometry (xrt_plan_hit_layout): the
+        hit count of each tile of its fill plan (16 per tile slot) and the words of
+        its hit-layout message."""
+        n, w = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._lib.xrt_plan_hit_layout(self._ctx, None, 0, ctypes.byref(n), ctypes.byref(w)),
+                    "xrt_plan_hit_layout")
+        hits = np.zeros(n.value, np.uint32)
+        self._check(self._lib.xrt_plan_hit_layout(self._ctx, hits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                  n.value, ctypes.byref(n), ctypes.byref(w)), "xrt_plan_hit_layout")
+        return hits, w.value
+
+    def set_transit_hits(self, capacity_words: int):
+        """Render L-buffers in the hit layout (message capacity in 32-bit words; 0: off)."""
+        self._check(self._lib.xrt_set_transit_hits(self._ctx, int(capacity_words)), "xrt_set_transit_hits")
+
+    def unpack_hits_device(self, width: int, n_blocks: int, d_desc: int, d_tdesc: int, d_msg: int, d_lbuffer: int,
+                           d_image: int, d_u8: int, d_bad: int = 0, stream: int = 0):
+        """Many strips' hit-layout messages into whole-frame planes in one launch (see xrt.h)."""
+        self._check(self._lib.xrt_unpack_hits_device(self._ctx, width, n_blocks, d_desc, d_tdesc, d_msg,
+                                                     d_lbuffer or None, d_image or None, d_u8 or None,
+                                                     d_bad or None, stream or None), "xrt_unpack_hits_device")
+
     def timing_begin(self):
         self._check(self._lib.xrt_timing_begin(self._ctx), "xrt_timing_begin")
 
@@ -485,6 +508,18 @@ class MultiContext:
         """XRT_SPLIT_EQUAL (the reference's H/N rows) or XRT_SPLIT_BALANCED (the default;
         link rate in bytes/us, 0 = measured once)."""
         self._check(self._lib.xrt_multi_set_split(self._m, int(mode), float(link_bytes_per_us)), "xrt_multi_set_split")
+
+    def set_transit(self, mode: int):
+        """XRT_TRANSIT_HITS (the default: hit masks and hit values once a strip geometry
+        repeats) or XRT_TRANSIT_PACKED (the fill plan's 32x32 blocks)."""
+        self._check(self._lib.xrt_multi_set_transit(self._m, int(mode)), "xrt_multi_set_transit")
+
+    def transit_stats(self):
+        """{frames_hits, frames_packed, last_bytes, bad} (xrt_multi_transit_stats)."""
+        out = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.xrt_multi_transit_stats(self._m, out), "xrt_multi_transit_stats")
+        return {"frames_hits": int(out[0]), "frames_packed": int(out[1]), "last_bytes": int(out[2]),
+                "bad": int(out[3])}
 
     def plan(self, cam: Camera):
         """The strips of cam's frame: ([(begin, end) per device], {link, span_us, step_us})."""

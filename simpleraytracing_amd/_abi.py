@@ -43,6 +43,9 @@ XRT_GATHER_RCCL = 2
 XRT_SPLIT_EQUAL = 0
 XRT_SPLIT_BALANCED = 1
 
+XRT_TRANSIT_PACKED = 0
+XRT_TRANSIT_HITS = 1
+
 XRT_IMAGE_TEXT = 0
 XRT_IMAGE_TGA = 1
 XRT_IMAGE_PGM = 2
@@ -160,6 +163,11 @@ XRT_SYMBOLS = {
                                                  _vp]),
     "xrt_set_transit_layout": (ctypes.c_int, [_CtxP, _u64]),
     "xrt_unpack_blocks_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "xrt_plan_hit_layout": (ctypes.c_int, [_CtxP, ctypes.POINTER(_u32), _u64, ctypes.POINTER(_u64),
+                                           ctypes.POINTER(_u64)]),
+    "xrt_set_transit_hits": (ctypes.c_int, [_CtxP, _u64]),
+    "xrt_unpack_hits_device": (ctypes.c_int, [_CtxP, ctypes.c_uint32, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                              _vp]),
     "xrt_multi_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_MultiP)]),
     "xrt_multi_destroy": (None, [_MultiP]),
     "xrt_multi_last_error": (ctypes.c_char_p, [_MultiP]),
@@ -173,6 +181,8 @@ XRT_SYMBOLS = {
     "xrt_multi_read_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(Stats)]),
     "xrt_multi_set_gather": (ctypes.c_int, [_MultiP, ctypes.c_int]),
     "xrt_multi_set_split": (ctypes.c_int, [_MultiP, ctypes.c_int, ctypes.c_double]),
+    "xrt_multi_set_transit": (ctypes.c_int, [_MultiP, ctypes.c_int]),
+    "xrt_multi_transit_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(_u64)]),
     "xrt_multi_plan": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), ctypes.POINTER(_u32), _dp]),
     "xrt_balanced_bounds": (ctypes.c_int, [_dp, _dp, _u32, _u32, ctypes.c_double, _u32, _u32, ctypes.c_double,
                                            ctypes.POINTER(_u32), _dp]),
@@ -193,7 +203,10 @@ _host = None
 
 
 def _bind(lib, table):
+    variant = bool(os.environ.get("XRT_LIB"))
     for name, (res, args) in table.items():
+        if variant and not hasattr(lib, name):     # an A/B build of an older ABI: its entry points only
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

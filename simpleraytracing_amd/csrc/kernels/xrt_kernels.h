@@ -93,11 +93,50 @@ struct Outputs {
     // (kMissTransit, expanded on the receiving device by k_expand).
     float miss_l;
     float mu;                  // kModelSigned: mesh 0's attenuation coefficient (fork :800)
-    // Packed transit layout (BINNED with a fill plan only): pixel (row, col) of
-    // the region in launch slot s goes to s * 1024 + its row-major offset in the
-    // region's 32x32 block; the plan's filled regions store nothing.
+    // Transit layouts (BINNED with a fill plan only; lbuffer is the message):
+    // kLayoutPacked -- pixel (row, col) of the region in launch slot s goes to
+    // s * 1024 + its row-major offset in the region's 32x32 block; the plan's
+    // filled regions store nothing.  kLayoutHits -- tile t of slot s (index i =
+    // s * 16 + t, i < hit_tiles) stores the 64-bit mask of its hit rays at
+    // words [2i, 2i + 2) and their L values, in lane order, at words
+    // 2 * hit_tiles + hit_off[i] ..; hit_off comes from the geometry's hit plan
+    // (xrt_plan_hit_layout).
     uint32_t packed;
+    uint32_t hit_tiles;
+    const uint32_t* hit_off;
 };
+// (the hit layout has its own instantiation of the binned render, kHits: its
+// stores in the ordinary render cost 10-35% of the kernel's time)
+constexpr uint32_t kLayoutRowMajor = 0u, kLayoutPacked = 1u, kLayoutHits = 2u;
+
+// A wave-uniform table entry read through the constant address space (a scalar load).
+__device__ __forceinline__ const __attribute__((address_space(4))) uint32_t* as_const_u32(const uint32_t* p)
+{
+    return (const __attribute__((address_space(4))) uint32_t*)p;
+}
+
+// The hit layout's element of a tile: its index (low 32 bits) and its plan's
+// first hit word (high 32 bits; hit_off, a scalar load issued when the tile
+// starts rather than where its values are stored).
+__device__ __forceinline__ size_t hit_element(const Outputs& out, uint32_t index)
+{
+    return (size_t)index | ((size_t)as_const_u32(out.hit_off)[index] << 32);
+}
+
+// The hit layout's per-tile stores (kLayoutHits): the mask by lane 0, a hit
+// lane's L value at its rank among the tile's hits.  `hit`: the lane's ray hit
+// mesh 0 at least once; `e`: hit_element's.  Every lane of the wave calls it.
+__device__ __forceinline__ void store_hit_tile(const Outputs& out, size_t e, bool hit, float lval)
+{
+    const unsigned long long m = __ballot(hit);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* msg = reinterpret_cast<uint32_t*>(out.lbuffer);
+    if (lane == 0u) reinterpret_cast<uint2*>(msg)[(uint32_t)e] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+    if (hit) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        out.lbuffer[2u * (size_t)out.hit_tiles + (uint32_t)(e >> 32) + rank] = lval;
+    }
+}
 
 // A signalling NaN no render produces (path lengths are >= 0, +inf, or x86's
 // default NaN): marks "no hit" in L-buffer strips in transit, where +inf
@@ -581,8 +620,9 @@ __device__ __forceinline__ float overflow_fixup(unsigned long long om, const Tri
 
 // Must be reached by the whole wave (the overflow fix-up is wave-wide).
 // (dx, dy, dz) is this lane's ray; n_cand / fetch the candidates the render
-// tested (fetch(k) = triangle of the k-th), cull(k) their tile cull.
-template <typename Fetch, typename Cull = NoCull>
+// tested (fetch(k) = triangle of the k-th), cull(k) their tile cull.  kHits:
+// the hit layout (o is the tile's hit_element).
+template <bool kHits = false, typename Fetch, typename Cull = NoCull>
 __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs& out, bool active,
                                            size_t o, const HitList& hl,
                                            WaveStats& ws, const TriRec* __restrict__ recs, float dx,
@@ -608,11 +648,15 @@ __device__ __forceinline__ void finish_ray(const RenderParams& p, const Outputs&
             lval = d;
         }
     }
-    if (!active) return;
     if (distance != distance) {                       // inf - inf: x86's default NaN (xrt_device.h)
         distance = xrt_f32_from_bits(kX86DefaultNaN);
         lval = distance;
     }
+    if constexpr (kHits) {
+        store_hit_tile(out, o, active && hl.n > 0u, lval);
+        return;
+    }
+    if (!active) return;
     // distance 0 (a miss or an odd count) shades to 80 * expf(-0) = 80 -> 255;
     // the wave skips expf and the LUT when none of its rays needs them.
     float photon = 80.0f;
@@ -1978,7 +2022,7 @@ __device__ __forceinline__ void merge_half(const RecStage& other, HitList& hl, u
     tests += wave_uniform(__float_as_uint(d.y));
 }
 
-template <bool kSigned>
+template <bool kSigned, bool kHits>
 __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restrict__ recs,
                                             const float4* __restrict__ culls, const RenderParams& p,
                                             const Outputs& out, const BinBuffers& bins, uint32_t n_glob,
@@ -2005,11 +2049,15 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
     const bool active = col < p.width && row < p.row_end;
     const float xc = (float)tx0 + 3.5f, yc = (float)ty0 + 3.5f;
     const float fx0 = (float)tx0, fx1 = (float)tx0 + 7.0f, fy0 = (float)ty0, fy1 = (float)ty0 + 7.0f;
-    // the lane's output element: row-major in the strip, or in its slot's packed block
-    const size_t o = out.packed ? (size_t)slot * kPackBlock + ((tile >> 2) * 8u + (lane >> 3)) * kRegion +
+    // the lane's output element: row-major in the strip, or in its slot's packed
+    // block; the hit layout's hit_element
+    constexpr bool hits = kHits;
+    const size_t o = hits ? hit_element(out, slot * kWavesPerRegion + tile)
+                   : out.packed ? (size_t)slot * kPackBlock + ((tile >> 2) * 8u + (lane >> 3)) * kRegion +
                                       (tile & 3u) * 8u + (lane & 7u)
                                 : (size_t)(row - p.row_begin) * p.width + col;
     if (!tile_live) {
+        if (hits && split != kSplitHalf1) store_hit_tile(out, o, false, 0.0f);
         if (split != kSplitNone) __syncthreads();  // the pair's one barrier (workgroup-uniform count)
         return;
     }
@@ -2105,13 +2153,14 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
         if constexpr (kSigned)
             finish_ray_signed(p, out, active, row, col, hl, ws, recs, dx, dy, dz, sx, sy, sz, n_cand, fetch, cull);
         else
-            finish_ray(p, out, active, o, hl, ws, recs, dx, dy, dz, n_cand, fetch, cull);
+            finish_ray<kHits>(p, out, active, o, hl, ws, recs, dx, dy, dz, n_cand, fetch, cull);
     } else if (kSigned) {   // no survivor: L stays 80 (fork :314; :808 with distance 0)
         ws.rays += (uint32_t)__popcll(__ballot(active));
         if (active && out.lbuffer) out.lbuffer[(size_t)(row - p.row_begin) * p.width + col] = 80.0f;
     } else {   // no survivor: every ray of the tile misses (main.cxx:700-718 with no hit)
         ws.rays += (uint32_t)__popcll(__ballot(active));
-        if (active) {
+        if (hits) store_hit_tile(out, o, false, 0.0f);
+        else if (active) {
             if (out.image) out.image[o] = 80.0f;
             if (out.lbuffer) out.lbuffer[o] = out.miss_l;
             if (out.image_u8) out.image_u8[o] = 255u;
@@ -2161,15 +2210,15 @@ __device__ __forceinline__ void fill_region_rows(const RenderParams& p, const Ou
 // launches a plan that this frame's k_prep confirmed (no pair binned past
 // tile_slots, an empty global list: BinBuffers::plan_miss); otherwise every
 // region renders as tiles.  The signed model always renders tiles.
-template <bool kSigned>
-__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(kSigned ? 5 : XRT_RENDER_WAVES, 8))) void k_render_binned(
-    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
-    BinBuffers bins, const BinState* __restrict__ bs)
+template <bool kSigned, bool kHits>
+__device__ __forceinline__ void render_binned(RecStage* st, const TriRec* __restrict__ recs,
+                                              const float4* __restrict__ culls, const RenderParams& p,
+                                              const Outputs& out, const BinBuffers& bins,
+                                              const BinState* __restrict__ bs)
 {
     static_assert(kWavesPerRegion >= kTileWaves && kWavesPerRegion % kTileWaves == 0,
                   "a workgroup's waves render tiles of one region");
     constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
-    __shared__ RecStage st[kTileWaves];            // one private stage per wave
     const uint64_t t_start = block_start_stamp();
     const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
     const uint32_t split_slots = kSigned || !kCanSplit ? 0u : bins.split_slots;
@@ -2213,7 +2262,7 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
         const uint32_t slot = g / (2u * kWavesPerRegion);
         const uint32_t tile = (g / 2u) % kWavesPerRegion;
         const uint32_t half = g & 1u;
-        render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand,
+        render_tile<kSigned, kHits>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand,
                              half ? kSplitHalf1 : kSplitHalf0, &st[kCanSplit ? wave ^ 1u : wave]);
         if (!half)                                 // one record per tile (the region's 16), by half 0
             store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, slot * kWavesPerRegion + tile,
@@ -2225,9 +2274,27 @@ __global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t g = (blk - split_blocks / 2u) * kTileWaves + wave; // wave of the grid (16 per region)
     const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
     const uint32_t tile = g % kWavesPerRegion;
-    render_tile<kSigned>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
+    render_tile<kSigned, kHits>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
     // candidates are counted once per region (by the wave holding tile 0)
     store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
+}
+
+template <bool kSigned>
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(kSigned ? 5 : XRT_RENDER_WAVES, 8))) void k_render_binned(
+    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
+    BinBuffers bins, const BinState* __restrict__ bs)
+{
+    __shared__ RecStage st[kTileWaves];            // one private stage per wave
+    render_binned<kSigned, false>(st, recs, culls, p, out, bins, bs);
+}
+
+// The same render writing the hit layout (Outputs::packed == kLayoutHits).
+__global__ __launch_bounds__(64 * kTileWaves) __attribute__((amdgpu_waves_per_eu(XRT_RENDER_WAVES, 8))) void k_render_binned_hits(
+    const TriRec* __restrict__ recs, const float4* __restrict__ culls, RenderParams p, Outputs out,
+    BinBuffers bins, const BinState* __restrict__ bs)
+{
+    __shared__ RecStage st[kTileWaves];
+    render_binned<false, true>(st, recs, culls, p, out, bins, bs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2455,6 +2522,44 @@ __global__ __launch_bounds__(256) void k_unpack_blocks(const float* __restrict__
                            __uint_as_float(kMissTransit), __uint_as_float(kMissTransit));
     if (d.w != kEmpty) v = *reinterpret_cast<const float4*>(packed + (size_t)d.w * kPackBlock + 4u * threadIdx.x);
     unpack_pixels(v, d.x + r, d.z + 4u * (threadIdx.x % 8u), width, lbuffer, image, image_u8);
+}
+
+// Many strips' hit-layout messages in one launch (Outputs::packed ==
+// kLayoutHits): block b is a region described by desc[b] as k_unpack_blocks'
+// (its last word: the index of the region's first tile descriptor, or kEmpty),
+// tile t of it by tdesc[desc[b].w + t] = (word of its 64-bit hit mask in msg,
+// word of its first hit value, the hit count its plan expects, 0).  A mask
+// whose count differs from the plan's sets *bad (the message is not this
+// geometry's), and hits past the plan's count read as misses: the reads stay
+// inside the plan's words.
+__global__ __launch_bounds__(256) void k_unpack_hits(const uint32_t* __restrict__ msg, const uint4* __restrict__ desc,
+                                                     const uint4* __restrict__ tdesc, float* __restrict__ lbuffer,
+                                                     float* __restrict__ image, uint8_t* __restrict__ image_u8,
+                                                     uint32_t width, uint32_t* __restrict__ bad)
+{
+    const uint4 d = desc[blockIdx.x];
+    const uint32_t r = threadIdx.x / 8u;
+    if (r >= d.y) return;
+    const uint32_t c4 = 4u * (threadIdx.x % 8u);
+    float l[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) l[k] = __uint_as_float(kMissTransit);
+    if (d.w != kEmpty) {
+        const uint4 td = tdesc[(size_t)d.w + (r / 8u) * 4u + c4 / 8u];
+        const uint2 mw = *reinterpret_cast<const uint2*>(msg + td.x);
+        const unsigned long long m = (unsigned long long)mw.x | ((unsigned long long)mw.y << 32);
+        if ((r & 7u) == 0u && (c4 & 7u) == 0u && (uint32_t)__popcll(m) != td.z && bad) atomicOr(bad, 1u);
+        const uint32_t bit0 = (r & 7u) * 8u + (c4 & 7u);
+        uint32_t rank = (uint32_t)__popcll(m & ((1ull << bit0) - 1ull));
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            if ((m >> (bit0 + k)) & 1ull) {
+                if (rank < td.z) l[k] = __uint_as_float(msg[td.y + rank]);
+                ++rank;
+            }
+        }
+    }
+    unpack_pixels(make_float4(l[0], l[1], l[2], l[3]), d.x + r, d.z + c4, width, lbuffer, image, image_u8);
 }
 
 // The receiving side: a packed strip into the frame's three planes (k_expand's

@@ -263,6 +263,7 @@ struct PendingFrame {
     // the frame renders the current geometry (bin_key) over its compact
     // layout and fill plan: its records can give the tile plan
     bool plan_source = false;
+    bool hit_plan_ok = false;          // hit layout: the context's hit plan is this frame's geometry's
     hipStream_t stream = nullptr;
     hipEvent_t prep_done = nullptr;    // k_prep complete (prep stream)
     // The host waits for prep_done and reads k_prep's check before the launch
@@ -424,6 +425,17 @@ struct xrt_context {
     bool moving = false;
     bool reuse_cameras = true;         // false for xrt_render_rows_multi's contexts
     BinKey last_key = {};              // the last frame's geometry
+    // Hit transit (xrt_set_transit_hits): the message buffer's capacity in
+    // 32-bit words (0: off), and the hit plan of geometry hit_key
+    // (xrt_plan_hit_layout): per tile of its fill plan the exclusive scan of
+    // the tiles' hit counts, n_tiles + 1 entries on the device.
+    uint64_t hits_cap = 0;
+    bool hit_valid = false;
+    BinKey hit_key = {};
+    uint32_t hit_tiles = 0;
+    uint64_t hit_words = 0;
+    uint32_t* d_hit_off = nullptr;
+    size_t hit_off_cap = 0;
     uint32_t still_frames = 0;         // frames in a row on one camera over reused lists
     // Prepare-ahead (DESIGN.md "Pipelining"): when a device-pointer render
     // repeats the previous call's frame geometry, the preparations of the next
@@ -970,11 +982,15 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     out.mu = ctx->mu;
     out.packed = 0u;
     out.wave_times = nullptr;          // launch_frame
-    if (ctx->packed_cap) {                         // xrt_set_transit_layout
+    out.hit_tiles = 0u;
+    out.hit_off = nullptr;
+    if (ctx->packed_cap || ctx->hits_cap) {        // xrt_set_transit_layout / _hits
         if (!binned || signed_model || d_image || d_u8)
             return fail(ctx, XRT_ERR_ARGUMENT,
-                        "the packed layout is for BINNED attenuation renders of the L-buffer only");
-        out.packed = 1u;
+                        "the transit layouts are for BINNED attenuation renders of the L-buffer only");
+        out.packed = ctx->hits_cap ? kLayoutHits : kLayoutPacked;
+        out.hit_tiles = ctx->hit_tiles;
+        out.hit_off = ctx->d_hit_off;
     }
     const uint32_t n_regions = rows ? rx * ry : 0u;
     BinBuffers bins = {};
@@ -996,7 +1012,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     ctx->last_key = key;
     bool reuse = false;
     if (binned && rows > 0 && fill_ok && ctx->bin_key_valid && ctx->compact && !ctx->bin_force_cap &&
-        !ctx->packed_cap) {
+        !ctx->packed_cap && !ctx->hits_cap) {
         if (ctx->reuse_cameras && !key.same(ctx->bin_key) && key.same_layout(ctx->bin_key) &&
             ctx->still_frames < kStillFrames) {
             reuse = true;
@@ -1137,6 +1153,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     pf.fs = &fs;
     pf.plan_source = binned && fill_ok && !reuse && ctx->compact && ctx->plan_valid && !ctx->bin_force_cap &&
                      bins.desc == ctx->compact_layout.d_desc && bins.tile_slots == ctx->plan_tile_slots;
+    pf.hit_plan_ok = ctx->hit_valid && key.same(ctx->hit_key);
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
     pf.host_wait = bins.plan_miss != nullptr;
@@ -1224,7 +1241,9 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     }
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;
+    bool missed = false;
     if (binned && bins.plan_miss && (fs.plan_flag[0] | fs.plan_flag[1]) != 0u) {
+        missed = true;
         // k_prep binned a pair into a region the plan fills, into the global
         // list or past a list's capacity: this frame renders every region as
         // tiles (an overflowed region from the whole mesh -- exact, slower), and
@@ -1240,10 +1259,18 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         ctx->bin_key_valid = false;
     }
     ctx->last_fill_regions = binned ? rx * ry - bins.tile_slots : 0u;
-    if (pf.out.packed && rows > 0 &&
+    if (pf.out.packed == kLayoutPacked && rows > 0 &&
         (bins.tile_slots >= rx * ry || (uint64_t)bins.tile_slots * kPackBlock > ctx->packed_cap))
         return fail(ctx, XRT_ERR_OVERFLOW, "the packed layout needs this frame's fill plan (and room for its "
                                         "unfilled regions): the frame was not rendered");
+    // the hit layout: the plan's tiles are exactly this frame's tile regions',
+    // and the message has room for the plan's words plus one tile's hits (a
+    // tile with more hits than its plan stays inside the buffer)
+    if (pf.out.packed == kLayoutHits && rows > 0 &&
+        (!pf.hit_plan_ok || missed || (uint64_t)bins.tile_slots * kWavesPerRegion != pf.out.hit_tiles ||
+         ctx->hit_words + kWavesPerRegion * 4u > ctx->hits_cap))
+        return fail(ctx, XRT_ERR_OVERFLOW, "the hit layout needs this geometry's hit plan (xrt_plan_hit_layout), "
+                                        "its fill plan and room for its words: the frame was not rendered");
 
     // Every render dispatch carries the set's stop event (the host needs it
     // to reuse the set).  Its waves store their timing records beside their
@@ -1300,7 +1327,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
             hipExtLaunchKernelGGL(k_render_tiled, dim3(rx, ry), dim3(256), 0, stream, t0, t1, 0,
                                   fs.recs, fs.cull, p, out);
         else
-            hipExtLaunchKernelGGL(sgn ? k_render_binned<true> : k_render_binned<false>, grid, dim3(64 * kTileWaves),
+            hipExtLaunchKernelGGL(sgn ? k_render_binned<true>
+                                      : out.packed == kLayoutHits ? k_render_binned_hits : k_render_binned<false>, grid, dim3(64 * kTileWaves),
                                   0, stream, t0, t1, 0, fs.recs, fs.cull, p, out, bins, (const BinState*)bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         ctx->acc_ms[4] += std::chrono::duration<double, std::milli>(HostClock::now() - t_launch).count();
@@ -1615,6 +1643,7 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_stats_partial);
     (void)hipFree(ctx->d_stats_done);
     (void)hipFree(ctx->d_stats_out);
+    (void)hipFree(ctx->d_hit_off);
     for (auto& c : ctx->tchunks) (void)hipFree(c.p);
     lap(1);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
@@ -1874,9 +1903,13 @@ int xrt_plan_region_map(xrt_context* ctx, uint32_t width, uint32_t rows, uint32_
     if (n_regions != (uint64_t)rx * ry)
         return fail(ctx, XRT_ERR_ARGUMENT, "map must hold ceil(width/32) x ceil(rows/32) regions");
     const SlotLayout& L = ctx->compact_layout;
-    const bool planned = ctx->last_fill_regions > 0 && ctx->plan_valid && L.rx == rx && L.ry == ry &&
-                         L.slot_region.size() == n_regions;
-    if (!planned) {                                 // every region travels
+    const bool layout = L.rx == rx && L.ry == ry && L.slot_region.size() == n_regions;
+    const bool planned = ctx->last_fill_regions > 0 && ctx->plan_valid && layout;
+    // no region of the geometry is empty: every region travels, in slot order
+    // (the order of the hit layout's tiles)
+    const bool whole = !ctx->plan_valid && ctx->last_fill_regions == 0 && layout && ctx->compact &&
+                       ctx->bin_key_valid && ctx->last_key.same(ctx->bin_key);
+    if (!planned && !whole) {                       // every region travels
         for (uint64_t r = 0; r < n_regions; ++r) map[r] = (uint32_t)r;
         *n_packed = (uint32_t)n_regions;
         return XRT_OK;
@@ -1937,7 +1970,77 @@ int xrt_set_transit_layout(xrt_context* ctx, uint64_t packed_floats)
 {
     if (!ctx) return XRT_ERR_ARGUMENT;
     ctx->packed_cap = packed_floats;
+    if (packed_floats) ctx->hits_cap = 0;
     ++ctx->state_gen;                   // frames prepared ahead are stale
+    return XRT_OK;
+}
+
+int xrt_set_transit_hits(xrt_context* ctx, uint64_t capacity_words)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    ctx->hits_cap = capacity_words;
+    if (capacity_words) ctx->packed_cap = 0;
+    ++ctx->state_gen;
+    return XRT_OK;
+}
+
+int xrt_plan_hit_layout(xrt_context* ctx, uint32_t* tile_hits, uint64_t capacity, uint64_t* n_tiles,
+                        uint64_t* words)
+{
+    if (!ctx || !n_tiles || !words) return fail(ctx, XRT_ERR_ARGUMENT, "NULL argument");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = sync_context(ctx);
+    if (rc) return rc;
+    const FrameSet* fs = ctx->last_set;
+    // the last frame rendered the lists' geometry over its fill plan (or, with
+    // no empty region, every region in slot order): its records s * 16 + t
+    // (s < the plan's tile slots) are the plan's tiles
+    const bool fill_frame = ctx->plan_valid && ctx->last_fill_regions > 0;
+    const bool whole_frame = !ctx->plan_valid && ctx->last_fill_regions == 0;
+    if (!fs || !fs->binned || !ctx->bin_key_valid || !ctx->compact || !(fill_frame || whole_frame) ||
+        !ctx->last_key.same(ctx->bin_key) || (uint64_t)ctx->plan_tile_slots * kWavesPerRegion > fs->rendered_blocks)
+        return fail(ctx, XRT_ERR_ARGUMENT, "the hit plan needs a BINNED frame rendered over its geometry's fill "
+                                           "plan just before");
+    const uint32_t tiles = ctx->plan_tile_slots * kWavesPerRegion;
+    std::vector<BlockStats> rec(tiles);
+    if (tiles) XRT_HIP(ctx, hipMemcpy(rec.data(), fs->block_stats, tiles * sizeof(BlockStats), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> off(tiles + 1u);
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < tiles; ++i) {
+        off[i] = (uint32_t)run;
+        run += rec[i].hit_rays;
+        if (tile_hits && i < capacity) tile_hits[i] = rec[i].hit_rays;
+    }
+    if (run + 2ull * tiles > 0xFFFFFFFFull) return fail(ctx, XRT_ERR_OVERFLOW, "hit message exceeds 2^32 words");
+    off[tiles] = (uint32_t)run;
+    if ((rc = ensure(ctx, ctx->d_hit_off, ctx->hit_off_cap, (size_t)tiles + 1u))) return rc;
+    XRT_HIP(ctx, hipMemcpy(ctx->d_hit_off, off.data(), off.size() * 4u, hipMemcpyHostToDevice));
+    ctx->hit_key = ctx->bin_key;
+    ctx->hit_tiles = tiles;
+    ctx->hit_words = 2ull * tiles + run;
+    ctx->hit_valid = true;
+    ++ctx->state_gen;                   // frames prepared ahead carry the old plan
+    *n_tiles = tiles;
+    *words = ctx->hit_words;
+    return XRT_OK;
+}
+
+int xrt_unpack_hits_device(xrt_context* ctx, uint32_t width, uint64_t n_blocks, const uint32_t* d_desc,
+                           const uint32_t* d_tdesc, const uint32_t* d_msg, float* d_lbuffer, float* d_image,
+                           uint8_t* d_u8, uint32_t* d_bad, void* stream)
+{
+    if (!ctx) return fail(nullptr, XRT_ERR_ARGUMENT, "context is NULL");
+    if (!n_blocks) return XRT_OK;
+    if (!d_desc || !d_tdesc || !d_msg) return fail(ctx, XRT_ERR_ARGUMENT, "NULL buffer");
+    if (n_blocks > 0x7FFFFFFFull) return fail(ctx, XRT_ERR_ARGUMENT, "too many blocks");
+    if (((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_tdesc)) & 15u) ||
+        (reinterpret_cast<uintptr_t>(d_msg) & 7u))
+        return fail(ctx, XRT_ERR_ARGUMENT, "descriptors not 16-B aligned or message not 8-B aligned");
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_unpack_hits, dim3((unsigned)n_blocks), dim3(256), 0, (hipStream_t)stream, d_msg,
+                       reinterpret_cast<const uint4*>(d_desc), reinterpret_cast<const uint4*>(d_tdesc), d_lbuffer,
+                       d_image, d_u8, width, d_bad);
+    XRT_HIP(ctx, hipGetLastError());
     return XRT_OK;
 }
 

@@ -133,6 +133,54 @@ def unpack_descriptors(width: int, spans, maps):
     return desc, bases, base
 
 
+def hit_descriptors(width: int, spans, maps, tile_hits):
+    """Descriptors of xrt_unpack_hits_device for the hit-layout messages of
+    `spans` ([begin, end) rows) with region maps `maps` (xrt_plan_region_map)
+    and hit plans `tile_hits` (xrt_plan_hit_layout: the hit count of tile
+    16 s + t of tile slot s), the strips' messages back to back in one buffer,
+    each at a 16-B aligned word (a strip with no tile still sends 4 words).
+    Returns (desc (n, 4) uint32 -- first row, rows, first column, index of the
+    region's first tile descriptor or EMPTY --, tdesc (m, 4) uint32 -- mask
+    word, first hit word, hit count, 0 per tile --, each strip's first word,
+    each strip's message words, total words)."""
+    rx = -(-width // 32)
+    descs, tdescs, bases, words = [], [], [], []
+    base, tbase = 0, 0
+    for (b, e), m, h in zip(spans, maps, tile_hits):
+        m = np.asarray(m, np.uint32)
+        h = np.asarray(h, np.uint64)
+        ry = -(-(e - b) // 32)
+        if m.size != rx * ry:
+            raise ValueError("region map does not match the strip")
+        n_tiles = h.size
+        if n_tiles != 16 * int(np.count_nonzero(m != EMPTY)):
+            raise ValueError("hit plan does not match the region map")
+        r = np.arange(m.size, dtype=np.uint64)
+        y, x = r // rx, r % rx
+        d = np.empty((m.size, 4), np.uint32)
+        d[:, 0] = b + 32 * y
+        d[:, 1] = np.minimum(32, (e - b) - 32 * y)
+        d[:, 2] = 32 * x
+        d[:, 3] = np.where(m == EMPTY, EMPTY, 16 * m.astype(np.uint64) + tbase).astype(np.uint32)
+        off = np.concatenate([[0], np.cumsum(h)[:-1]]).astype(np.uint64) if n_tiles else np.zeros(0, np.uint64)
+        t = np.zeros((n_tiles, 4), np.uint32)
+        t[:, 0] = base + 2 * np.arange(n_tiles, dtype=np.uint64)
+        t[:, 1] = base + 2 * n_tiles + off
+        t[:, 2] = h
+        descs.append(d)
+        tdescs.append(t)
+        bases.append(base)
+        w = max(2 * n_tiles + int(h.sum()), 4)
+        words.append(w)
+        base += -(-w // 4) * 4
+        tbase += n_tiles
+    desc = np.concatenate(descs) if descs else np.zeros((0, 4), np.uint32)
+    tdesc = np.concatenate(tdescs) if tdescs else np.zeros((0, 4), np.uint32)
+    if tdesc.size == 0:
+        tdesc = np.zeros((1, 4), np.uint32)
+    return desc, tdesc, bases, words, base
+
+
 def max_strip_pixels(width: int, height: int, n: int) -> int:
     b, e = strip_bounds(height, n, 0)
     return (e - b) * width

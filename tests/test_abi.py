@@ -48,7 +48,7 @@ def test_libxrt_host_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _abi.load().xrt_abi_version() == 4
+    assert _abi.load().xrt_abi_version() == 5
 
 
 def test_create_without_gpu_fails_cleanly():

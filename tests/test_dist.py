@@ -60,6 +60,66 @@ def test_unpack_descriptors_cover_strips():
     assert sorted(blocks.tolist()) == list(range(total))
 
 
+def test_hit_descriptors_round_trip():
+    """The hit layout's descriptors (xrt_unpack_hits_device): strips encoded as
+    a sender's render writes them (per planned tile a 64-bit hit mask, then
+    the hit values in bit order) and decoded through desc / tdesc exactly as
+    k_unpack_hits reads them give back every hit of every strip, and misses
+    elsewhere; messages start at 16-B aligned words."""
+    from simpleraytracing_amd.strips import EMPTY, hit_descriptors
+    W = 100
+    spans = [(10, 77), (77, 131), (131, 140)]
+    rng = np.random.default_rng(5)
+    rx = -(-W // 32)
+    maps, plans, msgs, truth = [], [], [], np.full((140, W), np.nan, np.float32)
+    for b, e in spans:
+        ry = -(-(e - b) // 32)
+        n = rx * ry
+        m = np.full(n, EMPTY, np.uint32)
+        keep = np.sort(rng.choice(n, max(n // 2, 1), replace=False))
+        m[keep] = rng.permutation(len(keep))
+        n_slots = len(keep)
+        masks = np.zeros(16 * n_slots, np.uint64)
+        vals = [[] for _ in range(16 * n_slots)]
+        for r in keep:
+            s_ = int(m[r])
+            y0, x0 = b + 32 * (r // rx), 32 * (r % rx)
+            for t in range(16):
+                for lane in range(64):
+                    row, col = y0 + 8 * (t // 4) + lane // 8, x0 + 8 * (t % 4) + lane % 8
+                    if row < e and col < W and rng.random() < 0.4:
+                        v = np.float32(rng.random() * 10)
+                        masks[16 * s_ + t] |= np.uint64(1 << lane)
+                        vals[16 * s_ + t].append(v)
+                        truth[row, col] = v
+        hits = np.array([len(v) for v in vals], np.uint32)
+        msg = np.concatenate([masks.view(np.uint32)] + [np.array(v, np.float32).view(np.uint32) for v in vals])
+        maps.append(m)
+        plans.append(hits)
+        msgs.append(msg.astype(np.uint32))
+    desc, tdesc, bases, words, total = hit_descriptors(W, spans, maps, plans)
+    assert all(b % 4 == 0 for b in bases) and words == [max(len(x), 4) for x in msgs]
+    buf = np.zeros(total, np.uint32)
+    for b0, x in zip(bases, msgs):
+        buf[b0:b0 + len(x)] = x
+    out = np.full((140, W), -1.0, np.float32)
+    for r0, rows, c0, first in desc:
+        for r in range(rows):
+            for c in range(32):
+                if c0 + c >= W:
+                    continue
+                v = np.nan
+                if first != EMPTY:
+                    mw, hw, cnt, _ = tdesc[first + (r // 8) * 4 + c // 8]
+                    mask = int(buf[mw]) | (int(buf[mw + 1]) << 32)
+                    bit = (r % 8) * 8 + c % 8
+                    assert bin(mask).count("1") == cnt
+                    if (mask >> bit) & 1:
+                        v = buf[hw + bin(mask & ((1 << bit) - 1)).count("1")].view(np.float32)
+                out[r0 + r, c0 + c] = v
+    assert np.array_equal(out[10:140], truth[10:140], equal_nan=True)
+
+
 def test_strip_bounds_cover_image():
     for H in (1, 7, 128, 2048, 4097):
         for n in (1, 2, 3, 4, 8):

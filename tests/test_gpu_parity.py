@@ -963,6 +963,52 @@ def test_multi_rccl_gather_one_rank(dragon, devices, W, H):
                     assert np.array_equal(bits(x), bits(y))
 
 
+@pytest.mark.parametrize("gather", ["rccl", "copy"])
+def test_multi_hit_transit(dragon, gather):
+    """xrt_render_rows_multi's hit transit (XRT_TRANSIT_HITS, the default): a
+    new geometry's frame travels packed, its repeats in the hit layout (the
+    senders' plans made once); in an alternation of two cameras the planned
+    one travels as hits, the other packed; XRT_TRANSIT_PACKED keeps the
+    blocks.  Every frame bit-equal to one device's frame; the hit frames move
+    fewer bytes; no mask disagrees."""
+    W, H, n = 1024, 1024, 4
+    cams = [xrt.camera_for_mesh(dragon, W, H), xrt.camera_from_bbox(*oracle.bbox(dragon[:5000]), W, H)]
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        refs = [one.render_rows(c) for c in cams]
+    with xrt.MultiContext([0] * n) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        m.set_gather(xrt.XRT_GATHER_RCCL if gather == "rccl" else xrt.XRT_GATHER_COPY)
+        m.set_split(xrt.XRT_SPLIT_EQUAL)
+
+        def check(k):
+            got = m.render(cams[k])
+            for x, y in zip(got[:3], refs[k][:3]):
+                assert np.array_equal(bits(x), bits(y))
+
+        check(0)
+        packed_bytes = m.transit_stats()["last_bytes"]
+        for _ in range(3):
+            check(0)
+        st = m.transit_stats()
+        assert st["frames_packed"] == 1 and st["frames_hits"] == 3 and st["bad"] == 0, st
+        assert 0 < st["last_bytes"] < 0.75 * packed_bytes, (st, packed_bytes)
+        for k in (1, 0, 1, 0):                                 # camera 0 keeps its plan
+            check(k)
+        st = m.transit_stats()
+        assert st["frames_packed"] == 3 and st["frames_hits"] == 5, st
+        check(0)
+        assert m.transit_stats()["frames_hits"] == 6
+        m.set_transit(xrt.XRT_TRANSIT_PACKED)
+        for _ in range(2):
+            check(0)
+        st = m.transit_stats()
+        assert st["frames_hits"] == 6 and st["frames_packed"] == 5 and st["bad"] == 0, st
+        assert st["last_bytes"] == packed_bytes
+
+
 @pytest.mark.parametrize("W,H,n,link", [(4096, 4096, 8, 0.0), (1000, 777, 3, 3.0e4), (512, 512, 4, 1.0e3)])
 def test_multi_balanced_split_rccl_one_rank(dragon, W, H, n, link):
     """xrt_render_rows_multi with the balanced split (the default): one GPU listed
@@ -1269,10 +1315,137 @@ def test_packed_transit_equals_direct_render(ctx, dragon, W, H, r0, r1):
         assert np.array_equal(x.cpu().numpy().view(np.uint8), y.cpu().numpy().view(np.uint8))
 
 
+def _hit_strip(c, cam, W, r0, r1, dev, stream, frames=3):
+    """One context's strip [r0, r1) in the hit layout: the geometry's first
+    frame (row-major), its region map and hit plan, then `frames` frames
+    rendered straight into the message.  Returns (map, tile hits, message)."""
+    import torch
+    rows = r1 - r0
+    lb = torch.zeros(W * rows, device=dev)
+    c.render_rows_device(cam, r0, r1, 0, lb.data_ptr(), 0, stream.cuda_stream)
+    rmap, n_packed = c.plan_region_map(W, rows)
+    hits, words = c.plan_hit_layout()
+    assert len(hits) == 16 * n_packed and words == 2 * len(hits) + int(hits.sum())
+    msg = torch.full((words + 64,), -5.0, device=dev)
+    c.set_transit_hits(msg.numel())
+    try:
+        for _ in range(frames):                        # the tile plan comes in after the first
+            c.render_rows_device(cam, r0, r1, 0, msg.data_ptr(), 0, stream.cuda_stream)
+    finally:
+        c.set_transit_hits(0)
+    torch.cuda.synchronize(dev)
+    return rmap, hits, msg[:words]
+
+
+@pytest.mark.parametrize("W,H,cuts", [(1000, 700, [0, 700]), (2048, 2048, [0, 900, 2048]),
+                                      (333, 517, [0, 100, 400, 517]), (4096, 4096, [0, 1536, 2560, 4096])])
+def test_hit_transit_equals_direct_render(dragon, W, H, cuts):
+    """Strips rendered straight into the hit layout (xrt_set_transit_hits: a
+    64-bit hit mask per tile of the fill plan, then the hit rays' L values),
+    gathered into one buffer and unpacked by one xrt_unpack_hits_device launch,
+    equal the single-device frame's three planes bit for bit; the message is
+    2 words per planned tile plus one per hit ray; no mask disagrees with its
+    plan."""
+    import torch
+    from simpleraytracing_amd.strips import hit_descriptors
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    spans = list(zip(cuts[:-1], cuts[1:]))
+    maps, plans, msgs = [], [], []
+    for r0, r1 in spans:
+        with xrt.Context(0) as c:
+            c.set_kernel(xrt.XRT_KERNEL_BINNED)
+            c.upload_mesh(dragon)
+            rmap, hits, msg = _hit_strip(c, cam, W, r0, r1, dev, stream)
+            st = c.read_stats()
+        assert int(hits.sum()) == st.hit_rays          # every hit ray of the strip travels, once
+        maps.append(rmap)
+        plans.append(hits)
+        msgs.append(msg)
+    desc, tdesc, bases, words, total = hit_descriptors(W, spans, maps, plans)
+    assert words == [max(m.numel(), 4) for m in msgs]
+    rbuf = torch.zeros(total, dtype=torch.float32, device=dev)
+    for b, m in zip(bases, msgs):
+        rbuf[b:b + m.numel()] = m
+    d_desc = torch.from_numpy(desc.reshape(-1).view(np.int32)).to(dev)
+    d_tdesc = torch.from_numpy(tdesc.reshape(-1).view(np.int32)).to(dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = [torch.full((W * H,), -2.0, device=dev), torch.full((W * H,), -2.0, device=dev),
+           torch.zeros(W * H, dtype=torch.uint8, device=dev)]
+    with xrt.Context(0) as c:
+        c.unpack_hits_device(W, len(desc), d_desc.data_ptr(), d_tdesc.data_ptr(), rbuf.data_ptr(), out[0].data_ptr(),
+                             out[1].data_ptr(), out[2].data_ptr(), bad.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert int(bad.item()) == 0
+        c.upload_mesh(dragon)
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        ref = c.render_rows(cam)
+    assert np.array_equal(bits(out[1].cpu().numpy()), bits(ref[0]))
+    assert np.array_equal(bits(out[0].cpu().numpy()), bits(ref[1]))
+    assert np.array_equal(out[2].cpu().numpy(), ref[2])
+
+
+def test_hit_transit_guards(dragon):
+    """The hit layout's guards: a message whose mask disagrees with the plan
+    sets the unpack's flag; a frame of another geometry (or with no plan) is
+    not rendered (XRT_ERR_OVERFLOW); image / u8 planes have no hit layout; the
+    plan needs a binned frame over a fill plan just before."""
+    import torch
+    from simpleraytracing_amd.strips import hit_descriptors
+    W, H, r0, r1 = 1024, 1024, 256, 768
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    cam2 = xrt.camera_from_bbox(*oracle.bbox(dragon[:5000]), W, H)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        with pytest.raises(RuntimeError):             # no frame yet
+            c.plan_hit_layout()
+        rmap, hits, msg = _hit_strip(c, cam, W, r0, r1, dev, stream, frames=1)
+        big = torch.zeros(msg.numel() + 64, device=dev)
+        c.set_transit_hits(big.numel())
+        try:
+            with pytest.raises(RuntimeError):         # another camera: not this plan's geometry
+                c.render_rows_device(cam2, r0, r1, 0, big.data_ptr(), 0, stream.cuda_stream)
+            img = torch.zeros(W * (r1 - r0), device=dev)
+            with pytest.raises(RuntimeError):
+                c.render_rows_device(cam, r0, r1, img.data_ptr(), big.data_ptr(), 0, stream.cuda_stream)
+        finally:
+            c.set_transit_hits(0)
+        c.set_transit_hits(msg.numel())               # no room for a tile's overrun
+        try:
+            with pytest.raises(RuntimeError):
+                c.render_rows_device(cam, r0, r1, 0, big.data_ptr(), 0, stream.cuda_stream)
+        finally:
+            c.set_transit_hits(0)
+        torch.cuda.synchronize(dev)
+    desc, tdesc, bases, words, total = hit_descriptors(W, [(r0, r1)], [rmap], [hits])
+    d_desc = torch.from_numpy(desc.reshape(-1).view(np.int32)).to(dev)
+    d_tdesc = torch.from_numpy(tdesc.reshape(-1).view(np.int32)).to(dev)
+    out = torch.zeros(W * H, device=dev)
+    i = int(np.flatnonzero(hits)[0])                  # a tile with hits: drop one from its mask
+    bad_msg = msg.clone()
+    m = bad_msg[2 * i:2 * i + 2].view(torch.int32).cpu().numpy().view(np.uint32).copy()
+    lo = int(m[0]) | (int(m[1]) << 32)
+    lo &= lo - 1
+    bad_msg[2 * i:2 * i + 2] = torch.from_numpy(np.array([lo & 0xFFFFFFFF, lo >> 32], np.uint32).view(np.float32))
+    for src, expect in ((msg, 0), (bad_msg, 1)):
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        with xrt.Context(0) as c:
+            c.unpack_hits_device(W, len(desc), d_desc.data_ptr(), d_tdesc.data_ptr(), src.data_ptr(),
+                                 out.data_ptr(), 0, 0, bad.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+        assert int(bad.item()) == expect
+
+
 @pytest.mark.parametrize("transit,ranks,share,size", [("packed", 2, "auto", 512), ("dense", 2, "auto", 512),
                                                        ("packed", 3, "equal", 512), ("dense", 3, "0.5", 512),
                                                        ("packed", 3, "balanced", 512), ("dense", 2, "balanced", 512),
                                                        ("packed", 4, "balanced", 512),
+                                                       ("hits", 2, "auto", 512), ("hits", 3, "balanced", 512),
+                                                       ("hits", 4, "equal", 1024),
                                                        ("packed", 8, "balanced", 4096)])
 def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
     """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
@@ -1284,7 +1457,7 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
     listed 8 times (one-rank RCCL), bit-equal as well."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    port = 29500 + (os.getpid() % 1000) + (7 if transit == "dense" else 0) + 13 * ranks
+    port = 29500 + (os.getpid() % 1000) + {"dense": 7, "hits": 3}.get(transit, 0) + 13 * ranks
     capi = ranks == 8
     cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
@@ -1318,7 +1491,7 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
         assert g["split"]["link_bytes_per_us"] > 0 and g["split"]["predicted_step_us"] > 0
     else:
         assert rows[0] > size // ranks
-    if transit == "packed":
+    if transit in ("packed", "hits"):
         assert g["bytes_gathered_per_step"] < g["dense_bytes_per_step"]
     else:
         assert g["bytes_gathered_per_step"] == g["dense_bytes_per_step"]
