@@ -1267,7 +1267,20 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
         double gamma = ps * rtn;   // per image column
         double l1n = l1_d(N[k]);
         double M = 4.0 * ((B[k] + 12.0 * kEps * l1n) * cp.dmax + 8.0 * kEps * cp.mag * l1n);
-        double nrm = sqrt(beta * beta + gamma * gamma);
+        // The edge is scaled by 1 / |(beta, gamma)|.  Any positive scale keeps
+        // the inequality; the unit length only makes the margins below pixel
+        // distances, so an approximate one serves: v_rsq_f32 (relative error
+        // ~1e-7) where beta^2 + gamma^2 is in f32's normal range, instead of an
+        // f64 sqrt and three f64 divisions per edge.
+        const double nn = beta * beta + gamma * gamma;
+        double nrm, inv_nrm;
+        if (nn > 0x1p-120 && nn < 0x1p120) {
+            inv_nrm = (double)__builtin_amdgcn_rsqf((float)nn);
+            nrm = 1.0 / inv_nrm;
+        } else {
+            nrm = sqrt(nn);
+            inv_nrm = 1.0 / nrm;
+        }
         if (!(nrm > 1e-30 * (fabs(alpha) + M + 1e-300))) {
             // Edge function constant over the image plane.
             if (s * alpha + M < 0.0) {
@@ -1282,9 +1295,9 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
             constant_edge = true;
             continue;
         }
-        double a = s * gamma / nrm;
-        double b = s * beta / nrm;
-        double cc = (s * alpha + M) / nrm;
+        double a = s * gamma * inv_nrm;
+        double b = s * beta * inv_nrm;
+        double cc = (s * alpha + M) * inv_nrm;
         cc += 0.05 + 64.0 * kEps * (cp.width + cp.height + fabs(cc));
         ea[k] = (float)a;
         eb[k] = (float)b;
@@ -1310,10 +1323,11 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
             double vx[3], vy[3];
             const int pi[3] = {0, 1, 2}, pj[3] = {1, 2, 0};
             const double cr[3] = {x01, x12, x20};
-            for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < 3; ++q) {     // (the box's margins cover the reciprocal's rounding)
                 int ii = pi[q], jj = pj[q];
-                vx[q] = (-Cq[ii] * Bq[jj] + Cq[jj] * Bq[ii]) / cr[q];
-                vy[q] = (-A[ii] * Cq[jj] + A[jj] * Cq[ii]) / cr[q];
+                const double inv_cr = 1.0 / cr[q];
+                vx[q] = (-Cq[ii] * Bq[jj] + Cq[jj] * Bq[ii]) * inv_cr;
+                vy[q] = (-A[ii] * Cq[jj] + A[jj] * Cq[ii]) * inv_cr;
             }
             double xmin = fmin(vx[0], fmin(vx[1], vx[2])), xmax = fmax(vx[0], fmax(vx[1], vx[2]));
             double ymin = fmin(vy[0], fmin(vy[1], vy[2])), ymax = fmax(vy[0], fmax(vy[1], vy[2]));
@@ -1333,9 +1347,10 @@ __device__ Footprint compute_footprint(const TriRec& r, const RenderParams& p, c
                 const double iw = cp.width + 2.0, ih = cp.height + 2.0;
                 const double area = fmin(0.5 * fabs((vx[1] - vx[0]) * (vy[2] - vy[0]) - (vx[2] - vx[0]) * (vy[1] - vy[0])),
                                          iw * ih);
-                double perim = 0.0;
+                double perim = 0.0;         // (a size estimate: f32 square roots serve)
                 for (int q = 0; q < 3; ++q)
-                    perim += sqrt((vx[pj[q]] - vx[q]) * (vx[pj[q]] - vx[q]) + (vy[pj[q]] - vy[q]) * (vy[pj[q]] - vy[q]));
+                    perim += (double)__builtin_amdgcn_sqrtf(
+                        (float)((vx[pj[q]] - vx[q]) * (vx[pj[q]] - vx[q]) + (vy[pj[q]] - vy[q]) * (vy[pj[q]] - vy[q])));
                 perim = fmin(perim, 2.0 * (iw + ih));
                 c.e2.w = (float)(area / (kRegion * kRegion) + 2.0 * perim / kRegion + 8.0);
             }
