@@ -1399,6 +1399,17 @@ static_assert(kRankCache % 64u == 0u, "whole DMA rounds");
 #ifndef XRT_PREP_BUFFER_OPS
 #define XRT_PREP_BUFFER_OPS 1
 #endif
+// Per-wave aggregation of the commit's count atomics (0: off): when the union
+// of the wave's region rectangles has at most kAggCells cells, the wave's pairs
+// first count per cell in LDS (each pair's offset in its cell from an LDS
+// atomic), then ONE global atomic per cell with pairs returns the cell's base
+// -- a wave's triangles are mesh-adjacent, so its pairs share few regions.
+#ifndef XRT_PREP_AGG
+#define XRT_PREP_AGG 1
+#endif
+constexpr uint32_t kAggCells = 256;
+static_assert(!(XRT_PREP_AGG && XRT_PREP_RANK_LDS), "one cell-indexed queue layout at a time");
+static_assert(!XRT_PREP_AGG || XRT_PREP_BUFFER_OPS, "the aggregated commit uses the buffer-op tables");
 constexpr int kBufferWord3 = 0x00020000;          // raw buffer resource, gfx9 family (32-bit elements)
 constexpr uint32_t kBufferOut = 0x80000000u;      // an offset past every buffer: no-op access
 
@@ -1706,6 +1717,27 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+#if XRT_PREP_AGG
+    // the union of the wave's rectangles (wave-uniform)
+    uint32_t ax0 = 0, ay0 = 0, aw = 0, acells = 0;
+    if (__ballot(has) != 0ull) {
+        ax0 = ~wave_reduce_u32<true>(has ? ~x0 : 0u);
+        ay0 = ~wave_reduce_u32<true>(has ? ~y0 : 0u);
+        const uint32_t ax1 = wave_reduce_u32<true>(has ? x1 : 0u);
+        const uint32_t ay1 = wave_reduce_u32<true>(has ? y1 : 0u);
+        aw = ax1 - ax0 + 1u;
+        acells = aw * (ay1 - ay0 + 1u);
+    }
+    const bool agg = acells <= kAggCells;
+    __shared__ uint32_t s_acnt[kPrepWaves][kAggCells];   // per cell: its pairs' count, then its base slot
+    __shared__ uint32_t s_alb[kPrepWaves][kAggCells];    //           its list's base
+    __shared__ uint32_t s_alc[kPrepWaves][kAggCells];    //           its list's capacity
+    __shared__ uint8_t s_qoff[kPrepWaves][kBinQueue];    // per queued pair: its offset in its cell
+    cached = agg;                                  // the queue holds cell indices (enqueue)
+    ux0 = ax0;
+    uy0 = ay0;
+    uw = aw;
+#endif
     // No lists (the sizing pass of a new geometry, DESIGN.md "List sizing"):
     // the pairs are counted, nothing is stored, nothing can overflow.
     const uint32_t count_only = wave_uniform(bins.list == nullptr ? 1u : 0u);
@@ -1723,6 +1755,82 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
     auto commit = [&]() {
+#if XRT_PREP_AGG
+        if (agg) {
+            // (a) per-cell counts in LDS; each pair's offset in its cell
+            for (uint32_t c = lane; c < acells; c += 64u) s_acnt[wave][c] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t q = lane; q < queued; q += 64u)
+                s_qoff[wave][q] = (uint8_t)atomicAdd(&s_acnt[wave][s_qreg[wave][q]], 1u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // (b) one count atomic per cell with pairs: every cell's slot loads,
+            // then every atomic and list description, in flight together
+            constexpr uint32_t kAggRounds = kAggCells / 64u;
+            uint32_t cn[kAggRounds], cs[kAggRounds], cb[kAggRounds], clb[kAggRounds], clc[kAggRounds];
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) {
+                const uint32_t c = k * 64u + lane;
+                cn[k] = c < acells ? s_acnt[wave][c] : 0u;
+                const uint32_t region = (ay0 + c / max(aw, 1u)) * bins.regions_x + ax0 + c % max(aw, 1u);
+                cs[k] = __builtin_amdgcn_raw_buffer_load_b32(r_rank, cn[k] ? region * 4u : kBufferOut, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) cs[k] = cn[k] ? cs[k] : kEmpty;
+            bool planned_empty = false;            // pairs for a region the fill plan fills
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) planned_empty |= cs[k] != kEmpty && cs[k] >= bins.tile_slots;
+            if (__builtin_expect(bins.plan_miss != nullptr && __ballot(planned_empty) != 0ull, 0) && lane == 0)
+                *bins.plan_miss = 1u;
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k)
+                cb[k] = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+                    (int)cn[k], r_cnt, cs[k] != kEmpty ? cs[k] * (kCounterStride * 4u) : kBufferOut, 0, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) {
+                const auto bc = __builtin_amdgcn_raw_buffer_load_b64(
+                    r_desc, cs[k] != kEmpty && count_only == 0u ? cs[k] * (uint32_t)sizeof(SlotDesc) : kBufferOut, 0,
+                    0);
+                clb[k] = bc[0];
+                clc[k] = bc[1];
+            }
+            if (count_only) {                       // the sizing pass: counts only
+                __builtin_amdgcn_wave_barrier();
+                queued = 0;
+                return;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) {
+                const uint32_t c = k * 64u + lane;
+                if (cs[k] == kEmpty) continue;
+                my_max = max(my_max, cb[k] + cn[k]);
+                if (cb[k] + cn[k] > clc[k]) over = true;
+                s_acnt[wave][c] = cb[k];
+                s_alb[wave][c] = clb[k];
+                s_alc[wave][c] = clc[k];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // (c) the entries
+            for (uint32_t q = lane; q < queued; q += 64u) {
+                const uint32_t c = s_qreg[wave][q];
+                const uint32_t idx = s_acnt[wave][c] + s_qoff[wave][q];
+                if (idx < s_alc[wave][c]) {
+                    float4* e = reinterpret_cast<float4*>(bins.list + (size_t)s_alb[wave][c] + idx);
+                    const uint32_t own = s_qown[wave][q];
+#pragma unroll
+                    for (uint32_t w = 0; w < kEntryQuads; ++w) e[w] = s_fp[wave][w][own];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();      // the queue is refilled after every lane read it
+            queued = 0;
+            return;
+        }
+#endif
 #if XRT_PREP_RANK_LDS
         if (cached && !rank_waited) {              // the slots' DMA has landed (issued before phase 1)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
