@@ -1566,6 +1566,9 @@ __device__ __forceinline__ bool bin_rect(float4 bb, float reach, const RenderPar
 // k_prep runs beside the previous frame's render: single-wave workgroups fit
 // the holes that retiring render waves leave (a 4-wave one needs a free slot
 // on all four SIMDs of a CU at once).
+#ifndef XRT_PREP_PRIO
+#define XRT_PREP_PRIO 0   // k_prep's wave priority (s_setprio; 0: the render's)
+#endif
 constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
 constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 #ifndef XRT_PREP_TRIS
@@ -1595,6 +1598,9 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     // i: the thread's index over the grid (pixel-offset tables, counter
     // clears); tri: its triangle -- p.prep_tris per wave (fewer than 64 spreads
     // the binning's cells and commits of a frame over more waves).
+#if XRT_PREP_PRIO
+    __builtin_amdgcn_s_setprio(XRT_PREP_PRIO);
+#endif
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t tri_lane = threadIdx.x & 63u;
     const uint32_t tri = (blockIdx.x * kPrepWaves + (threadIdx.x >> 6)) * p.prep_tris + tri_lane;
