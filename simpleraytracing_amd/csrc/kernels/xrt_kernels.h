@@ -409,7 +409,11 @@ __device__ float wave_overflow_distance(const TriRec* __restrict__ recs, uint32_
     float distance = 0.0f;
     if (most <= (uint32_t)kFixupSlots) {
         constexpr uint32_t N = 64u * kFixupSlots;
+        // rolled loops: unrolled, this rare path is most of the render's code
+        // (and its instruction cache footprint)
+#pragma nounroll
         for (uint32_t size = 2; size <= N; size <<= 1) {
+#pragma nounroll
             for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
                 if (stride >= 64u) {
                     const uint32_t ss = size >> 6;
@@ -431,6 +435,7 @@ __device__ float wave_overflow_distance(const TriRec* __restrict__ recs, uint32_
 #pragma unroll
         for (uint32_t r = 0; r < (uint32_t)kFixupSlots; ++r) {
             const float d = __shfl_xor(v[r], 1) - v[r];
+#pragma nounroll
             for (uint32_t l = 0; l < 64u && r * 64u + l + 1u < total; l += 2u)
                 distance += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), (int)l));
         }
@@ -2383,29 +2388,32 @@ __device__ __forceinline__ void render_binned(RecStage* st, const TriRec* __rest
         return b;
     };
     // Split regions first (BinBuffers::split_slots, heaviest first): two waves
-    // per tile, 2 * kBlocksPerRegion workgroups a region.
+    // per tile, 2 * kBlocksPerRegion workgroups a region; then the other tile
+    // regions, one wave per tile.  One render_tile call site for both: inlined
+    // twice, the render's code outgrew the instruction cache.
     const uint32_t split_blocks = split_slots * 2u * kBlocksPerRegion;
+    uint32_t slot, tile, split = kSplitNone;
+    const RecStage* partner = nullptr;
     if (!kSigned && blockIdx.x < split_blocks) {                     // workgroup-uniform
         const uint32_t blk = xcd_remap(blockIdx.x, split_blocks, 2u * kBlocksPerRegion);
         const uint32_t g = blk * kTileWaves + wave;                  // wave of the split segment
-        const uint32_t slot = g / (2u * kWavesPerRegion);
-        const uint32_t tile = (g / 2u) % kWavesPerRegion;
-        const uint32_t half = g & 1u;
-        render_tile<kSigned, kHits>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand,
-                             half ? kSplitHalf1 : kSplitHalf0, &st[kCanSplit ? wave ^ 1u : wave]);
-        if (!half)                                 // one record per tile (the region's 16), by half 0
-            store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, slot * kWavesPerRegion + tile,
-                             out.wave_times, t_start);
-        return;
+        slot = g / (2u * kWavesPerRegion);
+        tile = (g / 2u) % kWavesPerRegion;
+        split = (g & 1u) ? kSplitHalf1 : kSplitHalf0;
+        partner = &st[kCanSplit ? wave ^ 1u : wave];
+    } else {
+        const uint32_t blk = split_blocks + xcd_remap(blockIdx.x - split_blocks, tile_blocks - split_blocks / 2u,
+                                                      kBlocksPerRegion);
+        const uint32_t g = (blk - split_blocks / 2u) * kTileWaves + wave; // wave of the grid (16 per region)
+        slot = g / kWavesPerRegion;                  // workgroup-uniform
+        tile = g % kWavesPerRegion;
     }
-    const uint32_t blk = split_blocks + xcd_remap(blockIdx.x - split_blocks, tile_blocks - split_blocks / 2u,
-                                                  kBlocksPerRegion);
-    const uint32_t g = (blk - split_blocks / 2u) * kTileWaves + wave; // wave of the grid (16 per region)
-    const uint32_t slot = g / kWavesPerRegion;       // workgroup-uniform
-    const uint32_t tile = g % kWavesPerRegion;
-    render_tile<kSigned, kHits>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand);
-    // candidates are counted once per region (by the wave holding tile 0)
-    store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, g, out.wave_times, t_start);
+    render_tile<kSigned, kHits>(st[wave], recs, culls, p, out, bins, n_glob, slot, tile, ws, cand, split, partner);
+    // one record per tile (a split tile's by half 0); candidates are counted
+    // once per region (by the wave holding tile 0)
+    if (split != kSplitHalf1)
+        store_wave_stats(ws, tile == 0u ? cand : 0u, out.block_stats, slot * kWavesPerRegion + tile,
+                         out.wave_times, t_start);
 }
 
 template <bool kSigned>

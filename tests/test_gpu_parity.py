@@ -1337,7 +1337,7 @@ def _hit_strip(c, cam, W, r0, r1, dev, stream, frames=3):
     return rmap, hits, msg[:words]
 
 
-@pytest.mark.parametrize("W,H,cuts", [(1000, 700, [0, 700]), (2048, 2048, [0, 900, 2048]),
+@pytest.mark.parametrize("W,H,cuts", [(1000, 700, [0, 700]), (2048, 2048, [0, 900, 2048]), (1024, 1024, [0, 32, 1024]),
                                       (333, 517, [0, 100, 400, 517]), (4096, 4096, [0, 1536, 2560, 4096])])
 def test_hit_transit_equals_direct_render(dragon, W, H, cuts):
     """Strips rendered straight into the hit layout (xrt_set_transit_hits: a
