@@ -18,13 +18,15 @@ render are inside it.
                  loaded clocks (at_loaded_clocks, reported beside `value`).
   --gpus N > 1 (default --mode strips, 4096x4096: BASELINE configs[3]):
                  strong scaling -- one frame per step split into row strips
-                 (rows_per = H/N, remainder to the first, as
+                 (--root-share balanced: from the frame's per-band render cost
+                 and transit bytes, strips.balanced_bounds; 'equal': H/N, as
                  main-pthreads-rows.cxx:311-334); every rank but 0 sends its
-                 strip's L-buffer (misses coded XRT_MISS_TRANSIT, 4 B per
-                 pixel) to rank 0 over RCCL, which receives it into its frame
-                 and expands the image and u8 planes from it; frame k's gather
-                 overlaps frame k+1's render.  The gathered frame is checked bit
-                 for bit against rank 0's own single-device render after timing.
+                 strip to rank 0 over RCCL (--transit hits: per 8x8 tile a hit
+                 mask and the hit rays' L values; packed / dense as named),
+                 which expands it into its frame's three planes; frame k's
+                 gather overlaps frame k+1's render.  The gathered frame is
+                 checked bit for bit against rank 0's own single-device render
+                 after timing.
   --mode frames  weak scaling: every rank renders whole frames, no exchange.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size W H]
