@@ -1498,8 +1498,9 @@ def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
 
 
 def test_render_frames_batch_equals_single_calls(dragon):
-    """xrt_render_frames_device: 7 frames of one geometry in ONE call, alternating
-    two plane sets on two streams (each frame prepared and rendered in full) --
+    """xrt_render_frames_device: 7, 5 and 12 frames of one geometry, each run in ONE
+    call, alternating two plane sets on two streams (each frame prepared and
+    rendered in full) --
     every set's last frame bit-equal to a single xrt_render_rows; the
     host-buffer xrt_render_frames likewise, with its per-frame device time."""
     import torch
@@ -1513,8 +1514,10 @@ def test_render_frames_batch_equals_single_calls(dragon):
         with xrt.Context(0) as c:
             c.upload_mesh(dragon)
             ref = c.render_rows(cam, r0, r1)
-            c.render_frames_device(cam, r0, r1, 7, [(a.data_ptr(), b.data_ptr(), u.data_ptr(), s.cuda_stream)
-                                                    for a, b, u, s in sets])
+            # 7, 5, then 12 frames (each call's sets start where the last one's ended)
+            for nf in (7, 5, 12):
+                c.render_frames_device(cam, r0, r1, nf, [(a.data_ptr(), b.data_ptr(), u.data_ptr(), s.cuda_stream)
+                                                         for a, b, u, s in sets])
             torch.cuda.synchronize(dev)
             for a, b, u, _ in sets:
                 for x, y in zip((a, b, u), ref[:3]):
