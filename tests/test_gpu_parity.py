@@ -1446,18 +1446,18 @@ def test_hit_transit_guards(dragon):
                                                        ("packed", 4, "balanced", 512),
                                                        ("hits", 2, "auto", 512), ("hits", 3, "balanced", 512),
                                                        ("hits", 4, "equal", 1024),
-                                                       ("packed", 8, "balanced", 4096)])
+                                                       ("packed", 8, "balanced", 4096), ("hits", 8, "balanced", 4096)])
 def test_bench_strips_two_ranks_one_gpu(tmp_path, transit, ranks, share, size):
     """bench.py's N > 1 path (row strips, transit L-buffers sent to rank 0 --
     packed by region or dense --, expanded there) with 2-8 ranks on the one GPU
     (gloo, host-staged): the gathered frame is bit-equal to rank 0's
-    single-device render.  The 8-rank case is BASELINE configs[3]'s real split
-    (4096^2, 8 strips, balanced, packed), and it also runs the bench's
+    single-device render.  The 8-rank cases are BASELINE configs[3]'s real split
+    (4096^2, 8 strips, balanced; packed, and hits -- the default), and they also run the bench's
     capi_multi leg: the C ABI's xrt_render_rows_multi_device over device 0
     listed 8 times (one-rank RCCL), bit-equal as well."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    port = 29500 + (os.getpid() % 1000) + {"dense": 7, "hits": 3}.get(transit, 0) + 13 * ranks
+    port = 29500 + (os.getpid() % 1000) + {"dense": 7, "hits": 3}.get(transit, 0) + 13 * ranks + (size == 4096)
     capi = ranks == 8
     cmd = ["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
