@@ -1386,6 +1386,14 @@ def test_hit_transit_equals_direct_render(dragon, W, H, cuts):
     assert np.array_equal(out[2].cpu().numpy(), ref[2])
 
 
+def test_hit_transit_split_tiles_exact(dragon, monkeypatch):
+    """The hit layout with split tiles (XRT_SPLIT_MIN=1: every non-empty
+    region's tiles by two waves; half 0 stores the tile's mask and hits):
+    strips gathered and unpacked equal the single-device frame bit for bit."""
+    monkeypatch.setenv("XRT_SPLIT_MIN", "1")
+    test_hit_transit_equals_direct_render(dragon, 1024, 1024, [0, 256, 768, 1024])
+
+
 def test_hit_transit_guards(dragon):
     """The hit layout's guards: a message whose mask disagrees with the plan
     sets the unpack's flag; a frame of another geometry (or with no plan) is
