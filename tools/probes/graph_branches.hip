@@ -1,7 +1,7 @@
 // Probe: does a hipGraph run two independent kernel nodes at once on gfx950?
 // Two one-workgroup kernels that each spin for ~20 us (s_memrealtime, 100 MHz):
 // launched as a graph with no edge between them, as a graph with an edge, and
-// on two streams.  If the no-edge graph takes ~20 us per replay the runtime
+// on two streams (joined after every pair, and free).  If the no-edge graph takes ~20 us per replay the runtime
 // overlaps the branches (a frame graph could keep k_prep beside the previous
 // render); ~40 us means it serialises them.
 #include <hip/hip_runtime.h>
@@ -54,14 +54,17 @@ int main()
         CK(hipGraphDestroy(g));
     }
     const int n = 200;
-    const char* names[] = {"graph, no edge", "graph, edge", "two streams"};
-    for (int mode = 0; mode < 3; ++mode) {
+    const char* names[] = {"graph, no edge", "graph, edge", "two streams", "two streams, free"};
+    for (int mode = 0; mode < 4; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {
             CK(hipDeviceSynchronize());
             const auto t0 = Clock::now();
             for (int i = 0; i < n; ++i) {
                 if (mode < 2) {
                     CK(hipGraphLaunch(ex[mode], s0));
+                } else if (mode == 3) {               // no joins: each stream runs its own chain
+                    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s0, ticks, d);
+                    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s1, ticks, d);
                 } else {
                     hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s0, ticks, d);
                     hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s1, ticks, d);
