@@ -65,7 +65,8 @@ def test_hit_descriptors_round_trip():
     a sender's render writes them (per planned tile a 64-bit hit mask, then
     the hit values in bit order) and decoded through desc / tdesc exactly as
     k_unpack_hits reads them give back every hit of every strip, and misses
-    elsewhere; messages start at 16-B aligned words."""
+    elsewhere; messages start at 16-B aligned words; a strip with no planned
+    tile sends the minimum message."""
     from simpleraytracing_amd.strips import EMPTY, hit_descriptors
     W = 100
     spans = [(10, 77), (77, 131), (131, 140)]
@@ -76,7 +77,8 @@ def test_hit_descriptors_round_trip():
         ry = -(-(e - b) // 32)
         n = rx * ry
         m = np.full(n, EMPTY, np.uint32)
-        keep = np.sort(rng.choice(n, max(n // 2, 1), replace=False))
+        # the last strip: every region filled by its plan (no tile travels)
+        keep = np.sort(rng.choice(n, 0 if b == 131 else max(n // 2, 1), replace=False))
         m[keep] = rng.permutation(len(keep))
         n_slots = len(keep)
         masks = np.zeros(16 * n_slots, np.uint64)
