@@ -1346,9 +1346,25 @@ def test_hit_transit_equals_direct_render(dragon, W, H, cuts):
     equal the single-device frame's three planes bit for bit; the message is
     2 words per planned tile plus one per hit ray; no mask disagrees with its
     plan."""
+    _hit_transit_frame(dragon, W, H, cuts, xrt.camera_for_mesh(dragon, W, H))
+
+
+def test_hit_transit_empty_strips(dragon):
+    """A strip whose every region the fill plan fills (the camera zoomed out,
+    the top rows clear of the mesh): no tile of it travels -- a plan of 0
+    tiles, the minimum message -- and the gathered frame still equals the
+    single-device frame bit for bit."""
+    W = H = 1024
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    cam.pixel_spacing *= 3.0
+    plans = _hit_transit_frame(dragon, W, H, [0, 160, 864, 1024], cam)
+    assert len(plans[0]) == 0 and len(plans[1]) > 0     # (the mesh reaches the bottom strip)
+
+
+def _hit_transit_frame(dragon, W, H, cuts, cam):
+    """test_hit_transit_equals_direct_render's body; returns the strips' plans."""
     import torch
     from simpleraytracing_amd.strips import hit_descriptors
-    cam = xrt.camera_for_mesh(dragon, W, H)
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     spans = list(zip(cuts[:-1], cuts[1:]))
@@ -1384,6 +1400,7 @@ def test_hit_transit_equals_direct_render(dragon, W, H, cuts):
     assert np.array_equal(bits(out[1].cpu().numpy()), bits(ref[0]))
     assert np.array_equal(bits(out[0].cpu().numpy()), bits(ref[1]))
     assert np.array_equal(out[2].cpu().numpy(), ref[2])
+    return plans
 
 
 def test_hit_transit_split_tiles_exact(dragon, monkeypatch):
@@ -1391,7 +1408,7 @@ def test_hit_transit_split_tiles_exact(dragon, monkeypatch):
     region's tiles by two waves; half 0 stores the tile's mask and hits):
     strips gathered and unpacked equal the single-device frame bit for bit."""
     monkeypatch.setenv("XRT_SPLIT_MIN", "1")
-    test_hit_transit_equals_direct_render(dragon, 1024, 1024, [0, 256, 768, 1024])
+    _hit_transit_frame(dragon, 1024, 1024, [0, 256, 768, 1024], xrt.camera_for_mesh(dragon, 1024, 1024))
 
 
 def test_hit_transit_guards(dragon):
