@@ -963,6 +963,30 @@ def test_multi_rccl_gather_one_rank(dragon, devices, W, H):
                     assert np.array_equal(bits(x), bits(y))
 
 
+def test_multi_hit_transit_empty_strips(dragon):
+    """xrt_render_rows_multi over 8 equal strips with the camera zoomed out, so
+    the top strips' regions are all filled by their plans (no tile of theirs
+    travels): the hit frames equal one device's frame bit for bit."""
+    W = H = 1024
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    cam.pixel_spacing *= 3.0
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        ref = one.render_rows(cam)
+    with xrt.MultiContext([0] * 8) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        m.set_gather(xrt.XRT_GATHER_RCCL)
+        m.set_split(xrt.XRT_SPLIT_EQUAL)
+        for _ in range(3):                                     # packed, then hits
+            got = m.render(cam)
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y))
+        st = m.transit_stats()
+        assert st["frames_packed"] == 1 and st["frames_hits"] == 2 and st["bad"] == 0, st
+
+
 @pytest.mark.parametrize("gather", ["rccl", "copy"])
 def test_multi_hit_transit(dragon, gather):
     """xrt_render_rows_multi's hit transit (XRT_TRANSIT_HITS, the default): a
