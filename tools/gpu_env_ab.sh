@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of one environment knob of the production library: the GPU tests named
 # by TESTS under each setting, then the bench per config, REPS times each.
-# Usage: KNOB=XRT_PREP_STREAMS VALUES="1 2" TESTS="prepared_ahead or frames_batch" tools/gpu_env_ab.sh TAG
+# Usage: KNOB=XRT_TILE_PLAN VALUES="0 1" TESTS="fill_plan or frames_batch" tools/gpu_env_ab.sh TAG
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-env_ab}; mkdir -p $OUT
