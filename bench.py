@@ -75,6 +75,11 @@ def parse():
                     help="frames mode: frame k's camera is the default one turned k*DEG degrees about the "
                          "detector's up axis through the mesh centre (a projection sweep: every frame a "
                          "new geometry for the region lists); 0 = one camera")
+    ap.add_argument("--orbit-legs", type=float, nargs="*", default=[0.25, 1.0], metavar="DEG",
+                    help="after the timed region (one GPU, frames mode): a moving-camera leg per value, the camera "
+                         "turning DEG degrees per frame (reported under `orbit`, never `value`); none: no legs")
+    ap.add_argument("--orbit-frames", type=int, default=60,
+                    help="timed frames per orbit leg (at least --steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
@@ -564,17 +569,19 @@ def capi_multi_only(args) -> int:
         m.set_split(xrt.XRT_SPLIT_BALANCED if args.capi_split == "balanced" else xrt.XRT_SPLIT_EQUAL)
         # (--transit dense has no C-ABI counterpart: the blocks of the fill plan)
         m.set_transit(xrt.XRT_TRANSIT_HITS if args.transit == "hits" else xrt.XRT_TRANSIT_PACKED)
-        t_p = time.perf_counter()
-        bounds, info = m.plan(cam)
-        plan_ms = (time.perf_counter() - t_p) * 1e3
         img = torch.empty(W * H, dtype=torch.float32, device=dev)
         lb = torch.empty(W * H, dtype=torch.float32, device=dev)
         u8 = torch.empty(W * H, dtype=torch.uint8, device=dev)
         s = torch.cuda.Stream(dev)
         ptrs = (img.data_ptr(), lb.data_ptr(), u8.data_ptr(), s.cuda_stream)
+        # the first frame splits equally and models the split from its strips'
+        # records; the next frames take the balanced split planned from them
+        t_w = time.perf_counter()
         for _ in range(max(args.warmup, 1)):
             m.render_device(cam, *ptrs)
         s.synchronize()
+        warm_ms = (time.perf_counter() - t_w) * 1e3
+        bounds, info = m.plan(cam)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             m.render_device(cam, *ptrs)
@@ -582,6 +589,7 @@ def capi_multi_only(args) -> int:
         dt = time.perf_counter() - t0
         st = m.read_stats()
         transit = m.transit_stats()
+        plan_stats = m.plan_stats()
     ok = (np.array_equal(img.cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
           and np.array_equal(lb.cpu().numpy().view(np.uint32), ref[1].view(np.uint32))
           and np.array_equal(u8.cpu().numpy(), ref[2]))
@@ -590,7 +598,7 @@ def capi_multi_only(args) -> int:
            "gather": "RCCL, one communicator per device (ncclCommInitAll)" if distinct == len(devices) and distinct > 1
            else "RCCL, one rank (a device listed n times)" if distinct == 1 and len(devices) > 1 else "device copies",
            "split": args.capi_split, "strips": bounds, "strip_rows": [e - b for b, e in bounds],
-           "plan": info, "plan_ms": plan_ms, "steps": args.steps, "warmup": max(args.warmup, 1),
+           "plan": info, "plan_stats": plan_stats, "warmup_ms": warm_ms, "steps": args.steps, "warmup": max(args.warmup, 1),
            "ms_per_step": dt / args.steps * 1e3, "value": W * H * args.steps / dt / 1e6, "unit": "Mrays/s",
            "hit_rays": st.hit_rays, "transit": "hits" if args.transit == "hits" else "packed",
            "bytes_gathered_per_step": transit["last_bytes"], "transit_frames": transit,
@@ -950,6 +958,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    tp_before = ctx.tile_plan_counters()["frames"]
     ctx.timing_begin()
     GC.active = True
     t0 = time.perf_counter()
@@ -968,6 +977,11 @@ def main():
     kernel_ms, launches = ctx.timing_end()
     event_ms, event_launches = ctx.timing_events()
     stats = ctx.read_stats()
+    # Every timed frame culls from its own preparation: none may take the
+    # (opt-in) tile plan, which skips tiles an earlier identical frame found dead.
+    tile_plan_timed = ctx.tile_plan_counters()["frames"] - tp_before
+    if tile_plan_timed:
+        raise SystemExit(f"bench.py: {tile_plan_timed} timed frames used the tile plan")
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if nccl else "cpu")
     if world > 1:
@@ -1008,6 +1022,82 @@ def main():
                   "untimed_frames_before": n_load, "untimed_ms_before": load_ms,
                   "what": "after the timed region: --loaded-ms of untimed steps keep the GPU loaded (its clocks "
                           "ramp), then K steps timed as the region is; not the headline value"}
+
+    # Opt-in tile plan, never `value`: the same loop with it on (its frames skip
+    # the cull of tiles an earlier frame of the same camera found dead).
+    with_tile_plan = None
+    if root and not strips and not signed and not orbit_cams and world == 1 and args.steps > 0 and \
+            args.kernel in ("auto", "binned"):
+        ctx.set_tile_plan(True)
+        run_steps(max(args.warmup, 4))
+        torch.cuda.synchronize(dev)
+        tp0 = ctx.tile_plan_counters()["frames"]
+        t_p = time.perf_counter()
+        run_steps(args.steps)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t_p
+        tp_frames = ctx.tile_plan_counters()["frames"] - tp0
+        ctx.set_tile_plan(False)
+        with_tile_plan = {"value": W * H * args.steps / el / 1e6, "ms_per_step": el / args.steps * 1e3,
+                          "steps": args.steps, "tile_plan_frames": tp_frames,
+                          "what": "after at_loaded_clocks, the same loop with the opt-in tile plan "
+                                  "(xrt_debug_set_tile_plan): a tile without a survivor in an earlier frame of the "
+                                  "same camera skips its cull -- memoisation of an identical-frame loop, not `value`"}
+
+    # Moving camera (a projection sweep, the X-ray renderer's repeated
+    # workload): a fresh context per leg, the camera turning deg degrees per
+    # frame about the mesh centre, one xrt_render_rows_device call per frame
+    # (frames in flight as in the main loop), every frame prepared for its
+    # own camera.  The last frames are checked bit for bit afterwards.
+    orbit = None
+    if root and not strips and not signed and not orbit_cams and world == 1 and args.steps > 0 and \
+            args.orbit_legs:
+        orbit = {"fixed_camera_ms_per_step": elapsed_max / args.steps * 1e3}
+        lo_, hi_ = xrt.mesh_bbox(tris)
+        centre = 0.5 * (np.asarray(lo_, np.float64) + np.asarray(hi_, np.float64))
+        n_timed = max(args.steps, args.orbit_frames)
+        n_warm = 4
+        # planes of their own (the main loop's last frames are checked below)
+        oplanes = [(torch.zeros(W * H, dtype=torch.float32, device=dev), torch.zeros(W * H, dtype=torch.float32, device=dev),
+                    torch.zeros(W * H, dtype=torch.uint8, device=dev), s_f) for _, _, _, s_f in planes_of]
+        optrs = [(a.data_ptr(), b.data_ptr(), c.data_ptr(), s_f.cuda_stream) for a, b, c, s_f in oplanes]
+        for deg in args.orbit_legs:
+            cams_o = [orbit_camera(cam, centre, k * deg) for k in range(n_warm + n_timed)]
+            with xrt.Context(device_index) as oc:
+                oc.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
+                               "tiled": xrt.XRT_KERNEL_TILED, "binned": xrt.XRT_KERNEL_BINNED}[args.kernel])
+                oc.upload_mesh(tris)
+                for k in range(n_warm):
+                    img_k, lb_k, u8_k, s_k = optrs[k % inflight]
+                    oc.render_rows_device(cams_o[k], 0, H, img_k, lb_k, u8_k, s_k)
+                torch.cuda.synchronize(dev)
+                g0, q0 = oc.geometry_counters(), oc.pipeline_counters()
+                t_o = time.perf_counter()
+                for k in range(n_warm, n_warm + n_timed):
+                    img_k, lb_k, u8_k, s_k = optrs[k % inflight]
+                    oc.render_rows_device(cams_o[k], 0, H, img_k, lb_k, u8_k, s_k)
+                torch.cuda.synchronize(dev)
+                el = time.perf_counter() - t_o
+                g1, q1 = oc.geometry_counters(), oc.pipeline_counters()
+                exact = True
+                for j in range(inflight):
+                    k = n_warm + n_timed - 1 - j
+                    img_k, lb_k, u8_k, _ = oplanes[k % inflight]
+                    exact &= planes_equal((img_k.cpu().numpy(), lb_k.cpu().numpy(), u8_k.cpu().numpy()),
+                                          oc.render_rows(cams_o[k]))
+            if not exact:
+                raise SystemExit(f"bench.py: an orbit frame ({deg:g} deg per frame) differs from its synchronous render")
+            ms = el / n_timed * 1e3
+            orbit[f"deg_{deg:g}"] = {
+                "ms_per_step": ms, "value": W * H * n_timed / el / 1e6, "frames": n_timed, "warmup": n_warm,
+                "vs_fixed_camera": ms / orbit["fixed_camera_ms_per_step"],
+                "sizings": g1["sizings"] - g0["sizings"], "reused_lists": g1["reused"] - g0["reused"],
+                "plan_misses": g1["plan_misses"] - g0["plan_misses"], "overflows": g1["overflows"] - g0["overflows"],
+                "host_waits": q1["host_waits"] - q0["host_waits"], "last_frames_bit_exact": bool(exact)}
+        del oplanes
+        orbit["what"] = ("a fresh context per leg; the camera turns deg degrees per frame about the mesh centre "
+                         "(scenes.orbit_camera); one xrt_render_rows_device call per frame, frames in flight as in "
+                         "the main loop; each frame's k_prep bins its own camera; counters over the timed frames")
 
     # untimed: the gathered frame against rank 0's own render of the whole frame
     gather = None
@@ -1118,6 +1208,9 @@ def main():
             "untimed_frames_before_timed_region": untimed_before,
             "before_clock_ramp": cold,
             "at_loaded_clocks": loaded,
+            "tile_plan_frames_in_timed_region": tile_plan_timed,
+            "with_tile_plan": with_tile_plan,
+            "orbit": orbit,
             "latency": {"first_frame_ms": first_frame_ms,
                         "first_frame": "this context's first frame: k_prep, the synchronous list sizing, "
                                        "k_prep again and the render (device planes, synchronised)"},

@@ -155,9 +155,24 @@ int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16]);
  * Diagnostics: [0] binned frames rendered with a tile plan (tiles that had no
  * survivor in an earlier frame of the same geometry store their misses without
  * reading the region's list), [1] tile plans taken.
- * XRT_TILE_PLAN=0 in the environment at xrt_create turns the plan off.
+ * The plan is OFF by default (it reuses an earlier frame's cull results, so
+ * it only helps a loop of identical frames); XRT_TILE_PLAN=1 in the
+ * environment at xrt_create, or xrt_debug_set_tile_plan, turns it on.
  */
 int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2]);
+
+/* Turns the tile plan on (1) or off (0) for later frames. */
+int xrt_debug_set_tile_plan(xrt_context* ctx, int on);
+
+/*
+ * Diagnostics: k_prep's per-wave timestamps.  enable 1 / 0 turns the records
+ * on / off for later launches (-1 leaves it); *n_waves = the waves of the last
+ * recorded launch; with dst, waits for the context's work and copies up to
+ * `capacity` records of 4 u32 (s_memrealtime, 100 MHz, low 32 bits: the
+ * wave's start, after its records and footprints, after its cell tests, its
+ * end).
+ */
+int xrt_debug_prep_times(xrt_context* ctx, int enable, uint32_t* dst, uint64_t capacity, uint64_t* n_waves);
 
 /*
  * Diagnostics: the phases of the last xrt_destroy, ms: [0] waiting for the
@@ -173,6 +188,22 @@ int xrt_debug_destroy_ms(double ms[4]);
  * hit mask disagreed with its sender's plan (waits for the last gather).
  */
 int xrt_multi_transit_stats(xrt_multi* m, uint64_t out[4]);
+
+/*
+ * Diagnostics of a multi context's balanced split (xrt_multi_set_split): [0]
+ * balanced plans made (each from the strips' own records of an earlier
+ * frame -- no extra render), [1] frames split equally because no such model
+ * existed yet (the first frame), [2] link probes run (at most one per gather
+ * path), [3] strip models collected (one per new camera).
+ */
+int xrt_multi_plan_stats(xrt_multi* m, uint64_t out[4]);
+
+/*
+ * Test hook: the expected hit count of the first tile of the first sender's
+ * hit plan plus one, so the next hit frame's receive disagrees with its plan
+ * (the mismatch path: the frame's call fails, the plans are made again).
+ */
+int xrt_multi_debug_corrupt_hit_plan(xrt_multi* m);
 
 #ifdef __cplusplus
 }

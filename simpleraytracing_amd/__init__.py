@@ -254,6 +254,22 @@ class Context:
         self._check(self._lib.xrt_debug_tile_plan(self._ctx, c), "xrt_debug_tile_plan")
         return {"frames": int(c[0]), "plans": int(c[1])}
 
+    def prep_times(self, enable=None) -> np.ndarray:
+        """k_prep's per-wave timestamps of the last recorded launch (xrt_debug_prep_times):
+        (n, 4) u32 start / after footprints / after cell tests / end; enable turns recording on / off."""
+        n = ctypes.c_uint64()
+        en = -1 if enable is None else int(bool(enable))
+        self._check(self._lib.xrt_debug_prep_times(self._ctx, en, None, 0, ctypes.byref(n)), "xrt_debug_prep_times")
+        out = np.zeros((n.value, 4), np.uint32)
+        if n.value and enable is None:
+            self._check(self._lib.xrt_debug_prep_times(self._ctx, -1, out.ctypes.data, n.value, ctypes.byref(n)),
+                        "xrt_debug_prep_times")
+        return out
+
+    def set_tile_plan(self, on: bool):
+        """The tile plan on / off for later frames (off by default: xrt_debug_set_tile_plan)."""
+        self._check(self._lib.xrt_debug_set_tile_plan(self._ctx, 1 if on else 0), "xrt_debug_set_tile_plan")
+
     def pipeline_counters(self) -> dict:
         """Frames rendered from a preparation made ahead, preparations dropped, renders
         launched with no wait, renders launched after a host wait (xrt_debug_pipeline_counters)."""
@@ -520,6 +536,16 @@ class MultiContext:
         self._check(self._lib.xrt_multi_transit_stats(self._m, out), "xrt_multi_transit_stats")
         return {"frames_hits": int(out[0]), "frames_packed": int(out[1]), "last_bytes": int(out[2]),
                 "bad": int(out[3])}
+
+    def plan_stats(self):
+        """{plans, equal_no_model, link_probes, models} (xrt_multi_plan_stats)."""
+        out = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.xrt_multi_plan_stats(self._m, out), "xrt_multi_plan_stats")
+        return dict(zip(("plans", "equal_no_model", "link_probes", "models"), (int(v) for v in out)))
+
+    def corrupt_hit_plan(self):
+        """Test hook: the next hit frame's receive disagrees with its plan (xrt_multi_debug_corrupt_hit_plan)."""
+        self._check(self._lib.xrt_multi_debug_corrupt_hit_plan(self._m), "xrt_multi_debug_corrupt_hit_plan")
 
     def plan(self, cam: Camera):
         """The strips of cam's frame: ([(begin, end) per device], {link, span_us, step_us})."""

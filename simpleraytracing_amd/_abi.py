@@ -152,6 +152,9 @@ XRT_SYMBOLS = {
     "xrt_debug_host_call_ms": (ctypes.c_int, [_CtxP, _dp]),
     "xrt_debug_destroy_ms": (ctypes.c_int, [_dp]),
     "xrt_debug_tile_plan": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
+    "xrt_debug_set_tile_plan": (ctypes.c_int, [_CtxP, ctypes.c_int]),
+    "xrt_debug_prep_times": (ctypes.c_int, [_CtxP, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),
     "xrt_debug_wave_times": (ctypes.c_int, [_CtxP, _u32, ctypes.POINTER(_u32), _u64, ctypes.POINTER(_u64)]),
     "xrt_set_miss_code": (ctypes.c_int, [_CtxP, _u32]),
@@ -183,6 +186,8 @@ XRT_SYMBOLS = {
     "xrt_multi_set_split": (ctypes.c_int, [_MultiP, ctypes.c_int, ctypes.c_double]),
     "xrt_multi_set_transit": (ctypes.c_int, [_MultiP, ctypes.c_int]),
     "xrt_multi_transit_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(_u64)]),
+    "xrt_multi_plan_stats": (ctypes.c_int, [_MultiP, ctypes.POINTER(_u64)]),
+    "xrt_multi_debug_corrupt_hit_plan": (ctypes.c_int, [_MultiP]),
     "xrt_multi_plan": (ctypes.c_int, [_MultiP, ctypes.POINTER(Camera), ctypes.POINTER(_u32), _dp]),
     "xrt_balanced_bounds": (ctypes.c_int, [_dp, _dp, _u32, _u32, ctypes.c_double, _u32, _u32, ctypes.c_double,
                                            ctypes.POINTER(_u32), _dp]),

@@ -126,6 +126,10 @@ __device__ __forceinline__ size_t hit_element(const Outputs& out, uint32_t index
 // The hit layout's per-tile stores (kLayoutHits): the mask by lane 0, a hit
 // lane's L value at its rank among the tile's hits.  `hit`: the lane's ray hit
 // mesh 0 at least once; `e`: hit_element's.  Every lane of the wave calls it.
+// Values past the plan's count for the tile (hit_off[i + 1] - hit_off[i]; the
+// plan has tiles + 1 offsets) are not stored: a tile can never write into the
+// next tile's values.  Its mask still says how many hits it had, so the
+// receiver (k_unpack_hits) flags the disagreement.
 __device__ __forceinline__ void store_hit_tile(const Outputs& out, size_t e, bool hit, float lval)
 {
     const unsigned long long m = __ballot(hit);
@@ -133,8 +137,10 @@ __device__ __forceinline__ void store_hit_tile(const Outputs& out, size_t e, boo
     uint32_t* msg = reinterpret_cast<uint32_t*>(out.lbuffer);
     if (lane == 0u) reinterpret_cast<uint2*>(msg)[(uint32_t)e] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
     if (hit) {
+        const uint32_t first = (uint32_t)(e >> 32);
+        const uint32_t planned = as_const_u32(out.hit_off)[(uint32_t)e + 1u] - first;
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        out.lbuffer[2u * (size_t)out.hit_tiles + (uint32_t)(e >> 32) + rank] = lval;
+        if (rank < planned) out.lbuffer[2u * (size_t)out.hit_tiles + first + rank] = lval;
     }
 }
 
@@ -1594,8 +1600,19 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                                               float4* __restrict__ culls, BinBuffers bins,
                                               BinState* __restrict__ bs,
                                               RenderParams* __restrict__ frame_out,
-                                              float* __restrict__ offsets_out)
+                                              float* __restrict__ offsets_out,
+                                              uint4* __restrict__ prep_times)
 {
+    // Diagnostics (xrt_debug_prep_times; null otherwise): per wave its
+    // s_memrealtime at the start, after the records and footprints, after the
+    // cell tests (binning phase 1) and at the end.
+    const uint32_t t_start = prep_times ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    uint32_t t_fp = 0u, t_cells = 0u;
+    auto stamp_end = [&]() {
+        if (prep_times && (threadIdx.x & 63u) == 0u)
+            prep_times[blockIdx.x * kPrepWaves + (threadIdx.x >> 6)] =
+                make_uint4(t_start, t_fp, t_cells, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    };
     // The preparation shares the CUs with earlier frames' renders (prep
     // stream) at the default wave priority: frames are prepared ahead of their
     // renders, and a raised priority only took issue slots from the render
@@ -1650,7 +1667,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             fp.e0.w = __uint_as_float(tri);          // the region entries carry the id (make_entry's layout)
         }
     }
-    if (!bins.counts) return;                      // kernel-uniform
+    if (prep_times) t_fp = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (!bins.counts) {                            // kernel-uniform
+        stamp_end();
+        return;
+    }
     if (bins.clear) {                              // the other half, for the set's next frame
         if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
         if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
@@ -1996,6 +2017,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (prep_times) t_cells = (uint32_t)__builtin_amdgcn_s_memrealtime();
     commit();                                      // (2)
     // A region count past the list capacity: the render of that region falls
     // back to the whole mesh, and the host grows the lists for the next frame
@@ -2006,6 +2028,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
         atomicOr(&bs->overflow, 1u);
         if (bins.plan_miss) bins.plan_miss[1] = 1u;  // the host re-sizes for the next frame
     }
+    stamp_end();
 }
 
 // ---------------------------------------------------------------------------
@@ -2452,6 +2475,50 @@ __global__ __launch_bounds__(256) void k_tile_plan(const BlockStats* __restrict_
     for (uint32_t t = 0; t < kWavesPerRegion; ++t)
         live |= (recs[(size_t)s * kWavesPerRegion + t].tile_tests != 0u ? 1u : 0u) << t;
     desc[s].live = live;
+}
+
+// ---------------------------------------------------------------------------
+// k_band_model: the balanced split's model from a binned strip render's own
+// records (xrt_render_rows_multi, DESIGN.md "Multi-GPU") -- per 32-row band of
+// the strip (its region row, SlotDesc::xy >> 16) the wave time of its regions'
+// waves (timing records, 100 MHz ticks), the hit rays and the number of its
+// tile regions (slots below tile_slots: the regions that travel); span[0] /
+// span[1] = the first wave start / the last wave end.  One thread per slot (its
+// 16 records); `bands` and `span` are cleared by the caller (span[0] to ~0).
+// ---------------------------------------------------------------------------
+struct BandModel {
+    uint32_t ticks, hits, tiles, pad;
+};
+__global__ __launch_bounds__(256) void k_band_model(const BlockStats* __restrict__ recs,
+                                                   const uint2* __restrict__ times,
+                                                   const SlotDesc* __restrict__ desc, uint32_t n_slots,
+                                                   uint32_t tile_slots, BandModel* __restrict__ bands,
+                                                   uint32_t* __restrict__ span)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    if (s < n_slots) {
+        uint32_t ticks = 0, hits = 0;
+        for (uint32_t t = 0; t < kWavesPerRegion; ++t) {
+            const uint2 tt = times[(size_t)s * kWavesPerRegion + t];
+            ticks += tt.y - tt.x;
+            lo = min(lo, tt.x);
+            hi = max(hi, tt.y);
+            hits += recs[(size_t)s * kWavesPerRegion + t].hit_rays;
+        }
+        BandModel* b = bands + (desc[s].xy >> 16);
+        atomicAdd(&b->ticks, ticks);
+        if (s < tile_slots) {
+            atomicAdd(&b->hits, hits);
+            atomicAdd(&b->tiles, 1u);
+        }
+    }
+    lo = ~wave_reduce_u32<true>(~lo);
+    hi = wave_reduce_u32<true>(hi);
+    if ((threadIdx.x & 63u) == 0u && hi != 0u) {
+        atomicMin(&span[0], lo);
+        atomicMax(&span[1], hi);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -321,8 +321,14 @@ struct xrt_context {
     bool plan_valid = false;
     // Tile plan (SlotDesc::live): 0 = the compact layout's tiles all live (as
     // uploaded), 1 = k_tile_plan ran after a render of the current geometry
-    // (bin_key) with its fill plan.  XRT_TILE_PLAN=0 turns it off.
-    bool tile_plan_enabled = true;
+    // (bin_key) with its fill plan.  Off by default: it reuses an earlier
+    // frame's cull results, so it helps only a loop of identical frames
+    // (XRT_TILE_PLAN=1 or xrt_debug_set_tile_plan turn it on).
+    bool tile_plan_enabled = false;
+    // xrt_debug_prep_times: k_prep's per-wave timestamps of the last launch
+    bool prep_times_on = false;
+    uint4* d_prep_times = nullptr;
+    size_t prep_times_cap = 0, prep_times_n = 0;
     int tile_plan_state = 0;
     uint64_t hp_tile_plan_frames = 0, hp_tile_plans = 0;
     uint32_t last_fill_regions = 0;    // regions the last enqueued frame filled (diagnostics)
@@ -749,11 +755,18 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
     const uint64_t per_block = (uint64_t)kPrepWaves * p.prep_tris;
     const uint64_t blocks = std::max<uint64_t>((T + per_block - 1) / per_block,
                                                (threads + kPrepThreads - 1) / kPrepThreads);
+    uint4* ptimes = nullptr;                       // xrt_debug_prep_times
+    if (ctx->prep_times_on) {
+        int rc = ensure(ctx, ctx->d_prep_times, ctx->prep_times_cap, (size_t)blocks * kPrepWaves);
+        if (rc) return rc;
+        ptimes = ctx->d_prep_times;
+        ctx->prep_times_n = (size_t)blocks * kPrepWaves;
+    }
     const auto t_launch = HostClock::now();
     hipExtLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(kPrepThreads),
                           ctx->prep_lds, stream, nullptr, done, 0u,
                           ctx->d_tris, (uint32_t)T, p, cp, fs.recs, culled ? fs.cull : nullptr, bins, bin_ctl,
-                          fs.frame, fs.offsets);
+                          fs.frame, fs.offsets, ptimes);
     XRT_HIP(ctx, hipGetLastError());
     if (bins.counts) ctx->prep_reads_layout = true;
     ctx->acc_ms[4] += std::chrono::duration<double, std::milli>(HostClock::now() - t_launch).count();
@@ -1047,7 +1060,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.tile_slots = n_regions;
         if (compact) use_compact(ctx, n_regions, bins, fill_ok && !reuse);
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
-        bins.tile_plan = compact && fill_ok && !reuse && !sizing && ctx->plan_valid && ctx->tile_plan_state == 1 ? 1u : 0u;
+        bins.tile_plan = compact && fill_ok && !reuse && !sizing && ctx->plan_valid && ctx->tile_plan_enabled &&
+                         ctx->tile_plan_state == 1 ? 1u : 0u;
         if (sizing) prof_mark(ctx, "fixed layout upload");
         // the fill plan's test hook (every region planned empty) is checked every frame
         arm_plan_check(fs, n_regions, bins, reuse, ctx->fill_plan == 2);
@@ -1345,6 +1359,11 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
             hipLaunchKernelGGL(k_tile_plan, dim3((n + 255) / 256), dim3(256), 0, stream, fs.block_stats,
                                ctx->compact_layout.d_desc, bins.split_slots, bins.tile_slots);
             XRT_HIP(ctx, hipGetLastError());
+            // the set's completion event covers k_tile_plan too: the set's
+            // statistics records and the layout's descriptions are not
+            // rewritten while it reads / writes them
+            XRT_HIP(ctx, hipEventRecord(fs.done, stream));
+            fs.done_ev = fs.done;
             ctx->tile_plan_state = 1;
             ++ctx->hp_tile_plans;
         }
@@ -1644,6 +1663,7 @@ void xrt_destroy(xrt_context* ctx)
     (void)hipFree(ctx->d_stats_done);
     (void)hipFree(ctx->d_stats_out);
     (void)hipFree(ctx->d_hit_off);
+    (void)hipFree(ctx->d_prep_times);
     for (auto& c : ctx->tchunks) (void)hipFree(c.p);
     lap(1);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
@@ -2068,6 +2088,28 @@ int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16])
     return XRT_OK;
 }
 
+int xrt_debug_prep_times(xrt_context* ctx, int enable, uint32_t* dst, uint64_t capacity, uint64_t* n_waves)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (enable >= 0) ctx->prep_times_on = enable != 0;
+    if (n_waves) *n_waves = ctx->prep_times_n;
+    if (!dst || !ctx->d_prep_times || !ctx->prep_times_n) return XRT_OK;
+    XRT_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = sync_context(ctx);
+    if (rc) return rc;
+    const size_t n = std::min<size_t>(capacity, ctx->prep_times_n);
+    XRT_HIP(ctx, hipMemcpy(dst, ctx->d_prep_times, n * sizeof(uint4), hipMemcpyDeviceToHost));
+    return XRT_OK;
+}
+
+int xrt_debug_set_tile_plan(xrt_context* ctx, int on)
+{
+    if (!ctx) return XRT_ERR_ARGUMENT;
+    if (ctx->tile_plan_enabled != (on != 0)) ++ctx->state_gen;   // frames prepared ahead are dropped
+    ctx->tile_plan_enabled = on != 0;
+    return XRT_OK;
+}
+
 int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2])
 {
     if (!ctx || !counters) return XRT_ERR_ARGUMENT;
@@ -2467,7 +2509,7 @@ int xrt_probe_prep(xrt_context* ctx, const xrt_camera* camera, float* records, f
     BinBuffers nobins = {};
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((T + kPrepWaves * p.prep_tris - 1) / (kPrepWaves * p.prep_tris))),
                        dim3(kPrepThreads), 0, 0, ctx->d_tris,
-                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr);
+                       (uint32_t)T, p, cp, fs.recs, fs.cull, nobins, nullptr, nullptr, nullptr, nullptr);
     XRT_HIP(ctx, hipGetLastError());
     if (records)
         XRT_HIP(ctx, hipMemcpy(records, fs.recs, T * sizeof(TriRec), hipMemcpyDeviceToHost));

@@ -1037,13 +1037,15 @@ def test_multi_hit_transit(dragon, gather):
 def test_multi_balanced_split_rccl_one_rank(dragon, W, H, n, link):
     """xrt_render_rows_multi with the balanced split (the default): one GPU listed
     n times, gathered through a one-rank RCCL communicator -- 4096^2 in 8
-    strips is BASELINE configs[3]'s split, planned by the product path itself
-    (device 0's full-frame model, the link measured or given).  The strips are
-    band-aligned, cover the frame, device 0's run may sit anywhere; every frame
-    is bit-equal to one device's frame; the equal split (the reference's rule)
-    still gives the reference's strips and the same frame."""
+    strips is BASELINE configs[3]'s split.  The first frame splits equally
+    (the reference's rule; no model yet, no extra render, no link probe) and
+    models the split from its strips' own records; the next frame plans the
+    balanced split from them.  The strips are band-aligned, cover the frame,
+    device 0's run may sit anywhere; every frame is bit-equal to one device's
+    frame; the equal split still gives the reference's strips."""
     from simpleraytracing_amd.strips import strip_bounds
     cam = xrt.camera_for_mesh(dragon, W, H)
+    equal = [strip_bounds(H, n, g) for g in range(n)]
     with xrt.Context(0) as one:
         one.set_kernel(xrt.XRT_KERNEL_BINNED)
         one.upload_mesh(dragon)
@@ -1054,6 +1056,13 @@ def test_multi_balanced_split_rccl_one_rank(dragon, W, H, n, link):
         m.set_gather(xrt.XRT_GATHER_RCCL)
         m.set_split(xrt.XRT_SPLIT_BALANCED, link)
         bounds, info = m.plan(cam)
+        assert bounds == equal and info["predicted_step_us"] == 0.0       # no model before a frame
+        got = m.render(cam)
+        for x, y in zip(got[:3], ref[:3]):
+            assert np.array_equal(bits(x), bits(y))
+        st = m.plan_stats()
+        assert st["plans"] == 0 and st["link_probes"] == 0 and st["models"] == 0 and st["equal_no_model"] >= 1, st
+        bounds, info = m.plan(cam)
         assert len(bounds) == n and all(e > b for b, e in bounds)
         spans = sorted(bounds)
         assert spans[0][0] == 0 and spans[-1][1] == H and all(b % 32 == 0 for b, _ in spans)
@@ -1061,17 +1070,81 @@ def test_multi_balanced_split_rccl_one_rank(dragon, W, H, n, link):
         assert [b for b, _ in bounds[1:]] == sorted(b for b, _ in bounds[1:])     # senders in frame order
         assert info["frame_span_us"] > 0 and info["predicted_step_us"] > 0
         assert info["link_bytes_per_us"] == link if link else info["link_bytes_per_us"] > 0
-        assert m.plan(cam)[0] == bounds                        # planned once per geometry
+        assert m.plan(cam)[0] == bounds                        # planned once per camera
         for _ in range(3):                                     # the strip buffers rotate
             got = m.render(cam)
             for x, y in zip(got[:3], ref[:3]):
                 assert np.array_equal(bits(x), bits(y))
             assert got[3].hit_rays == ref[3].hit_rays and got[3].odd_rays == ref[3].odd_rays
+        st = m.plan_stats()
+        assert st["plans"] == 1 and st["models"] == 1 and st["link_probes"] == (0 if link else 1), st
         m.set_split(xrt.XRT_SPLIT_EQUAL)
-        assert m.plan(cam)[0] == [strip_bounds(H, n, g) for g in range(n)]
+        assert m.plan(cam)[0] == equal
         got = m.render(cam)
         for x, y in zip(got[:3], ref[:3]):
             assert np.array_equal(bits(x), bits(y))
+
+
+def test_multi_orbit_balanced_rccl_one_rank(dragon):
+    """An 8-frame orbit (1 degree a frame) through xrt_render_rows_multi on one
+    device listed 8 times with RCCL, balanced split: the first frame splits
+    equally, every later frame plans from an earlier frame's strip records
+    (no whole-frame model render: no extra renders at all), the link is probed
+    once, and every frame equals one device's render of its camera."""
+    from simpleraytracing_amd.scenes import orbit_camera
+    W = H = 1024
+    cam0 = xrt.camera_for_mesh(dragon, W, H)
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    cams = [orbit_camera(cam0, centre, k * 1.0) for k in range(8)]
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        refs = [one.render_rows(c) for c in cams]
+    with xrt.MultiContext([0] * 8) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        m.set_gather(xrt.XRT_GATHER_RCCL)
+        for k, c in enumerate(cams):
+            got = m.render(c)
+            for x, y in zip(got[:3], refs[k][:3]):
+                assert np.array_equal(bits(x), bits(y)), k
+        st = m.plan_stats()
+    # (frame k's model is taken by frame k + 1's plan: the last one is still pending)
+    assert st["equal_no_model"] == 1 and st["plans"] == 7 and st["link_probes"] == 1 and st["models"] == 7, st
+
+
+def test_multi_hit_mismatch_reported_and_replanned(dragon):
+    """A received hit mask that disagrees with its sender's plan (test hook: the
+    plan's expected count of one tile off by one) fails that frame's call with
+    XRT_ERR_DEVICE and drops the hit plans; the next frames travel packed,
+    then plan again, each bit-equal to one device's frame."""
+    W, H, n = 1024, 1024, 4
+    cam = xrt.camera_for_mesh(dragon, W, H)
+    with xrt.Context(0) as one:
+        one.set_kernel(xrt.XRT_KERNEL_BINNED)
+        one.upload_mesh(dragon)
+        ref = one.render_rows(cam)
+    with xrt.MultiContext([0] * n) as m:
+        m.set_kernel(xrt.XRT_KERNEL_BINNED)
+        m.upload_mesh(dragon)
+        m.set_gather(xrt.XRT_GATHER_RCCL)
+        m.set_split(xrt.XRT_SPLIT_EQUAL)
+        for _ in range(3):                                     # packed, then hits
+            m.render(cam)
+        assert m.transit_stats()["frames_hits"] == 2
+        m.corrupt_hit_plan()
+        with pytest.raises(xrt.XrtError) as e:
+            m.render(cam)
+        assert e.value.code == 2 and "hit mask" in str(e.value)
+        before = m.transit_stats()
+        for _ in range(3):                                     # packed (plans dropped), then hits again
+            got = m.render(cam)
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y))
+        st = m.transit_stats()
+        assert st["frames_packed"] == before["frames_packed"] + 1 and st["frames_hits"] == before["frames_hits"] + 2
+        assert st["bad"] == 0, st
 
 
 def test_fresh_context_after_two_stream_loop(dragon):
@@ -1134,7 +1207,7 @@ def test_host_buffer_d2h_pieces_exact(dragon):
 @pytest.mark.parametrize("W,H,r0,r1", [(2048, 2048, 0, 2048), (1000, 777, 0, 777), (4096, 4096, 1024, 2080),
                                        (333, 517, 100, 400)])
 def test_tile_plan_frames_exact(dragon, W, H, r0, r1):
-    """The tile plan (SlotDesc::live from one render's records): later frames of
+    """The tile plan (opt-in; SlotDesc::live from one render's records): later frames of
     the same geometry store the misses of the tiles that had no survivor
     without reading their region's list -- every such frame bit-equal to a
     brute-force render; a camera change re-plans, and the old plan is not used."""
@@ -1146,6 +1219,7 @@ def test_tile_plan_frames_exact(dragon, W, H, r0, r1):
     with xrt.Context(0) as c:
         c.set_kernel(xrt.XRT_KERNEL_BINNED)
         c.upload_mesh(dragon)
+        c.set_tile_plan(True)                  # opt-in (off by default)
         for k in range(8):
             ci = (k // 4) % 2
             got = c.render_rows(cams[ci], r0, r1)
