@@ -512,7 +512,8 @@ def end_to_end_isolated(args, W, H, device_index):
     cmd = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--e2e-device", str(device_index),
            "--size", str(W), str(H), "--mesh", args.mesh, "--tile-mesh", str(args.tile_mesh),
            "--kernel", args.kernel]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, XRT_SEGV_TRACE="1"))   # a fatal signal names its library
     if r.returncode != 0:
         raise RuntimeError(f"end-to-end child failed ({r.returncode}): {r.stderr[-2000:]}")
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -532,6 +533,16 @@ def e2e_only(args) -> int:
     W, H = args.size
     print(json.dumps(end_to_end(args, W, H, args.e2e_device, kernel)), flush=True)
     return 0
+
+
+def child_exit(code: int) -> None:
+    """A measurement child's exit once its JSON line is out: its contexts are
+    closed, so nothing of the path is left to tear down -- os._exit skips the
+    interpreter's and the shared libraries' finalizers (the HIP runtime's, a
+    profiler's), whose order no caller controls."""
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
 
 
 def capi_multi_only(args) -> int:
@@ -617,7 +628,8 @@ def capi_multi_isolated(args, W, H, devices, timeout_s=100):
            "--steps", str(args.steps), "--warmup", str(args.warmup), "--capi-split", args.capi_split,
            "--transit", args.transit]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s,
+                           env=dict(os.environ, XRT_SEGV_TRACE="1"))
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {timeout_s} s", "devices": devices}
     if r.returncode != 0:
@@ -628,9 +640,9 @@ def capi_multi_isolated(args, W, H, devices, timeout_s=100):
 def main():
     args = parse()
     if args.e2e_only:
-        return e2e_only(args)
+        child_exit(e2e_only(args))
     if args.capi_only:
-        return capi_multi_only(args)
+        child_exit(capi_multi_only(args))
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -4,6 +4,11 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -498,7 +503,12 @@ void prof_mark(xrt_context* ctx, const char* what)
     ctx->prof_t = HostClock::now();
 }
 
-static std::string g_create_error;
+// No static object of libxrt has a destructor: process exit runs the shared
+// libraries' finalizers (__cxa_finalize) in an order libxrt does not control,
+// the HIP runtime's among them, and contexts a caller leaks (RayTracer.cpp's
+// per-device slots) are reclaimed by the process's end, not torn down.  The
+// error strings of a failed create are heap objects that are never freed.
+static std::string& g_create_error = *new std::string();
 // xrt_destroy's phases, ms (xrt_debug_destroy_ms): [0] waiting for the
 // context's work, [1] device frees, [2] pinned host frees, [3] streams and events
 static double g_destroy_ms[4] = {};
@@ -1543,8 +1553,50 @@ int xrt_device_count(void)
     return n;
 }
 
+// XRT_SEGV_TRACE=1 (diagnostics): a fatal signal prints every frame of the
+// faulting thread with the shared library it lies in (dladdr), then the
+// signal is raised again with its default action.
+namespace {
+void fatal_signal_trace(int sig, siginfo_t* si, void*)
+{
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    char line[512];
+    int k = std::snprintf(line, sizeof line, "xrt: signal %d (fault address %p), pid %d, %d frames:\n", sig,
+                          si ? si->si_addr : nullptr, (int)getpid(), n);
+    (void)!write(2, line, (size_t)std::max(k, 0));
+    for (int i = 0; i < n; ++i) {
+        Dl_info d = {};
+        if (dladdr(frames[i], &d) && d.dli_fname)
+            k = std::snprintf(line, sizeof line, "  #%-2d %p %s + %#lx (%s)\n", i, frames[i], d.dli_fname,
+                              (unsigned long)((uintptr_t)frames[i] - (uintptr_t)d.dli_fbase),
+                              d.dli_sname ? d.dli_sname : "?");
+        else
+            k = std::snprintf(line, sizeof line, "  #%-2d %p (no library)\n", i, frames[i]);
+        (void)!write(2, line, (size_t)std::max(k, 0));
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+void install_fatal_signal_trace()
+{
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* v = std::getenv("XRT_SEGV_TRACE");
+        if (!v || std::atoi(v) == 0) return;
+        struct sigaction sa = {};
+        sa.sa_sigaction = fatal_signal_trace;
+        sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+        sigemptyset(&sa.sa_mask);
+        for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGILL, SIGFPE}) sigaction(sig, &sa, nullptr);
+    });
+}
+}  // namespace
+
 int xrt_create(int device, xrt_context** out)
 {
+    install_fatal_signal_trace();
     if (!out) return fail(nullptr, XRT_ERR_ARGUMENT, "out is NULL");
     *out = nullptr;
     int n = 0;

@@ -259,3 +259,18 @@ def test_cli_signed_two_gpus_rehearsal(tmp_path, dragon):
                            capture_output=True, text=True, cwd=tmp_path, timeout=300, env=env)
         assert r.returncode == 0, r.stderr
     assert (tmp_path / "out" / "one.txt").read_bytes() == (tmp_path / "out" / "two.txt").read_bytes()
+
+
+def test_exit_with_live_contexts():
+    """A process that leaves a context and a multi context alive (renders
+    done, frames streamed through the pinned ring and copy threads, nothing
+    destroyed) exits with status 0: libxrt holds no static object with a
+    destructor, so the finalizers the process's exit runs in an order libxrt
+    does not control never tear anything of it down (round 5 saw one SIGSEGV in
+    __cxa_finalize at a child's exit).  XRT_SEGV_TRACE=1 names the library of a
+    fatal signal, should one come."""
+    env = dict(os.environ, XRT_SEGV_TRACE="1")
+    r = subprocess.run([os.sys.executable, os.path.join(ROOT, "tests", "_exit_job.py")], capture_output=True,
+                       text=True, timeout=110, env=env)
+    assert r.returncode == 0, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
+    assert "exit job: ok" in r.stdout
