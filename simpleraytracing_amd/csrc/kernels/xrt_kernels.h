@@ -1580,6 +1580,9 @@ __device__ __forceinline__ bool bin_rect(float4 bb, float reach, const RenderPar
 #ifndef XRT_PREP_PRIO
 #define XRT_PREP_PRIO 0   // k_prep's wave priority (s_setprio; 0: the render's)
 #endif
+#ifndef XRT_PREP_LATE_STORES
+#define XRT_PREP_LATE_STORES 1   // k_prep's global stores after its binning (1) or before it (0)
+#endif
 constexpr uint32_t kPrepThreads = XRT_PREP_THREADS;
 constexpr uint32_t kPrepWaves = kPrepThreads / 64u;
 #ifndef XRT_PREP_TRIS
@@ -1627,11 +1630,9 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     const uint32_t tri_lane = threadIdx.x & 63u;
     const uint32_t tri = (blockIdx.x * kPrepWaves + (threadIdx.x >> 6)) * p.prep_tris + tri_lane;
     const bool valid = tri_lane < p.prep_tris && tri < T;
+    // (the one wave that writes the frame's parameters does so at once: kept to
+    // the end they would live in scratch)
     if (i == 0 && frame_out) *frame_out = p;       // the render's make_ray reads it (Outputs::frame)
-    if (offsets_out) {                             // v_off of every row, then u_off of every column
-        if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
-        else if (i - p.height < p.width) offsets_out[i] = pixel_offset(p.spacing, i - p.height, p.width);
-    }
     Footprint fp;
     TriRec r = {};
     if (valid) {
@@ -1657,24 +1658,46 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             r.pad1 = ny / len;
             r.pad2 = nz / len;
         }
-        recs[tri] = r;
         if (culls) {
             fp = compute_footprint(r, p, cp);
-            culls[tri] = fp.bbox;
-            culls[(size_t)T + tri] = fp.e0;
-            culls[2 * (size_t)T + tri] = fp.e1;
-            culls[3 * (size_t)T + tri] = fp.e2;
             fp.e0.w = __uint_as_float(tri);          // the region entries carry the id (make_entry's layout)
         }
     }
+    // The wave's global stores -- records, cull planes, the frame's pixel
+    // offsets, the other counter half's clears -- are issued at its
+    // END, after the binning: on gfx9 a store holds the vector-memory counter
+    // until it is acknowledged, and the binning's first wait for a load (its
+    // commit's slot loads, a loop's conservative wait) would otherwise wait
+    // for every one of them (2048^2: ~1-2 us per wave beside the render).
+    auto store_outputs = [&]() __attribute__((always_inline)) {
+        if (offsets_out) {                         // v_off of every row, then u_off of every column
+            if (i < p.height) offsets_out[i] = pixel_offset(p.spacing, i, p.height);
+            else if (i - p.height < p.width) offsets_out[i] = pixel_offset(p.spacing, i - p.height, p.width);
+        }
+        if (valid) {
+            recs[tri] = r;
+            if (culls) {
+                culls[tri] = fp.bbox;
+                culls[(size_t)T + tri] = make_float4(fp.e0.x, fp.e0.y, fp.e0.z, 0.0f);
+                culls[2 * (size_t)T + tri] = fp.e1;
+                culls[3 * (size_t)T + tri] = fp.e2;
+            }
+        }
+        if (bins.counts && bins.clear) {           // the other half, for the set's next frame
+            if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
+            if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
+        }
+    };
+#if !XRT_PREP_LATE_STORES
+    store_outputs();                               // (A/B: the stores before the binning)
+#endif
     if (prep_times) t_fp = (uint32_t)__builtin_amdgcn_s_memrealtime();
     if (!bins.counts) {                            // kernel-uniform
+#if XRT_PREP_LATE_STORES
+        store_outputs();
+#endif
         stamp_end();
         return;
-    }
-    if (bins.clear) {                              // the other half, for the set's next frame
-        if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
-        if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
     }
 
     // Binning, per wave, in two phases.  (1) Test: every cell of the wave's
@@ -2028,6 +2051,9 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
         atomicOr(&bs->overflow, 1u);
         if (bins.plan_miss) bins.plan_miss[1] = 1u;  // the host re-sizes for the next frame
     }
+#if XRT_PREP_LATE_STORES
+    store_outputs();
+#endif
     stamp_end();
 }
 

@@ -1683,3 +1683,51 @@ def test_cli_multi_gpu_golden_text(tmp_path):
     assert r.returncode == 0, r.stderr
     got = (tmp_path / "out" / "d.txt").read_bytes()
     assert got == open(os.path.join(GOLDEN, "dragon-128x128-serial.txt"), "rb").read()
+
+
+FIXTURES = ["planes_dragon_128", "planes_dragon_256", "rows_dragon_1024", "rows_dragon_2048", "rows_dragon_4096",
+            "rows_dragon_8192", "rows_tiled7_8192"]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture_rows_device(dragon, name):
+    """The device against the committed fixtures the reference's own classes
+    rendered (tools/gen_golden.py): every 8-GPU strip boundary row
+    (k*H/8 - 1, k*H/8), row 0, H/2 and H - 1 of dragon.ply at 1024^2..8192^2 and
+    of the 1.12 M-triangle tiled dragon at 8192^2, and whole 128^2 / 256^2
+    frames -- from a whole-frame BINNED render (device planes, the rows
+    gathered on the device) and from each row as a one-row strip, image,
+    L-buffer and u8 bit for bit, hit rays per row.  Nothing is recomputed on
+    this box: its libm is on neither side."""
+    import hashlib
+
+    import torch
+    from simpleraytracing_amd.scenes import tiled_mesh
+    g = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    W, H = int(g["width"]), int(g["height"])
+    tris = tiled_mesh(dragon, 7) if "tiled7" in name else dragon
+    assert hashlib.sha256(np.ascontiguousarray(tris, np.float32).tobytes()).hexdigest() == str(g["mesh_sha256"])
+    cam = xrt.camera_for_mesh(tris, W, H)
+    cam13 = np.array(list(cam.origin) + list(cam.detector) + list(cam.up) + list(cam.right) + [cam.pixel_spacing],
+                     np.float32)
+    assert np.array_equal(bits(cam13), bits(g["camera"]))
+    rows = g["rows"].astype(np.int64)
+    dev = torch.device("cuda", 0)
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(tris)
+        planes = (torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+                  torch.empty(W * H, dtype=torch.uint8, device=dev))
+        c.render_rows_device(cam, 0, H, *(p.data_ptr() for p in planes), 0)
+        torch.cuda.synchronize(dev)
+        idx = torch.from_numpy(rows).to(dev)
+        got = [p.view(H, W).index_select(0, idx).cpu().numpy() for p in planes]
+        assert np.array_equal(bits(got[0]), bits(g["image"])), "image"
+        assert np.array_equal(bits(got[1]), bits(g["lbuffer"])), "lbuffer"
+        assert np.array_equal(got[2], g["u8"]), "u8"
+        del planes
+        for i, r in enumerate(rows[:: max(1, len(rows) // 17)]):       # one-row strips
+            k = int(np.nonzero(rows == r)[0][0])
+            img, lb, u8, st = c.render_rows(cam, int(r), int(r) + 1)
+            assert np.array_equal(bits(img), bits(g["image"][k])) and np.array_equal(bits(lb), bits(g["lbuffer"][k]))
+            assert np.array_equal(u8, g["u8"][k]) and st.hit_rays == int((g["nhits"][k] > 0).sum()), int(r)

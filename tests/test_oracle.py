@@ -212,3 +212,38 @@ def test_scene_bbox_is_getbbox_of_mesh_boxes(REF, dragon):
         his.append(h)
     assert np.array_equal(lo, np.min(los, axis=0)) and np.array_equal(hi, np.max(his, axis=0))
     assert not np.array_equal(oracle.camera_for_scene(meshes, 64, 64), oracle.camera_for_mesh(dragon, 64, 64))
+
+
+# --- fixtures generated from the reference's own classes (tools/gen_golden.py) ---
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+
+
+def test_fixture_kat_intersect():
+    """tests/golden/kat_intersect.npz: the 64 K pairs of tests/kat.py through the
+    reference's own Ray::intersect (generated here from oracle/_ref); the
+    oracle reproduces every hit flag and distance bit for bit."""
+    import hashlib
+    g = _golden("kat_intersect")
+    rays, tris = kat_vectors()
+    assert hashlib.sha256(rays.tobytes() + tris.tobytes()).hexdigest() == str(g["inputs_sha256"])
+    hit, t = oracle.intersect_batch(rays, tris)
+    assert np.array_equal(hit, g["hit"]) and np.array_equal(bits(t), bits(g["t"]))
+
+
+@pytest.mark.parametrize("name", ["planes_dragon_128", "planes_dragon_256", "rows_dragon_1024"])
+def test_fixture_rows_oracle(dragon, name):
+    """The oracle against the committed frames / strip-boundary rows rendered by
+    the reference's own classes (tests/golden/<name>.npz): camera, image,
+    L-buffer bit for bit (u8, hit counts and odd rays were the oracle's at
+    generation and are pinned by the same run)."""
+    g = _golden(name)
+    W, H = int(g["width"]), int(g["height"])
+    cam = oracle.camera_for_mesh(dragon, W, H)
+    assert np.array_equal(bits(cam), bits(g["camera"]))
+    img, lb, u8, nh, odd = oracle.render_row_list(dragon, cam, W, H, g["rows"])
+    assert np.array_equal(bits(img), bits(g["image"].reshape(-1)))
+    assert np.array_equal(bits(lb), bits(g["lbuffer"].reshape(-1)))
+    assert np.array_equal(u8, g["u8"].reshape(-1)) and np.array_equal(nh, g["nhits"].reshape(-1))
+    assert odd == int(g["odd"])
