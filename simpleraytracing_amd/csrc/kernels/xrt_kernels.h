@@ -31,7 +31,7 @@ struct BinState {
     unsigned int max_count;     // largest region count of the frame (list sizing)
     unsigned int global_count;  // triangles in the global list
     unsigned int overflow;      // some region count exceeded the list capacity
-    unsigned int pad;
+    unsigned int cursor;        // a device-sized frame's pool cursor (k_size_lists)
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -2055,6 +2055,44 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     store_outputs();
 #endif
     stamp_end();
+}
+
+// ---------------------------------------------------------------------------
+// k_size_lists: the list sizing of a moving camera's frame on the device
+// (DESIGN.md "Moving camera"), between k_prep's count-only pass and its fill
+// pass on the prep stream -- no host round trip.  Each slot of the launch
+// layout `fixed` (its order and regions) gets room for exactly the pairs the
+// count pass counted, carved from the set's pool by one atomic per wave
+// (BinState::cursor; the lists need not follow the slot order); its counter
+// and the count pass's global-list count are zeroed for the fill pass.  A
+// slot past the pool gets what is left (its overflow makes the render take
+// that region from the whole mesh, exactly, and flags the frame: the host
+// grows the pool for later frames).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ counts, const SlotDesc* __restrict__ fixed,
+                                                   SlotDesc* __restrict__ out, uint32_t n_slots, uint32_t pool,
+                                                   BinState* __restrict__ bs)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = s < n_slots ? counts[(size_t)s * kCounterStride] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
+        if (lane >= off) incl += o;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    uint32_t base0 = 0;
+    if (lane == 0u && total) base0 = atomicAdd(&bs->cursor, total);
+    base0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+    if (s < n_slots) {
+        const uint32_t base = base0 + incl - c;
+        const uint32_t cap = base >= pool ? 0u : min(c, pool - base);
+        out[s] = SlotDesc{min(base, pool), cap, fixed[s].xy, 0xFFFFu};
+        counts[(size_t)s * kCounterStride] = 0u;
+    }
+    if (s == 0u) bs->global_count = 0u;             // the fill pass appends the global list again
 }
 
 // ---------------------------------------------------------------------------

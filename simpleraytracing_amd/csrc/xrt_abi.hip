@@ -174,6 +174,9 @@ struct FrameSet {
 
     // Completion events ride on the kernel dispatches themselves
     // (hipExtLaunchKernel stop events): no separate event packets.
+    SlotDesc* dyn_desc = nullptr;      // a device-sized frame's launch layout (k_size_lists)
+    size_t dyn_desc_cap = 0;
+    bool lazy_flags = false;           // plan_flag armed for a frame launched without reading it
     hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
     hipEvent_t done = nullptr;         // render end (a stop event on the render's dispatch)
     hipEvent_t done_ev = nullptr;      // the event that marks the set's last render complete
@@ -308,6 +311,7 @@ struct xrt_context {
     SlotLayout fixed;
     SlotLayout compact_layout;
     uint64_t slot_pool = 0;            // entries of the compact lists
+    uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
     bool compact = false;              // compact_layout is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     // Fill plan of the current geometry (bin_key): the compact layout's
@@ -981,6 +985,16 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         fs.done_valid = false;
         if (ctx->host_profile) ctx->hp_done += seconds_since(t);
     }
+    if (fs.lazy_flags) {
+        // the set's last frame was device-sized and launched without reading
+        // k_prep's flags; its render is complete: a list past the pool there
+        // (that region rendered from the whole mesh, exactly) grows the pool
+        fs.lazy_flags = false;
+        if (fs.plan_flag && fs.plan_flag[1] != 0u) {
+            ++ctx->hp_overflow;
+            ctx->motion_pool = std::min<uint64_t>(2 * ctx->motion_pool + 65536u, 0xFFFFFFFFull);
+        }
+    }
     if ((rc = ensure(ctx, fs.recs, fs.recs_cap, T))) return rc;
     if (culled && (rc = ensure(ctx, fs.cull, fs.cull_cap, (size_t)T * kCullPlanes))) return rc;
     if ((rc = ensure(ctx, fs.offsets, fs.offsets_cap, (size_t)cam->height + cam->width))) return rc;
@@ -1061,6 +1075,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     if (binned) {
         bins.regions_x = rx;
         bins.regions_y = ry;
+    }
+    if (binned && !reuse) {
         const bool compact = ctx->compact && !ctx->bin_force_cap;
         bool cleared = false;
         const uint64_t entries = compact ? ctx->slot_pool : sizing ? 0u : (uint64_t)n_regions * fixed_cap;
@@ -1074,10 +1090,43 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
                          ctx->tile_plan_state == 1 ? 1u : 0u;
         if (sizing) prof_mark(ctx, "fixed layout upload");
         // the fill plan's test hook (every region planned empty) is checked every frame
-        arm_plan_check(fs, n_regions, bins, reuse, ctx->fill_plan == 2);
+        arm_plan_check(fs, n_regions, bins, false, ctx->fill_plan == 2);
     }
 
     hipEvent_t prep_done = fs.ready;
+    if (reuse) {
+        // A moving camera (DESIGN.md "Moving camera"): its lists sized on the
+        // device, no host round trip -- k_prep counts its pairs per slot of the
+        // region grid's base layout (centre first), k_size_lists carves each
+        // slot's list from the set's pool, k_prep bins into them.  Every region
+        // renders as tiles (no fill plan: the host never sees the counts).
+        // k_prep's flags are read when the set is next used (lazy_flags).
+        ctx->motion_pool = std::max<uint64_t>(ctx->motion_pool, std::max<uint64_t>(2 * ctx->slot_pool, 65536u));
+        bool cleared = false;
+        if ((rc = bin_buffers(ctx, fs, n_regions, ctx->motion_pool, bins, bin_ctl, ps, cleared))) return rc;
+        if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+        if ((rc = ensure(ctx, fs.dyn_desc, fs.dyn_desc_cap, n_regions))) return rc;
+        bins.tile_slots = n_regions;
+        bins.split_slots = 0u;
+        bins.tile_plan = 0u;
+        bins.plan_miss = nullptr;
+        RegionEntry* const list = bins.list;
+        bins.list = nullptr;                           // the count-only pass
+        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, nullptr))) return rc;
+        hipLaunchKernelGGL(k_size_lists, dim3((n_regions + 255) / 256), dim3(256), 0, ps, bins.counts,
+                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, (uint32_t)std::min<uint64_t>(
+                               ctx->motion_pool, 0xFFFFFFFFull), bin_ctl);
+        XRT_HIP(ctx, hipGetLastError());
+        bins.list = list;
+        bins.desc = fs.dyn_desc;
+        bins.clear = nullptr;                          // (the count pass cleared the other half)
+        if (fs.plan_flag) {                            // [1]: a list past the pool, read lazily
+            fs.plan_flag[0] = 0u;
+            fs.plan_flag[1] = 0u;
+            bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
+            fs.lazy_flags = true;
+        }
+    }
     if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     if (sizing) {
         // Size the compact region lists once per frame geometry (mesh, camera,
@@ -1180,7 +1229,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     pf.hit_plan_ok = ctx->hit_valid && key.same(ctx->hit_key);
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
-    pf.host_wait = bins.plan_miss != nullptr;
+    pf.host_wait = bins.plan_miss != nullptr && !reuse;
     pf.kernel = kernel;
     pf.binned = binned;
     pf.rows = rows;
@@ -1266,7 +1315,7 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;
     bool missed = false;
-    if (binned && bins.plan_miss && (fs.plan_flag[0] | fs.plan_flag[1]) != 0u) {
+    if (binned && bins.plan_miss && pf.host_wait && (fs.plan_flag[0] | fs.plan_flag[1]) != 0u) {
         missed = true;
         // k_prep binned a pair into a region the plan fills, into the global
         // list or past a list's capacity: this frame renders every region as
