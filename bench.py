@@ -1235,7 +1235,10 @@ def main():
         # the timed loop's own planes (its last frame), checked against the oracle's rows
         last_cam = orbit_cams[(frame_no[0] - 1) % len(orbit_cams)] if orbit_cams else cam
         img_l, lb_l, u8_l, _ = planes_of[(frame_no[0] - 1) % inflight]
-        planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
+        # (its host copy is taken after the latency windows: host pages that a
+        # pageable device -> host copy locked, alive while a fresh context makes
+        # its first synchronous read-back, stalled that read-back 23-40 ms --
+        # tools/evict_probe.py, DESIGN.md "Measurement")
         if not args.no_latency:
             # in this process, right after the timed loop's streams and frame
             # sets (what a drop-in caller that renders an Image after streaming
@@ -1246,6 +1249,7 @@ def main():
             result["latency"]["process"] = "the bench process, after the timed loop (its contexts still open)"
             result["latency"]["child_process"] = end_to_end_isolated(args, W, H, device_index)
         if not args.no_cpu_baseline:
+            planes = (img_l.cpu().numpy(), lb_l.cpu().numpy(), u8_l.cpu().numpy())
             result["cpu_baseline"] = cpu_baseline(tris, last_cam, W, H, args.cpu_seconds, planes)
 
     if root and not strips and not signed and inflight > 1:

@@ -168,9 +168,10 @@ int xrt_debug_set_tile_plan(xrt_context* ctx, int on);
  * Diagnostics: k_prep's per-wave timestamps.  enable 1 / 0 turns the records
  * on / off for later launches (-1 leaves it); *n_waves = the waves of the last
  * recorded launch; with dst, waits for the context's work and copies up to
- * `capacity` records of 4 u32 (s_memrealtime, 100 MHz, low 32 bits: the
- * wave's start, after its records and footprints, after its cell tests, its
- * end).
+ * `capacity` records of 8 u32 (s_memrealtime, 100 MHz, low 32 bits): the
+ * wave's start, its triangle's record formed, its footprint, the binning's LDS
+ * staging and scan, the union of its rectangles, small then large rectangles'
+ * cells tested, its end.
  */
 int xrt_debug_prep_times(xrt_context* ctx, int enable, uint32_t* dst, uint64_t capacity, uint64_t* n_waves);
 

@@ -256,11 +256,11 @@ class Context:
 
     def prep_times(self, enable=None) -> np.ndarray:
         """k_prep's per-wave timestamps of the last recorded launch (xrt_debug_prep_times):
-        (n, 4) u32 start / after footprints / after cell tests / end; enable turns recording on / off."""
+        (n, 8) u32 stamps (xrt_debug.h); enable turns recording on / off."""
         n = ctypes.c_uint64()
         en = -1 if enable is None else int(bool(enable))
         self._check(self._lib.xrt_debug_prep_times(self._ctx, en, None, 0, ctypes.byref(n)), "xrt_debug_prep_times")
-        out = np.zeros((n.value, 4), np.uint32)
+        out = np.zeros((n.value, 8), np.uint32)
         if n.value and enable is None:
             self._check(self._lib.xrt_debug_prep_times(self._ctx, -1, out.ctypes.data, n.value, ctypes.byref(n)),
                         "xrt_debug_prep_times")

@@ -1606,15 +1606,23 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                                               float* __restrict__ offsets_out,
                                               uint4* __restrict__ prep_times)
 {
-    // Diagnostics (xrt_debug_prep_times; null otherwise): per wave its
-    // s_memrealtime at the start, after the records and footprints, after the
-    // cell tests (binning phase 1) and at the end.
-    const uint32_t t_start = prep_times ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
-    uint32_t t_fp = 0u, t_cells = 0u;
-    auto stamp_end = [&]() {
-        if (prep_times && (threadIdx.x & 63u) == 0u)
-            prep_times[blockIdx.x * kPrepWaves + (threadIdx.x >> 6)] =
-                make_uint4(t_start, t_fp, t_cells, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    // Diagnostics (xrt_debug_prep_times; null otherwise): per wave 8
+    // s_memrealtime stamps -- [0] start, [1] triangle loaded and its record
+    // formed, [2] footprint, [3] the binning's LDS staging and scan, [4] the
+    // union of the wave's rectangles, [5] small rectangles' cells tested,
+    // [6] large rectangles' cells tested (binning phase 1), [7] end.
+    uint32_t ts[8] = {};
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if (prep_times) ts[k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+    auto stamp_end = [&]() __attribute__((always_inline)) {
+        stamp(7);
+        if (prep_times && (threadIdx.x & 63u) == 0u) {
+            uint4* o = prep_times + 2 * (blockIdx.x * kPrepWaves + (threadIdx.x >> 6));
+            o[0] = make_uint4(ts[0], ts[1], ts[2], ts[3]);
+            o[1] = make_uint4(ts[4], ts[5], ts[6], ts[7]);
+        }
     };
     // The preparation shares the CUs with earlier frames' renders (prep
     // stream) at the default wave priority: frames are prepared ahead of their
@@ -1658,6 +1666,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             r.pad1 = ny / len;
             r.pad2 = nz / len;
         }
+        stamp(1);
         if (culls) {
             fp = compute_footprint(r, p, cp);
             fp.e0.w = __uint_as_float(tri);          // the region entries carry the id (make_entry's layout)
@@ -1691,7 +1700,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 #if !XRT_PREP_LATE_STORES
     store_outputs();                               // (A/B: the stores before the binning)
 #endif
-    if (prep_times) t_fp = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    stamp(2);
     if (!bins.counts) {                            // kernel-uniform
 #if XRT_PREP_LATE_STORES
         store_outputs();
@@ -1771,6 +1780,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    stamp(3);
 
 #if XRT_PREP_AGG
     // the union of the wave's rectangles (wave-uniform)
@@ -1795,6 +1805,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 #endif
     // No lists (the sizing pass of a new geometry, DESIGN.md "List sizing"):
     // the pairs are counted, nothing is stored, nothing can overflow.
+    stamp(4);
     const uint32_t count_only = wave_uniform(bins.list == nullptr ? 1u : 0u);
 #if XRT_PREP_BUFFER_OPS
     // the commit's tables as buffers (range-checked: kBufferOut is past all of them)
@@ -2023,6 +2034,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
         }
         enqueue(pass, rx, ry, lo);
     }
+    stamp(5);
     // (1b) large rectangles, one at a time over the whole wave
     unsigned long long mbig = __ballot(big);
     while (mbig) {                                 // wave-uniform
@@ -2040,7 +2052,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (prep_times) t_cells = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    stamp(6);
     commit();                                      // (2)
     // A region count past the list capacity: the render of that region falls
     // back to the whole mesh, and the host grows the lists for the next frame

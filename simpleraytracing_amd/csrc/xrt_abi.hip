@@ -771,7 +771,7 @@ int launch_prep(xrt_context* ctx, FrameSet& fs, const RenderParams& p, const Cul
                                                (threads + kPrepThreads - 1) / kPrepThreads);
     uint4* ptimes = nullptr;                       // xrt_debug_prep_times
     if (ctx->prep_times_on) {
-        int rc = ensure(ctx, ctx->d_prep_times, ctx->prep_times_cap, (size_t)blocks * kPrepWaves);
+        int rc = ensure(ctx, ctx->d_prep_times, ctx->prep_times_cap, 2 * (size_t)blocks * kPrepWaves);
         if (rc) return rc;
         ptimes = ctx->d_prep_times;
         ctx->prep_times_n = (size_t)blocks * kPrepWaves;
@@ -2199,7 +2199,7 @@ int xrt_debug_prep_times(xrt_context* ctx, int enable, uint32_t* dst, uint64_t c
     int rc = sync_context(ctx);
     if (rc) return rc;
     const size_t n = std::min<size_t>(capacity, ctx->prep_times_n);
-    XRT_HIP(ctx, hipMemcpy(dst, ctx->d_prep_times, n * sizeof(uint4), hipMemcpyDeviceToHost));
+    XRT_HIP(ctx, hipMemcpy(dst, ctx->d_prep_times, n * 2 * sizeof(uint4), hipMemcpyDeviceToHost));
     return XRT_OK;
 }
 

@@ -16,8 +16,9 @@ for v in ${VARIANTS:-early late}; do
 import json, sys
 for f in sys.argv[1:3]:
     d = json.load(open(f)); b = d["beside"]; a = d["alone"][-1]
-    print(sys.argv[3], d["size"], "alone span %.1f wave p50 %.1f cells p50 %.1f" % (a["span_us"], a["wave_us"]["p50"], a["cells_us"]["p50"]),
-          "| beside span %.1f start p90 %.1f wave p50 %.1f fp p50 %.1f cells p50 %.1f commit p50 %.1f" % (
-          b["span_us"], b["start_us"]["p90"], b["wave_us"]["p50"], b["footprint_us"]["p50"], b["cells_us"]["p50"], b["commit_us"]["p50"]))
+    ph = ["load_record", "footprint", "stage_scan", "union", "cells_small", "cells_large", "commit_stores"]
+    for tag, x in (("alone", a), ("beside", b)):
+        print(sys.argv[3], d["size"], tag, "span %.1f start p90 %.1f wave p50 %.1f |" % (x["span_us"], x["start_us"]["p90"], x["wave_us"]["p50"]),
+              " ".join("%s %.2f" % (k, x[k + "_us"]["p50"]) for k in ph if k + "_us" in x))
 PY
 done

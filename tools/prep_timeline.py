@@ -25,17 +25,20 @@ def pct(x):
     return {f"p{q}": round(float(np.percentile(x, q)), 2) for q in (0, 10, 50, 90, 100)} if len(x) else {}
 
 
+PHASES = ["load_record", "footprint", "stage_scan", "union", "cells_small", "cells_large", "commit_stores"]
+
+
 def summary(t, label):
     t = t.astype(np.int64)
     ref = t[:, 0].min()
     rel = (t - ref) % 2**32 / 100.0                       # us from the first wave's start
-    start, fp, cells, end = rel[:, 0], rel[:, 1], rel[:, 2], rel[:, 3]
-    binned = t[:, 2] != 0
+    start, end = rel[:, 0], rel[:, 7]
     out = {"what": label, "waves": int(len(t)), "span_us": round(float(end.max()), 2),
-           "start_us": pct(start), "wave_us": pct(end - start), "footprint_us": pct(fp - start)}
-    if binned.any():
-        out["cells_us"] = pct((cells - fp)[binned])
-        out["commit_us"] = pct((end - cells)[binned])
+           "start_us": pct(start), "wave_us": pct(end - start)}
+    valid = (t[:, 1:7] != 0).all(axis=1)
+    for k, name in enumerate(PHASES):
+        if valid.any():
+            out[name + "_us"] = pct((rel[:, k + 1] - rel[:, k])[valid])
     return out, ref
 
 
