@@ -407,6 +407,19 @@ def planes_equal(a, b) -> bool:
             and np.array_equal(np.asarray(a[2]), np.asarray(b[2])))
 
 
+def device_planes_equal(ctx, cam, H, planes, scratch, stream) -> bool:
+    """Device planes (img, lb, u8 tensors) against a synchronous render of `cam`
+    into `scratch`, compared bit for bit ON the device: no pageable device ->
+    host copy in the bench process before its latency windows (live host pages
+    such a copy locked stalled a fresh context's first read-back 11-40 ms:
+    tools/evict_probe.py)."""
+    import torch
+    ctx.render_rows_device(cam, 0, H, *(t.data_ptr() for t in scratch), stream.cuda_stream)
+    stream.synchronize()
+    return all(torch.equal(a.view(torch.int32), b.view(torch.int32)) if a.dtype == torch.float32 else torch.equal(a, b)
+               for a, b in zip(planes, scratch))
+
+
 def gather_verdict(dist, torch, rank: int, ok: bool, where) -> int:
     """Every rank learns rank 0's verdict on the gathered frame (`ok` is read on
     rank 0 only) and returns its exit code: 0, or EXIT_GATHER_MISMATCH on every
@@ -1092,11 +1105,17 @@ def main():
                 el = time.perf_counter() - t_o
                 g1, q1 = oc.geometry_counters(), oc.pipeline_counters()
                 exact = True
+                scratch = (torch.empty(W * H, dtype=torch.float32, device=dev),
+                           torch.empty(W * H, dtype=torch.float32, device=dev),
+                           torch.empty(W * H, dtype=torch.uint8, device=dev))
                 for j in range(inflight):
                     k = n_warm + n_timed - 1 - j
-                    img_k, lb_k, u8_k, _ = oplanes[k % inflight]
-                    exact &= planes_equal((img_k.cpu().numpy(), lb_k.cpu().numpy(), u8_k.cpu().numpy()),
-                                          oc.render_rows(cams_o[k]))
+                    with xrt.Context(device_index) as ref_ctx:       # a fresh context's synchronous render
+                        ref_ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
+                        ref_ctx.upload_mesh(tris)
+                        exact &= device_planes_equal(ref_ctx, cams_o[k], H, oplanes[k % inflight][:3], scratch,
+                                                     planes_of[0][3])
+                del scratch
             if not exact:
                 raise SystemExit(f"bench.py: an orbit frame ({deg:g} deg per frame) differs from its synchronous render")
             ms = el / n_timed * 1e3

@@ -32,6 +32,8 @@ struct BinState {
     unsigned int global_count;  // triangles in the global list
     unsigned int overflow;      // some region count exceeded the list capacity
     unsigned int cursor;        // a device-sized frame's pool cursor (k_size_lists)
+    unsigned int pairs;         // a device-sized frame's appended pairs (BinBuffers::pairs)
+    unsigned int pad[3];
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -1494,6 +1496,12 @@ struct BinBuffers {
     // 1: this frame's geometry is the one its layout's tile plan was taken for
     // (SlotDesc::live may skip tiles); 0: every tile renders.
     uint32_t tile_plan;
+    // Device-sized frames (a moving camera): the count-only pass also appends
+    // every pair as (slot, its index in the slot's list, triangle) to `pairs`
+    // (BinState::pairs counts them, at most pairs_cap); k_scatter_pairs writes
+    // the entries once k_size_lists has placed the lists.  Null: no pairs.
+    uint4* pairs;
+    uint32_t pairs_cap;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -1817,10 +1825,31 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     const __amdgpu_buffer_rsrc_t r_desc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<SlotDesc*>(bins.desc), 0, (int)(n_regions * (uint32_t)sizeof(SlotDesc)), kBufferWord3);
 #endif
+    const uint32_t tri_base = (blockIdx.x * kPrepWaves + wave) * p.prep_tris;   // the triangle of lane 0
     uint32_t my_max = 0;                           // 1 + the largest slot this lane took
     bool over = false;                             // a slot past its list's capacity
     uint32_t queued = 0;                           // wave-uniform queue length
-    auto commit = [&]() {
+#if XRT_PREP_AGG
+    // Device sizing (BinBuffers::pairs), aggregated commit: every queued pair
+    // as (slot, its index in the slot's list, triangle) -- s_alb[c] holds the
+    // cell's slot, s_acnt[c] its base index, s_qoff the pair's offset in its
+    // cell -- appended to the frame's pair buffer, one atomic per wave.
+    auto append_pairs = [&](bool) __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t at = 0;
+        if (lane == 0u) at = atomicAdd(&bs->pairs, queued);
+        at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
+        for (uint32_t q = lane; q < queued; q += 64u) {
+            const uint32_t c = s_qreg[wave][q];
+            if (at + q < bins.pairs_cap)
+                bins.pairs[at + q] = make_uint4(s_alb[wave][c], s_acnt[wave][c] + s_qoff[wave][q],
+                                                tri_base + s_qown[wave][q], 0u);
+        }
+    };
+#endif
+    auto commit = [&]() __attribute__((always_inline)) {
 #if XRT_PREP_AGG
         if (agg) {
             // (a) per-cell counts in LDS; each pair's offset in its cell
@@ -1864,6 +1893,17 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 clc[k] = bc[1];
             }
             if (count_only) {                       // the sizing pass: counts only
+                if (bins.pairs) {                   // (device sizing: and the pairs)
+#pragma unroll
+                    for (uint32_t k = 0; k < kAggRounds; ++k) {
+                        const uint32_t c = k * 64u + lane;
+                        if (cs[k] != kEmpty) {
+                            s_acnt[wave][c] = cb[k];
+                            s_alb[wave][c] = cs[k];
+                        }
+                    }
+                    append_pairs(true);
+                }
                 __builtin_amdgcn_wave_barrier();
                 queued = 0;
                 return;
@@ -1975,7 +2015,24 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 lcap[b] = bc.y;
             }
 #endif
-            if (count_only) continue;              // the sizing pass: counts only
+            if (count_only) {                      // the sizing pass: counts only
+                if (bins.pairs) {                  // (device sizing: and the pairs)
+#pragma unroll
+                    for (uint32_t b = 0; b < kBinBatch; ++b) {
+                        const unsigned long long vm = __ballot(reg[b] != kEmpty);
+                        uint32_t at = 0;
+                        if (lane == 0u && vm) at = atomicAdd(&bs->pairs, (uint32_t)__popcll(vm));
+                        at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
+                        if (reg[b] != kEmpty) {
+                            const uint32_t q = at + __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+                            if (q < bins.pairs_cap)
+                                bins.pairs[q] = make_uint4(reg[b], slot[b], tri_base + own[b], 0u);
+                        }
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 if (reg[b] == kEmpty) continue;
@@ -2102,9 +2159,38 @@ __global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ count
         const uint32_t base = base0 + incl - c;
         const uint32_t cap = base >= pool ? 0u : min(c, pool - base);
         out[s] = SlotDesc{min(base, pool), cap, fixed[s].xy, 0xFFFFu};
-        counts[(size_t)s * kCounterStride] = 0u;
     }
-    if (s == 0u) bs->global_count = 0u;             // the fill pass appends the global list again
+}
+
+// k_scatter_pairs: the entries of a device-sized frame (after k_size_lists):
+// pair i = (slot, index in the slot's list, triangle) from k_prep's count pass
+// becomes the triangle's region entry -- its footprint from the frame's cull
+// planes, e0.w = its id -- at list[base(slot) + index].  A pair past its list's
+// capacity (the pool ran out) is dropped and flagged: that region's count
+// exceeds its capacity, so the render takes it from the whole mesh (exact).
+__global__ __launch_bounds__(256) void k_scatter_pairs(const uint4* __restrict__ pairs, const BinState* __restrict__ bs,
+                                                      uint32_t pairs_cap, const SlotDesc* __restrict__ desc,
+                                                      const float4* __restrict__ culls, uint32_t T,
+                                                      RegionEntry* __restrict__ list, uint32_t* __restrict__ flag)
+{
+    const uint32_t total = as_const(bs)->pairs;
+    const uint32_t n = min(total, pairs_cap);
+    if (blockIdx.x == 0u && threadIdx.x == 0u && total > pairs_cap && flag) flag[1] = 1u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint4 pr = pairs[i];
+        const SlotDesc d = desc[pr.x];
+        if (pr.y >= d.cap) {
+            if (flag) flag[1] = 1u;
+            continue;
+        }
+        float4 e0 = culls[(size_t)T + pr.z];
+        e0.w = __uint_as_float(pr.z);
+        float4* e = reinterpret_cast<float4*>(list + (size_t)d.base + pr.y);
+        e[0] = e0;
+        e[1] = culls[2 * (size_t)T + pr.z];
+        e[2] = culls[3 * (size_t)T + pr.z];
+        e[3] = culls[pr.z];
+    }
 }
 
 // ---------------------------------------------------------------------------

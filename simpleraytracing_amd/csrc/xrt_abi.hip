@@ -176,6 +176,8 @@ struct FrameSet {
     // (hipExtLaunchKernel stop events): no separate event packets.
     SlotDesc* dyn_desc = nullptr;      // a device-sized frame's launch layout (k_size_lists)
     size_t dyn_desc_cap = 0;
+    uint4* pairs = nullptr;            // its (slot, index, triangle) pairs (k_prep's count pass)
+    size_t pairs_cap = 0;
     bool lazy_flags = false;           // plan_flag armed for a frame launched without reading it
     hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
     hipEvent_t done = nullptr;         // render end (a stop event on the render's dispatch)
@@ -312,6 +314,7 @@ struct xrt_context {
     SlotLayout compact_layout;
     uint64_t slot_pool = 0;            // entries of the compact lists
     uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
+    uint64_t motion_pool_forced = 0;   // test hook XRT_MOTION_POOL: that many entries, never grown
     bool compact = false;              // compact_layout is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     // Fill plan of the current geometry (bin_key): the compact layout's
@@ -1101,33 +1104,44 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // slot's list from the set's pool, k_prep bins into them.  Every region
         // renders as tiles (no fill plan: the host never sees the counts).
         // k_prep's flags are read when the set is next used (lazy_flags).
-        ctx->motion_pool = std::max<uint64_t>(ctx->motion_pool, std::max<uint64_t>(2 * ctx->slot_pool, 65536u));
+        ctx->motion_pool = ctx->motion_pool_forced
+                               ? ctx->motion_pool_forced
+                               : std::max<uint64_t>(ctx->motion_pool, std::max<uint64_t>(2 * ctx->slot_pool, 65536u));
         bool cleared = false;
         if ((rc = bin_buffers(ctx, fs, n_regions, ctx->motion_pool, bins, bin_ctl, ps, cleared))) return rc;
         if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
         if ((rc = ensure(ctx, fs.dyn_desc, fs.dyn_desc_cap, n_regions))) return rc;
+        if ((rc = ensure(ctx, fs.pairs, fs.pairs_cap, ctx->motion_pool))) return rc;
+        const uint32_t pool = (uint32_t)std::min<uint64_t>(ctx->motion_pool, 0xFFFFFFFFull);
         bins.tile_slots = n_regions;
         bins.split_slots = 0u;
         bins.tile_plan = 0u;
         bins.plan_miss = nullptr;
         RegionEntry* const list = bins.list;
-        bins.list = nullptr;                           // the count-only pass
+        bins.list = nullptr;                           // the count-only pass, appending its pairs
+        bins.pairs = fs.pairs;
+        bins.pairs_cap = pool;
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, nullptr))) return rc;
         hipLaunchKernelGGL(k_size_lists, dim3((n_regions + 255) / 256), dim3(256), 0, ps, bins.counts,
-                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, (uint32_t)std::min<uint64_t>(
-                               ctx->motion_pool, 0xFFFFFFFFull), bin_ctl);
+                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, pool, bin_ctl);
+        XRT_HIP(ctx, hipGetLastError());
+        uint32_t* const flag = fs.plan_flag ? const_cast<uint32_t*>(fs.plan_flag) : nullptr;
+        if (flag) {                                    // [1]: a list past the pool, read lazily
+            flag[0] = 0u;
+            flag[1] = 0u;
+            fs.lazy_flags = true;
+        }
+        const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((pool + 255u) / 256u, 2048u);
+        hipExtLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, ps, nullptr, prep_done, 0u,
+                              (const uint4*)fs.pairs, (const BinState*)bin_ctl, pool, (const SlotDesc*)fs.dyn_desc,
+                              (const float4*)fs.cull, (uint32_t)T, list, flag);
         XRT_HIP(ctx, hipGetLastError());
         bins.list = list;
         bins.desc = fs.dyn_desc;
-        bins.clear = nullptr;                          // (the count pass cleared the other half)
-        if (fs.plan_flag) {                            // [1]: a list past the pool, read lazily
-            fs.plan_flag[0] = 0u;
-            fs.plan_flag[1] = 0u;
-            bins.plan_miss = const_cast<uint32_t*>(fs.plan_flag);
-            fs.lazy_flags = true;
-        }
+        bins.pairs = nullptr;
+        bins.clear = nullptr;
     }
-    if (rows > 0 && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+    if (rows > 0 && !reuse && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
     if (sizing) {
         // Size the compact region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of every region's count (the count-only
@@ -1665,6 +1679,7 @@ int xrt_create(int device, xrt_context** out)
     const char* sp = std::getenv("XRT_SIZING_PROFILE");
     ctx->sizing_profile = sp ? std::atoi(sp) : 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
+    if (const char* mp = std::getenv("XRT_MOTION_POOL")) ctx->motion_pool_forced = std::strtoull(mp, nullptr, 10);
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
         n_cu = 256;

@@ -472,6 +472,42 @@ def test_moving_camera_reuses_lists_exactly(dragon, W, H, r0, r1, degs):
     assert paths[still]["sizings"] == 1 and fills[still] > 0, (paths[still], fills[still])
 
 
+def test_moving_camera_pool_overflow_exact(dragon, monkeypatch):
+    """A moving camera's device-sized lists with a pool far too small
+    (XRT_MOTION_POOL=300 entries): the lists that do not fit get what is left,
+    their regions render from the whole mesh (exact), k_prep's flags report
+    the overflows when the set is next used; every frame, through device planes
+    on two streams, equals a brute-force render of its camera."""
+    import torch
+    monkeypatch.setenv("XRT_MOTION_POOL", "300")
+    W, H = 512, 384
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    cams = [orbit_camera(base, centre, 2.0 * k) for k in range(10)]
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    with xrt.Context(0) as brute:
+        brute.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        brute.upload_mesh(dragon)
+        refs = [brute.render_rows(c) for c in cams]
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        outs = [(torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+                 torch.empty(W * H, dtype=torch.uint8, device=dev)) for _ in cams]
+        for k, cam in enumerate(cams):
+            c.render_rows_device(cam, 0, H, *(t.data_ptr() for t in outs[k]), streams[k % 2].cuda_stream)
+        torch.cuda.synchronize(dev)
+        for k in range(len(cams)):
+            for x, y in zip(outs[k], refs[k][:3]):
+                assert np.array_equal(bits(x.cpu().numpy()), bits(y)), k
+        for cam in cams[:4]:                                   # the sets come round: flags read
+            c.render_rows(cam)
+        g = c.geometry_counters()
+    assert g["reused"] >= 9 and g["overflows"] > 0, g
+
+
 @pytest.mark.parametrize("devices", [[0, 0]])
 def test_multi_strips_orbit_exact(dragon, devices):
     """xrt_render_rows_multi under a moving camera: its contexts size
