@@ -16,7 +16,7 @@ import statistics
 
 
 def short(name):
-    for k in ("k_prep", "k_size_lists", "k_render_binned_hits", "k_render_binned", "k_render_tiled", "k_render_brute",
+    for k in ("k_prep", "k_size_lists", "k_scatter_pairs", "k_render_binned_hits", "k_render_binned", "k_render_tiled", "k_render_brute",
               "k_reduce_stats", "k_tile_plan", "k_band_model", "k_hole_fill"):
         if k in name:
             return k
@@ -43,7 +43,7 @@ def main():
     for j in range(1, len(renders)):
         a, b = renders[j - 1], renders[j]
         r0, r1 = rows[a], rows[b]
-        prep = [rows[i] for i in range(a + 1, b) if rows[i][2] in ("k_prep", "k_size_lists")]
+        prep = [rows[i] for i in range(a + 1, b) if rows[i][2] in ("k_prep", "k_size_lists", "k_scatter_pairs")]
         steps.append((r1[0] - r0[0]) / 1e3)
         durs.append((r1[1] - r1[0]) / 1e3)
         if prep:
