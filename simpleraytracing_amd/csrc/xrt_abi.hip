@@ -178,10 +178,6 @@ struct FrameSet {
     size_t dyn_desc_cap = 0;
     uint4* pairs = nullptr;            // its (slot, index, triangle) pairs (k_prep's count pass)
     size_t pairs_cap = 0;
-    SlotDesc* plan_desc = nullptr;     // its render layout (tiles first, then fills) and counts by it
-    size_t plan_desc_cap = 0;
-    uint32_t* plan_counts = nullptr;
-    size_t plan_counts_cap = 0;
     bool lazy_flags = false;           // plan_flag armed for a frame launched without reading it
     hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
     hipEvent_t done = nullptr;         // render end (a stop event on the render's dispatch)
@@ -319,7 +315,6 @@ struct xrt_context {
     uint64_t slot_pool = 0;            // entries of the compact lists
     uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
     uint64_t motion_pool_forced = 0;   // test hook XRT_MOTION_POOL: that many entries, never grown
-    bool device_fill = true;           // moving frames render over the device fill plan (XRT_DEVICE_FILL=0: off)
     bool compact = false;              // compact_layout is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     // Fill plan of the current geometry (bin_key): the compact layout's
@@ -1117,8 +1112,6 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
         if ((rc = ensure(ctx, fs.dyn_desc, fs.dyn_desc_cap, n_regions))) return rc;
         if ((rc = ensure(ctx, fs.pairs, fs.pairs_cap, ctx->motion_pool))) return rc;
-        if ((rc = ensure(ctx, fs.plan_desc, fs.plan_desc_cap, n_regions))) return rc;
-        if ((rc = ensure(ctx, fs.plan_counts, fs.plan_counts_cap, (size_t)n_regions * kCounterStride))) return rc;
         const uint32_t pool = (uint32_t)std::min<uint64_t>(ctx->motion_pool, 0xFFFFFFFFull);
         bins.tile_slots = n_regions;
         bins.split_slots = 0u;
@@ -1130,8 +1123,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.pairs_cap = pool;
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, nullptr))) return rc;
         hipLaunchKernelGGL(k_size_lists, dim3((n_regions + 255) / 256), dim3(256), 0, ps, bins.counts,
-                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, pool, bin_ctl, fs.plan_desc,
-                           fs.plan_counts);
+                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, pool, bin_ctl);
         XRT_HIP(ctx, hipGetLastError());
         uint32_t* const flag = fs.plan_flag ? const_cast<uint32_t*>(fs.plan_flag) : nullptr;
         if (flag) {                                    // [1]: a list past the pool, read lazily
@@ -1144,14 +1136,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
                               (const uint4*)fs.pairs, (const BinState*)bin_ctl, pool, (const SlotDesc*)fs.dyn_desc,
                               (const float4*)fs.cull, (uint32_t)T, list, flag);
         XRT_HIP(ctx, hipGetLastError());
-        // the render: the device fill plan's layout (tiles first, one fill
-        // workgroup per empty region); its grid covers every region as tiles
         bins.list = list;
-        bins.desc = ctx->device_fill ? fs.plan_desc : fs.dyn_desc;
-        if (ctx->device_fill) {
-            bins.counts = fs.plan_counts;
-            bins.dev_plan = 1u;
-        }
+        bins.desc = fs.dyn_desc;
         bins.pairs = nullptr;
         bins.clear = nullptr;
     }
@@ -1694,7 +1680,6 @@ int xrt_create(int device, xrt_context** out)
     ctx->sizing_profile = sp ? std::atoi(sp) : 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
     if (const char* mp = std::getenv("XRT_MOTION_POOL")) ctx->motion_pool_forced = std::strtoull(mp, nullptr, 10);
-    if (const char* df = std::getenv("XRT_DEVICE_FILL")) ctx->device_fill = std::atoi(df) != 0;
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
@@ -1780,10 +1765,6 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
         (void)hipFree(fs.times);
-        (void)hipFree(fs.dyn_desc);
-        (void)hipFree(fs.pairs);
-        (void)hipFree(fs.plan_desc);
-        (void)hipFree(fs.plan_counts);
         for (hipEvent_t e : {fs.ready, fs.done})
             if (e) (void)hipEventDestroy(e);
     }
