@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--orbit-legs", type=float, nargs="*", default=[0.25, 1.0], metavar="DEG",
                     help="after the timed region (one GPU, frames mode): a moving-camera leg per value, the camera "
                          "turning DEG degrees per frame (reported under `orbit`, never `value`); none: no legs")
+    ap.add_argument("--no-tile-plan-leg", action="store_true",
+                    help="skip the opt-in tile plan's leg after the timed region (counter runs: its renders differ)")
     ap.add_argument("--orbit-frames", type=int, default=60,
                     help="timed frames per orbit leg (at least --steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1052,7 +1054,7 @@ def main():
     # the cull of tiles an earlier frame of the same camera found dead).
     with_tile_plan = None
     if root and not strips and not signed and not orbit_cams and world == 1 and args.steps > 0 and \
-            args.kernel in ("auto", "binned"):
+            args.kernel in ("auto", "binned") and not args.no_tile_plan_leg:
         ctx.set_tile_plan(True)
         run_steps(max(args.warmup, 4))
         torch.cuda.synchronize(dev)

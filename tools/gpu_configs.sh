@@ -32,11 +32,11 @@ for c in "${CONFIGS[@]}"; do
   IFS='|' read -r name args short key <<< "$c"
   base=$(echo "$args" | sed -e 's/--steps [0-9]*//' -e 's/--warmup [0-9]*//')
   echo "[$name] kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${name}_trace -o run -- python3 bench.py --no-cpu-baseline --no-latency --no-timing-check $base $short > $OUT/${name}_trace_bench.json 2> $OUT/${name}_trace.err || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${name}_trace -o run -- python3 bench.py --no-cpu-baseline --no-latency --no-timing-check --orbit-legs --no-tile-plan-leg $base $short > $OUT/${name}_trace_bench.json 2> $OUT/${name}_trace.err || exit 1
   i=0
   for grp in "${PASSES[@]}"; do
     i=$((i+1))
-    timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/${name}_pmc/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --ramp-ms 0 --no-timing-check $base $short > /dev/null 2> $OUT/${name}_pmc$i.err || exit 1
+    timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/${name}_pmc/p$i -o run -- python3 bench.py --no-cpu-baseline --no-latency --ramp-ms 0 --no-timing-check --orbit-legs --no-tile-plan-leg $base $short > /dev/null 2> $OUT/${name}_pmc$i.err || exit 1
   done
   python3 tools/pmc_summary.py $OUT/${name}_pmc > $OUT/pmc_summary_${name}.txt || exit 1
   python3 tools/make_traffic_json.py $OUT/${name}_pmc/summary.json "binned:$key" --kernel "k_render_binned<false>" --source-as profiles/$TAG/pmc_summary_${name}.json > /dev/null || exit 1
