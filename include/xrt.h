@@ -373,7 +373,11 @@ int xrt_multi_set_gather(xrt_multi* m, int mode);
  * values, rendered straight into that layout (xrt_set_transit_hits; the plan
  * is made once per geometry, synchronously); a frame of a new geometry sends
  * the packed layout.  XRT_TRANSIT_PACKED: always the 32x32 blocks of the
- * regions the fill plan leaves (xrt_set_transit_layout's layout).
+ * regions the fill plan leaves (xrt_set_transit_layout's layout).  A received
+ * hit mask that disagrees with its sender's plan fails the call that sees it
+ * (xrt_render_rows_multi: that frame; the device entry: its next call) with
+ * XRT_ERR_DEVICE and drops the hit plans (the next frames travel packed, then
+ * plan again).
  */
 #define XRT_TRANSIT_PACKED 0
 #define XRT_TRANSIT_HITS 1
@@ -391,16 +395,19 @@ int xrt_multi_set_transit(xrt_multi* m, int mode);
  *                       devices 1 .. n-1 the bands above it, then below it, in
  *                       frame order, so that max(device 0's render + unpack,
  *                       each sender's max(render, bytes / link)) is least
- *                       (xrt_balanced_bounds).  The model comes from device 0:
- *                       the whole frame rendered (binned) once per frame
- *                       geometry -- per band its share of the render (the waves'
- *                       timing records) and its packed bytes -- and the link
- *                       rate: link_bytes_per_us when > 0, else measured once
- *                       (every sender sends 4 MB to device 0 at once through
- *                       this context's gather).  Planning is synchronous and
- *                       happens on the first frame of a geometry.  The signed
- *                       model, and frames with fewer bands than devices, split
- *                       equally.
+ *                       (xrt_balanced_bounds).  The model comes from the
+ *                       strips' own renders of an earlier frame -- per band the
+ *                       wave time of its regions (timing records, summed on each
+ *                       device behind its render of a new camera) and its
+ *                       transit bytes -- never from an extra render; the first
+ *                       frame of a multi context has no model and splits
+ *                       equally.  Link rate: link_bytes_per_us when > 0, else
+ *                       measured once per context and gather path (every sender
+ *                       sends 4 MB to device 0 at once through the context's
+ *                       gather) when a balanced plan is first made.  A camera
+ *                       keeps its plan; a new camera plans from the latest
+ *                       complete model without waiting.  The signed model, and
+ *                       frames with fewer bands than devices, split equally.
  * Every split is exact: the gathered frame equals one device's frame.
  */
 #define XRT_SPLIT_EQUAL 0
@@ -408,7 +415,8 @@ int xrt_multi_set_transit(xrt_multi* m, int mode);
 int xrt_multi_set_split(xrt_multi* m, int mode, double link_bytes_per_us);
 
 /*
- * The strips of `camera`'s frame (planned now when its geometry is new):
+ * The strips of `camera`'s frame (planned now from the latest strip model when
+ * the camera is new; the equal split, info zeros, before any frame):
  * bounds[2g], bounds[2g+1] = [begin, end) rows of device g's strip (2n
  * entries).  info (may be NULL): [0] the link rate the plan used (bytes per
  * microsecond), [1] the modelled frame's render span (us), [2] the step the

@@ -289,6 +289,15 @@ struct PendingFrame {
     Outputs out;
     BinBuffers bins = {};
     BinState* bin_ctl = nullptr;
+    // A device-sized frame (a moving camera): k_size_lists and k_scatter_pairs
+    // run on the render's stream ahead of the render (the prep stream holds
+    // only the count passes, so the next frame's k_prep is not queued behind them).
+    struct DevSize {
+        bool on = false;
+        uint32_t n_slots = 0, pool = 0;
+        const SlotDesc* fixed = nullptr;
+        uint32_t* flag = nullptr;
+    } dev_size;
     HostClock::time_point t_call;
 };
 
@@ -1121,21 +1130,19 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.list = nullptr;                           // the count-only pass, appending its pairs
         bins.pairs = fs.pairs;
         bins.pairs_cap = pool;
-        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, nullptr))) return rc;
-        hipLaunchKernelGGL(k_size_lists, dim3((n_regions + 255) / 256), dim3(256), 0, ps, bins.counts,
-                           (const SlotDesc*)bins.desc, fs.dyn_desc, n_regions, pool, bin_ctl);
-        XRT_HIP(ctx, hipGetLastError());
+        if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
         uint32_t* const flag = fs.plan_flag ? const_cast<uint32_t*>(fs.plan_flag) : nullptr;
         if (flag) {                                    // [1]: a list past the pool, read lazily
             flag[0] = 0u;
             flag[1] = 0u;
             fs.lazy_flags = true;
         }
-        const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((pool + 255u) / 256u, 2048u);
-        hipExtLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, ps, nullptr, prep_done, 0u,
-                              (const uint4*)fs.pairs, (const BinState*)bin_ctl, pool, (const SlotDesc*)fs.dyn_desc,
-                              (const float4*)fs.cull, (uint32_t)T, list, flag);
-        XRT_HIP(ctx, hipGetLastError());
+        // k_size_lists and k_scatter_pairs: launch_frame, on the render's stream
+        pf.dev_size.on = true;
+        pf.dev_size.n_slots = n_regions;
+        pf.dev_size.pool = pool;
+        pf.dev_size.fixed = bins.desc;
+        pf.dev_size.flag = flag;
         bins.list = list;
         bins.desc = fs.dyn_desc;
         bins.pairs = nullptr;
@@ -1325,6 +1332,17 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
         if (q == hipSuccess) ++ctx->hp_launch_nowait;
         else if (q == hipErrorNotReady) XRT_HIP(ctx, hipStreamWaitEvent(stream, pf.prep_done, 0));
         else XRT_HIP(ctx, q);
+    }
+    if (pf.dev_size.on) {                          // a device-sized frame's lists (prepare_frame)
+        const PendingFrame::DevSize& d = pf.dev_size;
+        hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, stream, pf.bins.counts, d.fixed,
+                           fs.dyn_desc, d.n_slots, d.pool, bin_ctl);
+        XRT_HIP(ctx, hipGetLastError());
+        const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((d.pool + 255u) / 256u, 2048u);
+        hipLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, stream, (const uint4*)fs.pairs,
+                           (const BinState*)bin_ctl, d.pool, (const SlotDesc*)fs.dyn_desc, (const float4*)fs.cull,
+                           (uint32_t)ctx->num_tris, pf.bins.list, d.flag);
+        XRT_HIP(ctx, hipGetLastError());
     }
     dim3 grid = pf.grid;
     BinBuffers bins = pf.bins;
