@@ -1103,6 +1103,7 @@ def main():
                 for k in range(n_warm, n_warm + n_timed):
                     img_k, lb_k, u8_k, s_k = optrs[k % inflight]
                     oc.render_rows_device(cams_o[k], 0, H, img_k, lb_k, u8_k, s_k)
+                enq = time.perf_counter() - t_o
                 torch.cuda.synchronize(dev)
                 el = time.perf_counter() - t_o
                 g1, q1 = oc.geometry_counters(), oc.pipeline_counters()
@@ -1126,7 +1127,8 @@ def main():
                 "vs_fixed_camera": ms / orbit["fixed_camera_ms_per_step"],
                 "sizings": g1["sizings"] - g0["sizings"], "reused_lists": g1["reused"] - g0["reused"],
                 "plan_misses": g1["plan_misses"] - g0["plan_misses"], "overflows": g1["overflows"] - g0["overflows"],
-                "host_waits": q1["host_waits"] - q0["host_waits"], "last_frames_bit_exact": bool(exact)}
+                "host_waits": q1["host_waits"] - q0["host_waits"], "last_frames_bit_exact": bool(exact),
+                "host_enqueue_ms_per_step": enq / n_timed * 1e3}
         del oplanes
         orbit["what"] = ("a fresh context per leg; the camera turns deg degrees per frame about the mesh centre "
                          "(scenes.orbit_camera); one xrt_render_rows_device call per frame, frames in flight as in "
