@@ -1531,6 +1531,9 @@ __device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot,
     live = d.w;
 }
 
+#ifndef XRT_BIN_TIGHT
+#define XRT_BIN_TIGHT 1   // the region rectangle of a footprint box: exactly the regions the box meets
+#endif
 // Region rectangle [x0,x1] x [y0,y1] (strip-relative region indices) that a
 // footprint box may touch; false when it touches none.
 __device__ __forceinline__ bool footprint_regions(float4 bb, const RenderParams& p,
@@ -1542,9 +1545,20 @@ __device__ __forceinline__ bool footprint_regions(float4 bb, const RenderParams&
     float xmin = fmaxf(bb.x, -64.0f), xmax = fminf(bb.y, (float)p.width + 64.0f);
     float ymin = fmaxf(bb.z - (float)p.row_begin, -64.0f), ymax = fminf(bb.w - (float)p.row_begin, rows + 64.0f);
     if (xmax < 0.0f || ymax < 0.0f || xmin > (float)p.width || ymin > rows) return false;
+    // Region r covers columns [32r, 32r + 31] and meets the box (box_overlaps'
+    // test) iff 32r + 31 >= xmin and 32r <= xmax: r from ceil((xmin - 31) / 32)
+    // to floor(xmax / 32).  (Rounded to nearest, the subtractions cannot cross an
+    // integer -- every integer here is a float -- so the computed first region is
+    // never past the exact one.)  Round 1-5 took floor for the first one too: one
+    // region column and row more than the box meets for nearly every footprint.
+#if XRT_BIN_TIGHT
+    int ix0 = (int)ceilf((xmin - 31.0f) * (1.0f / 32.0f));
+    int iy0 = (int)ceilf((ymin - 31.0f) * (1.0f / 32.0f));
+#else
     int ix0 = (int)floorf((xmin - 31.0f) * (1.0f / 32.0f));
-    int ix1 = (int)floorf(xmax * (1.0f / 32.0f));
     int iy0 = (int)floorf((ymin - 31.0f) * (1.0f / 32.0f));
+#endif
+    int ix1 = (int)floorf(xmax * (1.0f / 32.0f));
     int iy1 = (int)floorf(ymax * (1.0f / 32.0f));
     ix0 = max(ix0, 0);
     iy0 = max(iy0, 0);
