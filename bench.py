@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--no-tile-plan-leg", action="store_true",
                     help="skip the opt-in tile plan's leg after the timed region (counter runs: its renders differ)")
     ap.add_argument("--orbit-frames", type=int, default=60,
-                    help="timed frames per orbit leg (at least --steps)")
+                    help="timed frames per orbit leg (after 4 untimed ones)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI (production); gloo = CPU-staged, for rehearsing "
@@ -1082,7 +1082,7 @@ def main():
         orbit = {"fixed_camera_ms_per_step": elapsed_max / args.steps * 1e3}
         lo_, hi_ = xrt.mesh_bbox(tris)
         centre = 0.5 * (np.asarray(lo_, np.float64) + np.asarray(hi_, np.float64))
-        n_timed = max(args.steps, args.orbit_frames)
+        n_timed = args.orbit_frames            # the same sweep whatever K (a 1-degree leg turns 60 degrees)
         n_warm = 4
         # planes of their own (the main loop's last frames are checked below)
         oplanes = [(torch.zeros(W * H, dtype=torch.float32, device=dev), torch.zeros(W * H, dtype=torch.float32, device=dev),

@@ -2142,15 +2142,14 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 
 // ---------------------------------------------------------------------------
 // k_size_lists: the list sizing of a moving camera's frame on the device
-// (DESIGN.md "Moving camera"), between k_prep's count-only pass and its fill
-// pass on the prep stream -- no host round trip.  Each slot of the launch
-// layout `fixed` (its order and regions) gets room for exactly the pairs the
-// count pass counted, carved from the set's pool by one atomic per wave
-// (BinState::cursor; the lists need not follow the slot order); its counter
-// and the count pass's global-list count are zeroed for the fill pass.  A
-// slot past the pool gets what is left (its overflow makes the render take
-// that region from the whole mesh, exactly, and flags the frame: the host
-// grows the pool for later frames).
+// (DESIGN.md "Moving camera"), after k_prep's count-only pass (which appended
+// its pairs) and before k_scatter_pairs -- no host round trip.  Each slot of
+// the launch layout `fixed` (its order and regions) gets room for exactly the
+// pairs the count pass counted, carved from the set's pool by one atomic per
+// wave (BinState::cursor; the lists need not follow the slot order); the
+// counters stay (the render reads them).  A slot past the pool gets what is
+// left (its overflow makes the render take that region from the whole mesh,
+// exactly, and flags the frame: the host grows the pool for later frames).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ counts, const SlotDesc* __restrict__ fixed,
                                                    SlotDesc* __restrict__ out, uint32_t n_slots, uint32_t pool,
@@ -2169,9 +2168,14 @@ __global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ count
     uint32_t base0 = 0;
     if (lane == 0u && total) base0 = atomicAdd(&bs->cursor, total);
     base0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+    // More pairs than the pair buffer holds (its capacity is the pool's): the
+    // lost pairs may belong to any slot, so no list is known complete -- every
+    // region with a pair renders from the whole mesh (exact) and the frame is
+    // flagged (k_scatter_pairs).
+    const bool lost = as_const(bs)->pairs > pool;
     if (s < n_slots) {
         const uint32_t base = base0 + incl - c;
-        const uint32_t cap = base >= pool ? 0u : min(c, pool - base);
+        const uint32_t cap = lost || base >= pool ? 0u : min(c, pool - base);
         out[s] = SlotDesc{min(base, pool), cap, fixed[s].xy, 0xFFFFu};
     }
 }
