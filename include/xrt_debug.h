@@ -161,6 +161,14 @@ int xrt_debug_host_call_ms(xrt_context* ctx, double ms[16]);
  */
 int xrt_debug_tile_plan(xrt_context* ctx, uint64_t counters[2]);
 
+/*
+ * Host code (no device): the cull's direction grid of `camera` (DESIGN.md
+ * section 5, step 0) as the library computes it -- grids[0], a bisection per
+ * axis -- and by a scan of every row or column, grids[1].  Equal for every
+ * camera (the test's claim).
+ */
+int xrt_debug_direction_grid(const xrt_camera* camera, int grids[2]);
+
 /* Turns the tile plan on (1) or off (0) for later frames. */
 int xrt_debug_set_tile_plan(xrt_context* ctx, int on);
 

@@ -153,6 +153,7 @@ XRT_SYMBOLS = {
     "xrt_debug_destroy_ms": (ctypes.c_int, [_dp]),
     "xrt_debug_tile_plan": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_set_tile_plan": (ctypes.c_int, [_CtxP, ctypes.c_int]),
+    "xrt_debug_direction_grid": (ctypes.c_int, [ctypes.POINTER(Camera), ctypes.POINTER(ctypes.c_int)]),
     "xrt_debug_prep_times": (ctypes.c_int, [_CtxP, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_block_records": (ctypes.c_int, [_CtxP, _vp, _u64, ctypes.POINTER(_u64)]),

@@ -684,7 +684,38 @@ inline float pixel_offset(float spacing, uint32_t i, uint32_t n)
 // varies with both, a grid bound: X_k is a rounded sum of multiples of the
 // grids of its terms, every nonzero offset being >= spacing / 2.  0 when X_k
 // is 0 at every pixel.
-double min_nonzero_x(const xrt_camera& c, int k)
+// Smallest nonzero |x(i)| over i < n of a monotone sequence (non-decreasing or
+// non-increasing; NaN-free): the last element below 0 and the first above 0,
+// found by bisection -- O(log n) instead of a scan.
+template <typename F>
+double min_nonzero_monotone(uint32_t n, F x)
+{
+    double best = std::numeric_limits<double>::infinity();
+    if (n == 0) return best;
+    const bool up = x(0) <= x(n - 1);
+    // first index whose value is past 0 in the sequence's direction (n if none)
+    auto first = [&](auto past) {
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (past(x(mid))) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+    };
+    // up: the first x > 0, and the last x < 0 (one before the first x >= 0)
+    const uint32_t i_pos = up ? first([](float v) { return v > 0.0f; }) : first([](float v) { return v <= 0.0f; });
+    const uint32_t i_neg = up ? first([](float v) { return v >= 0.0f; }) : first([](float v) { return v < 0.0f; });
+    if (up) {
+        if (i_pos < n) best = std::min(best, (double)std::fabs(x(i_pos)));
+        if (i_neg > 0) best = std::min(best, (double)std::fabs(x(i_neg - 1)));
+    } else {                                           // positives first, then zeros, then negatives
+        if (i_pos > 0) best = std::min(best, (double)std::fabs(x(i_pos - 1)));
+        if (i_neg < n) best = std::min(best, (double)std::fabs(x(i_neg)));
+    }
+    return best;
+}
+
+double min_nonzero_x(const xrt_camera& c, int k, bool scan = false)
 {
     const float cu = c.up[k], cr = c.right[k], cc = c.detector[k], co = c.origin[k];
     auto x_of = [&](float v, float u) { return ((cc + cu * v) + cr * u) - co; };
@@ -693,12 +724,22 @@ double min_nonzero_x(const xrt_camera& c, int k)
     auto take = [&](float x) {
         if (x != 0.0f) best = std::min(best, (double)std::fabs(x));
     };
+    // Along one axis x is monotone in the pixel index (pixel_offset and each
+    // rounded f32 operation are monotone), so its smallest nonzero magnitude is
+    // next to its sign change: a bisection per camera instead of a scan of
+    // every row or column (xrt_debug_direction_grid compares the two).
+    const bool finite = std::isfinite(cu) && std::isfinite(cr) && std::isfinite(cc) && std::isfinite(co) &&
+                        std::isfinite(c.pixel_spacing);
     if (cr == 0.0f && c.height <= kMaxScan) {
         const float u0 = pixel_offset(c.pixel_spacing, 0, c.width);
-        for (uint32_t row = 0; row < c.height; ++row) take(x_of(pixel_offset(c.pixel_spacing, row, c.height), u0));
+        auto xr = [&](uint32_t row) { return x_of(pixel_offset(c.pixel_spacing, row, c.height), u0); };
+        if (!scan && finite) best = min_nonzero_monotone(c.height, xr);
+        else for (uint32_t row = 0; row < c.height; ++row) take(xr(row));
     } else if (cu == 0.0f && c.width <= kMaxScan) {
         const float v0 = pixel_offset(c.pixel_spacing, 0, c.height);
-        for (uint32_t col = 0; col < c.width; ++col) take(x_of(v0, pixel_offset(c.pixel_spacing, col, c.width)));
+        auto xc = [&](uint32_t col) { return x_of(v0, pixel_offset(c.pixel_spacing, col, c.width)); };
+        if (!scan && finite) best = min_nonzero_monotone(c.width, xc);
+        else for (uint32_t col = 0; col < c.width; ++col) take(xc(col));
     } else {
         const double ps = std::fabs((double)c.pixel_spacing);
         const int goff = ps > 0.0 ? grid_floor(0.5 * ps * (1.0 - 0x1p-23)) : kNoGrid;
@@ -714,11 +755,11 @@ double min_nonzero_x(const xrt_camera& c, int k)
 // image (make_ray: main.cxx:652-661 and Ray.inl:80-84) is a multiple of it:
 // the two normalisations divide X_k by |X| <= dmax and by ~1, so a nonzero
 // component is >= min|X_k| / (1.001 dmax), a float whose ulp is the grid.
-int direction_grid(const xrt_camera& c, double dmax)
+int direction_grid(const xrt_camera& c, double dmax, bool scan = false)
 {
     int g = kNoGrid;
     for (int k = 0; k < 3; ++k) {
-        const double xmin = min_nonzero_x(c, k);
+        const double xmin = min_nonzero_x(c, k, scan);
         if (xmin > 0.0) g = std::min(g, grid_floor(xmin / (1.001 * dmax)));
     }
     return g;
@@ -2233,6 +2274,15 @@ int xrt_debug_prep_times(xrt_context* ctx, int enable, uint32_t* dst, uint64_t c
     if (rc) return rc;
     const size_t n = std::min<size_t>(capacity, ctx->prep_times_n);
     XRT_HIP(ctx, hipMemcpy(dst, ctx->d_prep_times, n * 2 * sizeof(uint4), hipMemcpyDeviceToHost));
+    return XRT_OK;
+}
+
+int xrt_debug_direction_grid(const xrt_camera* camera, int grids[2])
+{
+    if (!camera || !grids) return XRT_ERR_ARGUMENT;
+    const CullParams cp = make_cull_params(*camera);
+    grids[0] = cp.dir_grid;
+    grids[1] = direction_grid(*camera, cp.dmax, true);
     return XRT_OK;
 }
 

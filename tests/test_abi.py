@@ -361,3 +361,40 @@ def test_image_writers(tmp_path):
     assert np.array_equal(np.frombuffer(data[len(head):], np.uint8).reshape(H, W), lut)
     assert save("no/such/dir.tga", _abi.XRT_IMAGE_TGA)[0] == _abi.XRT_ERR_IO
     assert save("x", 9)[0] == _abi.XRT_ERR_ARGUMENT
+
+
+def test_direction_grid_bisection_equals_scan():
+    """The cull's direction grid per camera: the
+    library's bisection along an axis (x is monotone in the pixel index) equals
+    the scan of every row or column it replaced, on orbit cameras of the dragon
+    and on random cameras with axis-aligned up / right vectors (the scanned
+    branches), 1..8192 pixels a side (host code: no device)."""
+    import numpy as np
+    import simpleraytracing_amd as xrt
+    from simpleraytracing_amd.scenes import orbit_camera
+    lib = _abi.load()
+    grids = (ctypes.c_int * 2)()
+    tris = xrt.load_ply(DRAGON)
+    lo, hi = xrt.mesh_bbox(tris)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    cams = []
+    for size in (7, 1024, 2048, 8192):
+        base = xrt.camera_for_mesh(tris, size, size)
+        cams += [orbit_camera(base, centre, d) for d in (0.0, 0.25, 1.0, 37.0, 90.0, 180.0)]
+    rng = np.random.default_rng(20250302)
+    for _ in range(300):
+        c = xrt.Camera()
+        c.width, c.height = (int(v) for v in rng.integers(1, 8193, 2))
+        for name in ("origin", "detector", "up", "right"):
+            v = rng.normal(0.0, float(rng.choice([1e-3, 1.0, 100.0])), 3).astype(np.float32)
+            if name in ("up", "right"):
+                v[rng.integers(0, 3)] = 0.0                  # the scanned branches
+                if rng.random() < 0.3:
+                    v[rng.integers(0, 3)] = 0.0
+            getattr(c, name)[:] = [float(x) for x in v]
+        c.pixel_spacing = float(np.float32(rng.choice([1e-4, 0.01, 0.3, -0.05])))
+        cams.append(c)
+    for c in cams:
+        assert lib.xrt_debug_direction_grid(ctypes.byref(c), grids) == 0
+        assert grids[0] == grids[1], (list(c.origin), list(c.detector), list(c.up), list(c.right),
+                                      c.pixel_spacing, c.width, c.height, grids[0], grids[1])
