@@ -1423,6 +1423,10 @@ static_assert(kRankCache % 64u == 0u, "whole DMA rounds");
 constexpr uint32_t kAggCells = 256;
 static_assert(!(XRT_PREP_AGG && XRT_PREP_RANK_LDS), "one cell-indexed queue layout at a time");
 static_assert(!XRT_PREP_AGG || XRT_PREP_BUFFER_OPS, "the aggregated commit uses the buffer-op tables");
+// raw buffer atomic OR (no clang builtin for it; the LLVM intrinsic, whose
+// no-return form is selected when the result is unused)
+__device__ int buffer_atomic_or_i32(int v, __amdgpu_buffer_rsrc_t r, int off, int soff, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.atomic.or.i32");
 constexpr int kBufferWord3 = 0x00020000;          // raw buffer resource, gfx9 family (32-bit elements)
 constexpr uint32_t kBufferOut = 0x80000000u;      // an offset past every buffer: no-op access
 
@@ -1502,6 +1506,11 @@ struct BinBuffers {
     // the entries once k_size_lists has placed the lists.  Null: no pairs.
     uint4* pairs;
     uint32_t pairs_cap;
+    // 1: k_prep ORs each pair's box tile mask (span_tile_mask) into its slot's
+    // counter line, and the render stores the misses of a tile outside its
+    // slot's mask without reading the list (exact: no candidate's box meets
+    // it).  0: neither (xrt_context::box_masks).
+    uint32_t box_masks;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -1510,25 +1519,60 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 // SlotDesc, issued back to back as scalar loads and awaited once.  One asm
 // statement, so the compiler cannot put the count load behind a branch that
 // consumes the description (two serial round trips).  slot is wave-uniform.
-__device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot, uint32_t& count, uint32_t& base,
-                                          uint32_t& cap, uint32_t& xy, uint32_t& live)
+// The counter line of a slot: [0] its pair count, [1] its box tile mask (the
+// OR over its pairs of box_tile_mask), both from k_prep's atomics.
+__device__ __forceinline__ void load_slot(const BinBuffers& bins, uint32_t slot, uint32_t& count, uint32_t& mask,
+                                          uint32_t& base, uint32_t& cap, uint32_t& xy, uint32_t& live)
 {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t* count_addr = bins.counts + (size_t)slot * kCounterStride;
     const SlotDesc* desc_addr = bins.desc + slot;
     u32x4 d;
-    uint32_t c;
-    asm volatile("s_load_dword %0, %2, 0x0\n\t"
+    u32x2 c;
+    asm volatile("s_load_dwordx2 %0, %2, 0x0\n\t"
                  "s_load_dwordx4 %1, %3, 0x0\n\t"
                  "s_waitcnt lgkmcnt(0)"
                  : "=&s"(c), "=&s"(d)
                  : "s"(count_addr), "s"(desc_addr)
                  : "memory");
-    count = c;
+    count = c.x;
+    mask = c.y;
     base = d.x;
     cap = d.y;
     xy = d.z;
     live = d.w;
+}
+
+#ifndef XRT_TILE_MASK
+#define XRT_TILE_MASK 1   // k_prep ORs each pair's box tile mask into its slot; the render skips tiles outside it
+#endif
+// The 8x8 tiles a footprint box meets by box_overlaps' test, as a span of
+// strip tile columns and rows (tile column j: pixels 8j .. 8j + 7; tile row i:
+// strip rows 8i .. 8i + 7): column j meets [xmin, xmax] iff j runs from
+// ceil((xmin - 7) / 8) to floor(xmax / 8).  Rounded to nearest, the
+// subtractions cannot cross a multiple of 8 (every integer here is a float),
+// so the computed span never lies inside the exact one; NaN bounds give the
+// widest span.  Packed (first + 4) | (last + 4) << 16 per axis, clamped to
+// [-4, 32000] first.
+__device__ __forceinline__ uint2 box_tile_span(float4 bb, uint32_t row_begin)
+{
+    const float rb = (float)row_begin;
+    auto first = [](float v) { return (uint32_t)(fminf(fmaxf(ceilf(v * 0.125f), -4.0f), 32000.0f) + 4.0f); };
+    auto last = [](float v) { return (uint32_t)(fmaxf(fminf(floorf(v * 0.125f), 32000.0f), -4.0f) + 4.0f); };
+    return make_uint2(first(bb.x - 7.0f) | last(bb.y) << 16, first(bb.z - (rb + 7.0f)) | last(bb.w - rb) << 16);
+}
+
+// The tiles of region (rx, ry) in a box_tile_span: bit 4i + j for the
+// region's tile row i, column j (render_tile's numbering).
+__device__ __forceinline__ uint32_t span_tile_mask(uint2 span, uint32_t rx, uint32_t ry)
+{
+    const int dx = (int)(rx * 4u) + 4, dy = (int)(ry * 4u) + 4;
+    const int j0 = min(max((int)(span.x & 0xFFFFu) - dx, 0), 4), j1 = min(max((int)(span.x >> 16) + 1 - dx, 0), 4);
+    const int i0 = min(max((int)(span.y & 0xFFFFu) - dy, 0), 4), i1 = min(max((int)(span.y >> 16) + 1 - dy, 0), 4);
+    const uint32_t cols = j1 > j0 ? (1u << j1) - (1u << j0) : 0u;
+    const uint32_t rows = i1 > i0 ? (1u << (4 * i1)) - (1u << (4 * i0)) : 0u;
+    return rows & (cols * 0x1111u);
 }
 
 #ifndef XRT_BIN_TIGHT
@@ -1715,7 +1759,8 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             }
         }
         if (bins.counts && bins.clear) {           // the other half, for the set's next frame
-            if (i < bins.clear_regions) bins.clear[(size_t)i * kCounterStride] = 0u;
+            if (i < bins.clear_regions)            // count and tile mask
+                *reinterpret_cast<uint2*>(bins.clear + (size_t)i * kCounterStride) = make_uint2(0u, 0u);
             if (i < sizeof(BinState) / sizeof(uint32_t)) (bins.clear - kCounterStride)[i] = 0u;
         }
     };
@@ -1745,6 +1790,10 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     __shared__ uint32_t s_cum[kPrepWaves][64];     // inclusive prefix of the small cell counts
     __shared__ uint32_t s_qreg[kPrepWaves][kBinQueue];   // passing pairs: region
     __shared__ uint8_t s_qown[kPrepWaves][kBinQueue];    //                owner lane
+#if XRT_TILE_MASK
+    __shared__ uint16_t s_qmask[kPrepWaves][kBinQueue];  //                box tile mask
+    __shared__ uint2 s_tspan[kPrepWaves][64];      // the lane's box_tile_span
+#endif
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool global = false;
@@ -1771,6 +1820,10 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
     s_fp[wave][2][lane] = fp.e2;
     s_fp[wave][3][lane] = fp.bbox;
     s_rect[wave][lane] = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
+#if XRT_TILE_MASK
+    const bool masks = bins.box_masks != 0u;       // kernel-uniform
+    if (masks) s_tspan[wave][lane] = box_tile_span(fp.bbox, p.row_begin);
+#endif
     s_cum[wave][lane] = cum;
     // The slots of the union of the wave's rectangles (mesh-adjacent triangles
     // bin to neighbouring regions), DMAed into LDS under phase 1 when few.
@@ -1867,12 +1920,21 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 #if XRT_PREP_AGG
         if (agg) {
             // (a) per-cell counts in LDS; each pair's offset in its cell
+            // (and per cell the OR of its pairs' tile masks, in s_alc until (b) reads it)
             for (uint32_t c = lane; c < acells; c += 64u) s_acnt[wave][c] = 0u;
+#if XRT_TILE_MASK
+            if (masks)
+                for (uint32_t c = lane; c < acells; c += 64u) s_alc[wave][c] = 0u;
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t q = lane; q < queued; q += 64u)
+            for (uint32_t q = lane; q < queued; q += 64u) {
                 s_qoff[wave][q] = (uint8_t)atomicAdd(&s_acnt[wave][s_qreg[wave][q]], 1u);
+#if XRT_TILE_MASK
+                if (masks) atomicOr(&s_alc[wave][s_qreg[wave][q]], (uint32_t)s_qmask[wave][q]);
+#endif
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1889,6 +1951,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             }
 #pragma unroll
             for (uint32_t k = 0; k < kAggRounds; ++k) cs[k] = cn[k] ? cs[k] : kEmpty;
+#if XRT_TILE_MASK
+            uint32_t cm[kAggRounds];               // the cells' tile masks
+#pragma unroll
+            for (uint32_t k = 0; k < kAggRounds; ++k) cm[k] = masks ? s_alc[wave][k * 64u + lane] : 0u;
+#endif
             bool planned_empty = false;            // pairs for a region the fill plan fills
 #pragma unroll
             for (uint32_t k = 0; k < kAggRounds; ++k) planned_empty |= cs[k] != kEmpty && cs[k] >= bins.tile_slots;
@@ -1906,6 +1973,16 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 clb[k] = bc[0];
                 clc[k] = bc[1];
             }
+#if XRT_TILE_MASK
+            // the masks' atomics last (no return value; issued after the loads and
+            // atomics whose results the wave waits for, they do not delay them)
+            if (masks) {
+#pragma unroll
+                for (uint32_t k = 0; k < kAggRounds; ++k)
+                    buffer_atomic_or_i32((int)cm[k], r_cnt,
+                                         cs[k] != kEmpty ? cs[k] * (kCounterStride * 4u) + 4u : kBufferOut, 0, 0);
+            }
+#endif
             if (count_only) {                       // the sizing pass: counts only
                 if (bins.pairs) {                   // (device sizing: and the pairs)
 #pragma unroll
@@ -2019,10 +2096,25 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
                 lbase[b] = bc[0];
                 lcap[b] = bc[1];
             }
+#if XRT_TILE_MASK
+            if (masks) {
+#pragma unroll
+                for (uint32_t b = 0; b < kBinBatch; ++b) {   // the pairs' tile masks, last (no return value)
+                    const uint32_t q = base + b * 64u + lane;
+                    buffer_atomic_or_i32((int)s_qmask[wave][q < kBinQueue ? q : 0u], r_cnt,
+                                         reg[b] != kEmpty ? reg[b] * (kCounterStride * 4u) + 4u : kBufferOut, 0, 0);
+                }
+            }
+#endif
 #else
 #pragma unroll
             for (uint32_t b = 0; b < kBinBatch; ++b) {
                 slot[b] = reg[b] != kEmpty ? atomicAdd(&bins.counts[(size_t)reg[b] * kCounterStride], 1u) : 0u;
+#if XRT_TILE_MASK
+                if (masks && reg[b] != kEmpty)
+                    atomicOr(&bins.counts[(size_t)reg[b] * kCounterStride + 1u],
+                             (uint32_t)s_qmask[wave][min(base + b * 64u + lane, kBinQueue - 1u)]);
+#endif
                 const uint2 bc = reg[b] != kEmpty && count_only == 0u
                                      ? *reinterpret_cast<const uint2*>(bins.desc + reg[b]) : make_uint2(0u, 0u);
                 lbase[b] = bc.x;
@@ -2077,6 +2169,9 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
             // the cached slot's index, or the region
             s_qreg[wave][q] = cached ? (ry - uy0) * uw + (rx - ux0) : ry * bins.regions_x + rx;
             s_qown[wave][q] = (uint8_t)owner;
+#if XRT_TILE_MASK
+            if (masks) s_qmask[wave][q] = (uint16_t)span_tile_mask(s_tspan[wave][owner], rx, ry);
+#endif
         }
         queued += (uint32_t)__popcll(m);
     };
@@ -2368,8 +2463,8 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
 {
     const uint32_t lane = threadIdx.x & 63u;
     // the slot's count (k_prep) and description (host): two scalar loads in flight together
-    uint32_t n_local, d_base, d_cap, d_xy, d_live;
-    load_slot(bins, slot, n_local, d_base, d_cap, d_xy, d_live);
+    uint32_t n_local, box_mask, d_base, d_cap, d_xy, d_live;
+    load_slot(bins, slot, n_local, box_mask, d_base, d_cap, d_xy, d_live);
     const uint32_t reg_x = d_xy & 0xFFFFu, reg_y = d_xy >> 16;
     const RegionEntry* __restrict__ local = bins.list + d_base;
     const RegionEntry* __restrict__ glob = bins.global_list;
@@ -2400,7 +2495,15 @@ __device__ __forceinline__ void render_tile(RecStage& st, const TriRec* __restri
     }
     // a tile the geometry's tile plan found without survivors: its misses,
     // without reading the region's list (exact: SlotDesc::live)
-    const bool planned_dead = !kSigned && bins.tile_plan && split == kSplitNone && !((d_live >> tile) & 1u);
+    // A tile no candidate's footprint box meets (the region's box tile mask,
+    // k_prep's OR over its pairs; the global list's entries are not in it):
+    // no candidate can pass its tile test -- its misses, the same way.  Both
+    // halves of a split tile skip alike.
+    const bool planned_dead = (!kSigned && bins.tile_plan && split == kSplitNone && !((d_live >> tile) & 1u))
+#if XRT_TILE_MASK
+                              || (bins.box_masks && n_glob == 0u && !((box_mask >> tile) & 1u))
+#endif
+        ;
 
     float dx = 1.0f, dy = 0.0f, dz = 0.0f;
     float sx = 1.0f, sy = 0.0f, sz = 0.0f;         // kSigned: the once-normalised direction

@@ -324,6 +324,12 @@ struct xrt_context {
     uint64_t slot_pool = 0;            // entries of the compact lists
     uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
     uint64_t motion_pool_forced = 0;   // test hook XRT_MOTION_POOL: that many entries, never grown
+    // Box tile masks (BinBuffers::box_masks; XRT_BOX_MASKS): 0 (default)
+    // never, 1 in the host-sized frames of meshes under kPrepBigMesh
+    // triangles, 2 in every binned frame.  Exact either way; measured a wash
+    // (DESIGN.md "Box tile masks"): the renders' dispatches shrink, k_prep's
+    // grow by about as much, and the step does not move beyond box-to-box noise.
+    int box_masks = 0;
     bool compact = false;              // compact_layout is valid for bin_key
     size_t bin_force_cap = 0;          // test hook (xrt_set_bin_capacity)
     // Fill plan of the current geometry (bin_key): the compact layout's
@@ -1141,6 +1147,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         else if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
         bins.tile_plan = compact && fill_ok && !reuse && !sizing && ctx->plan_valid && ctx->tile_plan_enabled &&
                          ctx->tile_plan_state == 1 ? 1u : 0u;
+        bins.box_masks = ctx->box_masks == 2 || (ctx->box_masks == 1 && ctx->num_tris < kPrepBigMesh) ? 1u : 0u;
         if (sizing) prof_mark(ctx, "fixed layout upload");
         // the fill plan's test hook (every region planned empty) is checked every frame
         arm_plan_check(fs, n_regions, bins, false, ctx->fill_plan == 2);
@@ -1167,6 +1174,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.split_slots = 0u;
         bins.tile_plan = 0u;
         bins.plan_miss = nullptr;
+        bins.box_masks = ctx->box_masks == 2 ? 1u : 0u;
         RegionEntry* const list = bins.list;
         bins.list = nullptr;                           // the count-only pass, appending its pairs
         bins.pairs = fs.pairs;
@@ -1739,6 +1747,7 @@ int xrt_create(int device, xrt_context** out)
     ctx->sizing_profile = sp ? std::atoi(sp) : 0;
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
     if (const char* mp = std::getenv("XRT_MOTION_POOL")) ctx->motion_pool_forced = std::strtoull(mp, nullptr, 10);
+    if (const char* bm = std::getenv("XRT_BOX_MASKS")) ctx->box_masks = std::atoi(bm);
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
         n_cu = 256;

@@ -508,6 +508,78 @@ def test_moving_camera_pool_overflow_exact(dragon, monkeypatch):
     assert g["reused"] >= 9 and g["overflows"] > 0, g
 
 
+def _box_masks_case(name, dragon):
+    if name == "dragon-strip":
+        return dragon, 1000, 777, 13, 700
+    if name == "soup":
+        return synthetic_soup(seed=3, n=3000), 300, 200, 0, None
+    if name == "corner":
+        return corner_soup(), 33, 31, 0, None
+    return tiled_mesh(dragon, 3), 1024, 1024, 0, None
+
+
+@pytest.mark.parametrize("model", ["attenuation", "signed"])
+@pytest.mark.parametrize("name", ["dragon-strip", "soup", "corner", "tiled3-1024"])
+def test_box_masks_exact(dragon, monkeypatch, name, model):
+    """Box tile masks (BinBuffers::box_masks) forced on (XRT_BOX_MASKS=2) and
+    off (0): a tile outside its region's mask stores its misses without reading
+    the list.  Both frames -- image, L-buffer, u8, statistics -- are
+    bit-identical to a brute-force render, in both models, over a row strip
+    starting off the tile grid (row 13), odd frame sizes and a mesh of 206 K
+    triangles."""
+    tris, W, H, r0, r1 = _box_masks_case(name, dragon)
+    cam = xrt.camera_for_mesh(tris, W, H)
+    outs = {}
+    for mode in ("2", "0", "brute"):
+        monkeypatch.setenv("XRT_BOX_MASKS", "0" if mode == "brute" else mode)
+        with xrt.Context(0) as c:
+            if model == "signed":
+                c.set_model(xrt.XRT_MODEL_SIGNED, 0.1037)
+            c.set_kernel(xrt.XRT_KERNEL_BRUTE if mode == "brute" else xrt.XRT_KERNEL_BINNED)
+            c.upload_mesh(tris)
+            # the sizing frame, then a steady one (the signed model: whole frames)
+            outs[mode] = [c.render_signed(cam) if model == "signed" else c.render_rows(cam, r0, r1) for _ in range(2)]
+    for mode in ("2", "0"):
+        for k in range(2):
+            got, ref = outs[mode][k], outs["brute"][0]
+            for x, y in zip(got[:3], ref[:3]):
+                assert np.array_equal(bits(x), bits(y)), (mode, k)
+            for f in ("rays", "hits", "hit_rays", "odd_rays", "max_hits"):
+                assert getattr(got[3], f) == getattr(ref[3], f), (mode, k, f)
+
+
+def test_box_masks_moving_camera_exact(dragon, monkeypatch):
+    """Box tile masks forced on in a moving camera's device-sized frames (the
+    count pass ORs the masks; the default leaves them off there): every frame of
+    a sweep, through device planes on two streams, equals brute force."""
+    import torch
+    monkeypatch.setenv("XRT_BOX_MASKS", "2")
+    W, H = 640, 480
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    cams = [orbit_camera(base, centre, 0.75 * k) for k in range(8)]
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    with xrt.Context(0) as brute:
+        brute.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        brute.upload_mesh(dragon)
+        refs = [brute.render_rows(c) for c in cams]
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        outs = [(torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+                 torch.empty(W * H, dtype=torch.uint8, device=dev)) for _ in cams]
+        for k, cam in enumerate(cams):
+            c.render_rows_device(cam, 0, H, *(t.data_ptr() for t in outs[k]), streams[k % 2].cuda_stream)
+        torch.cuda.synchronize(dev)
+        for k in range(len(cams)):
+            for x, y in zip(outs[k], refs[k][:3]):
+                assert np.array_equal(bits(x.cpu().numpy()), bits(y)), k
+        g = c.geometry_counters()
+    assert g["reused"] >= 6, g
+
+
 @pytest.mark.parametrize("devices", [[0, 0]])
 def test_multi_strips_orbit_exact(dragon, devices):
     """xrt_render_rows_multi under a moving camera: its contexts size
