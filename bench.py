@@ -80,6 +80,8 @@ def parse():
                          "turning DEG degrees per frame (reported under `orbit`, never `value`); none: no legs")
     ap.add_argument("--no-tile-plan-leg", action="store_true",
                     help="skip the opt-in tile plan's leg after the timed region (counter runs: its renders differ)")
+    ap.add_argument("--orbit-ramp-ms", type=float, default=30.0,
+                    help="untimed moving frames before each orbit leg's timed ones, ms of sustained load")
     ap.add_argument("--orbit-frames", type=int, default=60,
                     help="timed frames per orbit leg (after 4 untimed ones)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1088,31 +1090,60 @@ def main():
         oplanes = [(torch.zeros(W * H, dtype=torch.float32, device=dev), torch.zeros(W * H, dtype=torch.float32, device=dev),
                     torch.zeros(W * H, dtype=torch.uint8, device=dev), s_f) for _, _, _, s_f in planes_of]
         optrs = [(a.data_ptr(), b.data_ptr(), c.data_ptr(), s_f.cuda_stream) for a, b, c, s_f in oplanes]
+        fplanes = [(torch.empty(W * H, dtype=torch.float32, device=dev), torch.empty(W * H, dtype=torch.float32, device=dev),
+                    torch.empty(W * H, dtype=torch.uint8, device=dev), s_f) for _, _, _, s_f in planes_of]
+        fptrs = [(a.data_ptr(), b.data_ptr(), c.data_ptr(), s_f.cuda_stream) for a, b, c, s_f in fplanes]
         for deg in args.orbit_legs:
-            cams_o = [orbit_camera(cam, centre, k * deg) for k in range(n_warm + n_timed)]
+            # untimed: the sweep's frames before angle n_warm * deg, as many as
+            # --orbit-ramp-ms of sustained load takes at twice the main loop's step
+            # (the clock ramp, DESIGN.md "Clock ramp"); timed: the n_timed frames
+            # from angle n_warm * deg on (the angles of the round-6 legs)
+            n_ramp = max(int(args.orbit_ramp_ms / (2.0 * orbit["fixed_camera_ms_per_step"])), 0)
+            k0 = n_warm + n_ramp
+            cams_o = [orbit_camera(cam, centre, (k - n_ramp) * deg) for k in range(k0 + n_timed)]
+            # a fresh context beside the bench's: it shares the device's prep and
+            # host streams (libxrt's acquire_streams), so it adds no hardware
+            # queue (DESIGN.md "Moving camera")
             with xrt.Context(device_index) as oc:
                 oc.set_kernel({"auto": xrt.XRT_KERNEL_AUTO, "brute": xrt.XRT_KERNEL_BRUTE,
                                "tiled": xrt.XRT_KERNEL_TILED, "binned": xrt.XRT_KERNEL_BINNED}[args.kernel])
                 oc.upload_mesh(tris)
-                for k in range(n_warm):
+                for k in range(k0):
                     img_k, lb_k, u8_k, s_k = optrs[k % inflight]
                     oc.render_rows_device(cams_o[k], 0, H, img_k, lb_k, u8_k, s_k)
-                torch.cuda.synchronize(dev)
                 g0, q0 = oc.geometry_counters(), oc.pipeline_counters()
                 t_o = time.perf_counter()
-                for k in range(n_warm, n_warm + n_timed):
+                for k in range(k0, k0 + n_timed):
                     img_k, lb_k, u8_k, s_k = optrs[k % inflight]
                     oc.render_rows_device(cams_o[k], 0, H, img_k, lb_k, u8_k, s_k)
                 enq = time.perf_counter() - t_o
                 torch.cuda.synchronize(dev)
                 el = time.perf_counter() - t_o
                 g1, q1 = oc.geometry_counters(), oc.pipeline_counters()
+                # the same context at the same clocks, the camera held still: a few
+                # untimed frames (the still camera's list sizing, frames prepared
+                # ahead), then n_timed timed ones -- the moving camera's cost per se
+                cam_f = cams_o[-1]
+                for j in range(8):
+                    img_k, lb_k, u8_k, s_k = fptrs[j % inflight]
+                    oc.render_rows_device(cam_f, 0, H, img_k, lb_k, u8_k, s_k)
+                torch.cuda.synchronize(dev)
+                gf0, qf0 = oc.geometry_counters(), oc.pipeline_counters()
+                t_f = time.perf_counter()
+                for j in range(n_timed):
+                    img_k, lb_k, u8_k, s_k = fptrs[j % inflight]
+                    oc.render_rows_device(cam_f, 0, H, img_k, lb_k, u8_k, s_k)
+                torch.cuda.synchronize(dev)
+                el_f = time.perf_counter() - t_f
+                gf1, qf1 = oc.geometry_counters(), oc.pipeline_counters()
+                fixed_paths = {k_: v_ - gf0[k_] for k_, v_ in gf1.items() if v_ != gf0[k_]}
+                fixed_paths.update({k_: v_ - qf0[k_] for k_, v_ in qf1.items() if v_ != qf0[k_]})
                 exact = True
                 scratch = (torch.empty(W * H, dtype=torch.float32, device=dev),
                            torch.empty(W * H, dtype=torch.float32, device=dev),
                            torch.empty(W * H, dtype=torch.uint8, device=dev))
                 for j in range(inflight):
-                    k = n_warm + n_timed - 1 - j
+                    k = k0 + n_timed - 1 - j
                     with xrt.Context(device_index) as ref_ctx:       # a fresh context's synchronous render
                         ref_ctx.set_kernel(xrt.XRT_KERNEL_BINNED)
                         ref_ctx.upload_mesh(tris)
@@ -1122,17 +1153,26 @@ def main():
             if not exact:
                 raise SystemExit(f"bench.py: an orbit frame ({deg:g} deg per frame) differs from its synchronous render")
             ms = el / n_timed * 1e3
+            ms_f = el_f / n_timed * 1e3
             orbit[f"deg_{deg:g}"] = {
                 "ms_per_step": ms, "value": W * H * n_timed / el / 1e6, "frames": n_timed, "warmup": n_warm,
-                "vs_fixed_camera": ms / orbit["fixed_camera_ms_per_step"],
+                "ramp_frames": n_ramp, "fixed_camera_same_context_ms_per_step": ms_f,
+                "fixed_camera_same_context_paths": fixed_paths,
+                "vs_fixed_camera": ms / ms_f,
+                "vs_main_loop_step": ms / orbit["fixed_camera_ms_per_step"],
                 "sizings": g1["sizings"] - g0["sizings"], "reused_lists": g1["reused"] - g0["reused"],
                 "plan_misses": g1["plan_misses"] - g0["plan_misses"], "overflows": g1["overflows"] - g0["overflows"],
                 "host_waits": q1["host_waits"] - q0["host_waits"], "last_frames_bit_exact": bool(exact),
                 "host_enqueue_ms_per_step": enq / n_timed * 1e3}
-        del oplanes
-        orbit["what"] = ("a fresh context per leg; the camera turns deg degrees per frame about the mesh centre "
+        del oplanes, fplanes
+        orbit["what"] = ("a fresh context per leg (beside the bench's, on the device's shared streams); the camera "
+                         "turns deg degrees per frame about the mesh centre "
                          "(scenes.orbit_camera); one xrt_render_rows_device call per frame, frames in flight as in "
-                         "the main loop; each frame's k_prep bins its own camera; counters over the timed frames")
+                         "the main loop; each frame's k_prep bins its own camera; untimed frames of the sweep until "
+                         "--orbit-ramp-ms of load (clock ramp), then `frames` timed ones; then, in the same context, "
+                         "the last camera held still for 8 untimed and `frames` timed frames "
+                         "(fixed_camera_same_context_ms_per_step): vs_fixed_camera = the moving step / that step; "
+                         "vs_main_loop_step = the moving step / the main loop's; counters over the timed moving frames")
 
     # untimed: the gathered frame against rank 0's own render of the whole frame
     gather = None

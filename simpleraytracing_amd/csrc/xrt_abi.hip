@@ -312,7 +312,8 @@ struct xrt_context {
     FrameSet sets[kFrameSets];
     int next_set = 0;
     FrameSet* last_set = nullptr;      // set of the last enqueued frame
-    hipStream_t prep_stream = nullptr;
+    hipStream_t prep_stream = nullptr;    // the device's, shared with its other contexts (acquire_streams)
+    bool owns_streams = false;         // holds a reference to them
     size_t prep_lds = 0;               // dynamic LDS of a k_prep launch (kPrepLds in all)
 
     // Launch layouts of the region grid (SlotLayout): the fixed-capacity one
@@ -534,6 +535,53 @@ static std::string& g_create_error = *new std::string();
 // xrt_destroy's phases, ms (xrt_debug_destroy_ms): [0] waiting for the
 // context's work, [1] device frees, [2] pinned host frees, [3] streams and events
 static double g_destroy_ms[4] = {};
+
+// The prep and host streams are shared by every context of one device in the
+// process (reference-counted; the last context's destroy destroys them).  A
+// process gets GPU_MAX_HW_QUEUES hardware queues (4 by default) and HIP shares
+// one between streams past that: a second context with streams of its own
+// beside a caller's two render streams put its prep stream on a render
+// stream's queue, where a frame's k_prep waits for the render queued before it
+// and the next render for that k_prep -- preparation and render serialised
+// (2048^2: 32 -> 58 us a still frame, 51 -> 69 us a moving one; DESIGN.md
+// "Moving camera").  Shared, contexts add no queue: their k_preps serialise on
+// the device's prep stream, which they would on one queue anyway.
+struct DeviceStreams {
+    hipStream_t prep = nullptr, host = nullptr;
+    int refs = 0;
+};
+static std::mutex& g_streams_mu = *new std::mutex();
+static std::vector<DeviceStreams>& g_streams = *new std::vector<DeviceStreams>();
+
+bool acquire_streams(int device, hipStream_t& prep, hipStream_t& host)
+{
+    std::lock_guard<std::mutex> lock(g_streams_mu);
+    if ((size_t)device >= g_streams.size()) g_streams.resize((size_t)device + 1);
+    DeviceStreams& d = g_streams[(size_t)device];
+    if (d.refs == 0) {
+        if (hipStreamCreateWithFlags(&d.prep, hipStreamNonBlocking) != hipSuccess) return false;
+        if (hipStreamCreateWithFlags(&d.host, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipStreamDestroy(d.prep);
+            d.prep = nullptr;
+            return false;
+        }
+    }
+    ++d.refs;
+    prep = d.prep;
+    host = d.host;
+    return true;
+}
+
+void release_streams(int device)
+{
+    std::lock_guard<std::mutex> lock(g_streams_mu);
+    DeviceStreams& d = g_streams[(size_t)device];
+    if (--d.refs == 0) {
+        (void)hipStreamDestroy(d.prep);
+        (void)hipStreamDestroy(d.host);
+        d.prep = d.host = nullptr;
+    }
+}
 
 // AUTO switches from TILED to BINNED past this many footprint-box tests
 // (T x regions) per frame (DESIGN.md "Kernels").
@@ -1755,7 +1803,8 @@ int xrt_create(int device, xrt_context** out)
     // The prep stream at the default queue priority: frames are prepared ahead
     // of their renders (the highest and the lowest priority measured the same).
     bool ok = hipEventCreate(&ctx->ev_begin) == hipSuccess && hipEventCreate(&ctx->ev_end) == hipSuccess;
-    ok = ok && hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && acquire_streams(device, ctx->prep_stream, ctx->host_stream);
+    ctx->owns_streams = ok;
     hipFuncAttributes prep_attr = {};
     ok = ok && hipFuncGetAttributes(&prep_attr, reinterpret_cast<const void*>(k_prep)) == hipSuccess;
     // k_prep's own LDS must fit the cap (else more than XRT_PREP_PER_CU would not fit beside the render)
@@ -1774,8 +1823,7 @@ int xrt_create(int device, xrt_context** out)
     // the host-buffer entry points' stream, pinned D2H ring and copy threads
     int threads = kD2HThreads;
     if (const char* th = std::getenv("XRT_D2H_THREADS")) threads = std::max(0, std::atoi(th));
-    ok = ok && hipStreamCreateWithFlags(&ctx->host_stream, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&ctx->host_render_done, hipEventDisableTiming) == hipSuccess &&
+    ok = ok && hipEventCreateWithFlags(&ctx->host_render_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&ctx->sizing_ev, hipEventDisableTiming) == hipSuccess &&
          hipHostMalloc((void**)&ctx->h_sizing, kSizingScratch, hipHostMallocDefault) == hipSuccess;
     if (ok) ctx->h_sizing_cap = kSizingScratch;
@@ -1854,8 +1902,7 @@ void xrt_destroy(xrt_context* ctx)
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_sizing) (void)hipHostFree(ctx->h_sizing);
     lap(2);
-    if (ctx->prep_stream) (void)hipStreamDestroy(ctx->prep_stream);
-    if (ctx->host_stream) (void)hipStreamDestroy(ctx->host_stream);
+    if (ctx->owns_streams) release_streams(ctx->device);     // the device's shared streams
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->stage_ev)
         if (e) (void)hipEventDestroy(e);

@@ -548,6 +548,68 @@ def test_box_masks_exact(dragon, monkeypatch, name, model):
                 assert getattr(got[3], f) == getattr(ref[3], f), (mode, k, f)
 
 
+def test_contexts_share_device_streams_exact(dragon):
+    """Contexts of one device share its prep and host streams (acquire_streams):
+    two contexts interleaving frames in flight on two caller streams -- one
+    camera still, the other moving -- then the first destroyed while the second
+    keeps rendering and a third joins: every frame equals brute force."""
+    import torch
+    W, H = 512, 384
+    lo, hi = xrt.mesh_bbox(dragon)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    base = xrt.camera_for_mesh(dragon, W, H)
+    cams = [orbit_camera(base, centre, 1.5 * k) for k in range(6)]
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    with xrt.Context(0) as brute:
+        brute.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        brute.upload_mesh(dragon)
+        ref_still = brute.render_rows(base)
+        refs = [brute.render_rows(c) for c in cams]
+
+    def make():
+        c = xrt.Context(0)
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(dragon)
+        return c
+
+    def planes():
+        return (torch.empty(W * H, device=dev), torch.empty(W * H, device=dev),
+                torch.empty(W * H, dtype=torch.uint8, device=dev))
+
+    def check(out, ref, what):
+        for x, y in zip(out, ref[:3]):
+            assert np.array_equal(bits(x.cpu().numpy()), bits(y)), what
+
+    a, b = make(), make()
+    outs_a = [planes() for _ in cams]
+    outs_b = [planes() for _ in cams]
+    for k, cam in enumerate(cams):
+        a.render_rows_device(base, 0, H, *(t.data_ptr() for t in outs_a[k]), streams[k % 2].cuda_stream)
+        b.render_rows_device(cam, 0, H, *(t.data_ptr() for t in outs_b[k]), streams[(k + 1) % 2].cuda_stream)
+    torch.cuda.synchronize(dev)
+    for k in range(len(cams)):
+        check(outs_a[k], ref_still, ("a", k))
+        check(outs_b[k], refs[k], ("b", k))
+    a.close()                                   # b keeps the device's streams
+    c = make()
+    for k, cam in enumerate(cams):
+        b.render_rows_device(cam, 0, H, *(t.data_ptr() for t in outs_b[k]), streams[k % 2].cuda_stream)
+        c.render_rows_device(base, 0, H, *(t.data_ptr() for t in outs_a[k]), streams[(k + 1) % 2].cuda_stream)
+    torch.cuda.synchronize(dev)
+    for k in range(len(cams)):
+        check(outs_b[k], refs[k], ("b after a closed", k))
+        check(outs_a[k], ref_still, ("c", k))
+    for k in (0, 3):                            # host-buffer calls on the shared host stream
+        got_b, got_c = b.render_rows(cams[k]), c.render_rows(base)
+        for x, y in zip(got_b[:3], refs[k][:3]):
+            assert np.array_equal(bits(x), bits(y)), ("b host", k)
+        for x, y in zip(got_c[:3], ref_still[:3]):
+            assert np.array_equal(bits(x), bits(y)), ("c host", k)
+    b.close()
+    c.close()
+
+
 def test_box_masks_moving_camera_exact(dragon, monkeypatch):
     """Box tile masks forced on in a moving camera's device-sized frames (the
     count pass ORs the masks; the default leaves them off there): every frame of
