@@ -33,7 +33,9 @@ struct BinState {
     unsigned int overflow;      // some region count exceeded the list capacity
     unsigned int cursor;        // a device-sized frame's pool cursor (k_size_lists)
     unsigned int pairs;         // a device-sized frame's appended pairs (BinBuffers::pairs)
-    unsigned int pad[3];
+    unsigned int tile_slots;    // a device-planned frame's tile regions (k_size_lists; BinBuffers::dev_plan)
+    unsigned int fill_slots;    //                          and its empty ones
+    unsigned int pad;
 };
 
 // Host-computed bounds for the cull derivation (DESIGN.md "Tile cull").
@@ -1506,6 +1508,11 @@ struct BinBuffers {
     // the entries once k_size_lists has placed the lists.  Null: no pairs.
     uint4* pairs;
     uint32_t pairs_cap;
+    // 1: the render's tile regions number BinState::tile_slots (a device fill
+    // plan, k_size_lists: the slots with candidates first, then one fill
+    // workgroup per empty region); its grid covers every region as tiles and
+    // the workgroups past the plan's tiles and fills leave at once.
+    uint32_t dev_plan;
     // 1: k_prep ORs each pair's box tile mask (span_tile_mask) into its slot's
     // counter line, and the render stores the misses of a tile outside its
     // slot's mask without reading the list (exact: no candidate's box meets
@@ -2248,11 +2255,31 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const float* __restrict__
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ counts, const SlotDesc* __restrict__ fixed,
                                                    SlotDesc* __restrict__ out, uint32_t n_slots, uint32_t pool,
-                                                   BinState* __restrict__ bs)
+                                                   BinState* __restrict__ bs, SlotDesc* __restrict__ plan_desc,
+                                                   uint32_t* __restrict__ plan_counts)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = s < n_slots ? counts[(size_t)s * kCounterStride] : 0u;
+    // The device fill plan (BinBuffers::dev_plan; plan_desc null: none): the
+    // render's layout lists the slots with candidates first (tiles), then the
+    // empty ones (one fill workgroup each) -- empty only when the global list
+    // is empty too.  Counts (and box tile masks) follow into that order.
+    uint32_t pos = 0;
+    if (plan_desc) {
+        const bool empty = c == 0u && as_const(bs)->global_count == 0u;
+        const unsigned long long m_tile = __ballot(s < n_slots && !empty), m_fill = __ballot(s < n_slots && empty);
+        uint32_t t0 = 0, f0 = 0;
+        if (lane == 0u) {
+            if (m_tile) t0 = atomicAdd(&bs->tile_slots, (uint32_t)__popcll(m_tile));
+            if (m_fill) f0 = atomicAdd(&bs->fill_slots, (uint32_t)__popcll(m_fill));
+        }
+        t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t0);
+        f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)f0);
+        const unsigned long long mine = empty ? m_fill : m_tile;
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        pos = empty ? n_slots - 1u - (f0 + r) : t0 + r;
+    }
     uint32_t incl = c;
 #pragma unroll
     for (uint32_t off = 1; off < 64u; off <<= 1) {
@@ -2271,7 +2298,13 @@ __global__ __launch_bounds__(256) void k_size_lists(uint32_t* __restrict__ count
     if (s < n_slots) {
         const uint32_t base = base0 + incl - c;
         const uint32_t cap = lost || base >= pool ? 0u : min(c, pool - base);
-        out[s] = SlotDesc{min(base, pool), cap, fixed[s].xy, 0xFFFFu};
+        const SlotDesc d = SlotDesc{min(base, pool), cap, fixed[s].xy, 0xFFFFu};
+        out[s] = d;
+        if (plan_desc) {
+            plan_desc[pos] = d;
+            *reinterpret_cast<uint2*>(plan_counts + (size_t)pos * kCounterStride) =
+                make_uint2(c, counts[(size_t)s * kCounterStride + 1u]);
+        }
     }
 }
 
@@ -2660,7 +2693,10 @@ __device__ __forceinline__ void render_binned(RecStage* st, const TriRec* __rest
                   "a workgroup's waves render tiles of one region");
     constexpr uint32_t kBlocksPerRegion = kWavesPerRegion / kTileWaves;
     const uint64_t t_start = block_start_stamp();
-    const uint32_t tile_blocks = bins.tile_slots * kBlocksPerRegion;
+    // a device-planned frame (BinBuffers::dev_plan, a moving camera): its tile
+    // regions' number from k_size_lists
+    const uint32_t tile_slots = !kSigned && !kHits && bins.dev_plan ? as_const(bs)->tile_slots : bins.tile_slots;
+    const uint32_t tile_blocks = tile_slots * kBlocksPerRegion;
     const uint32_t split_slots = kSigned || !kCanSplit ? 0u : bins.split_slots;
     const uint32_t tile_end = tile_blocks + split_slots * kBlocksPerRegion;   // the tile regions' workgroups
     const uint32_t wave = wave_in_block();
@@ -2668,7 +2704,8 @@ __device__ __forceinline__ void render_binned(RecStage* st, const TriRec* __rest
     WaveStats ws = {};
     uint32_t cand = 0;
     if (!kSigned && blockIdx.x >= tile_end) {      // a planned-empty region (workgroup-uniform)
-        const uint32_t slot = bins.tile_slots + (blockIdx.x - tile_end);
+        const uint32_t slot = tile_slots + (blockIdx.x - tile_end);
+        if (!kHits && bins.dev_plan && slot >= bins.regions_x * bins.regions_y) return;   // past the device plan
         // statistics records: kBlocksPerRegion per wave, after the tile waves' (16 per region)
         const uint32_t rec0 =
             tile_blocks * kTileWaves + ((blockIdx.x - tile_end) * kTileWaves + wave) * kBlocksPerRegion;

@@ -178,6 +178,10 @@ struct FrameSet {
     size_t dyn_desc_cap = 0;
     uint4* pairs = nullptr;            // its (slot, index, triangle) pairs (k_prep's count pass)
     size_t pairs_cap = 0;
+    SlotDesc* plan_desc = nullptr;     // its render layout under the device fill plan (tiles first, then fills)
+    size_t plan_desc_cap = 0;
+    uint32_t* plan_counts = nullptr;   // and its counter lines in that order
+    size_t plan_counts_cap = 0;
     bool lazy_flags = false;           // plan_flag armed for a frame launched without reading it
     hipEvent_t ready = nullptr;        // k_prep complete (prep stream)
     hipEvent_t done = nullptr;         // render end (a stop event on the render's dispatch)
@@ -297,6 +301,9 @@ struct PendingFrame {
         uint32_t n_slots = 0, pool = 0;
         const SlotDesc* fixed = nullptr;
         uint32_t* flag = nullptr;
+        uint32_t* counts = nullptr;        // the count pass's counter lines (the base layout's order)
+        SlotDesc* plan_desc = nullptr;     // the device fill plan's layout (null: none)
+        uint32_t* plan_counts = nullptr;
     } dev_size;
     HostClock::time_point t_call;
 };
@@ -325,6 +332,7 @@ struct xrt_context {
     uint64_t slot_pool = 0;            // entries of the compact lists
     uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
     uint64_t motion_pool_forced = 0;   // test hook XRT_MOTION_POOL: that many entries, never grown
+    bool device_fill = true;           // moving frames render over the device fill plan (XRT_DEVICE_FILL=0: off)
     // Box tile masks (BinBuffers::box_masks; XRT_BOX_MASKS): 0 (default)
     // never, 1 in the host-sized frames of meshes under kPrepBigMesh
     // triangles, 2 in every binned frame.  Exact either way; measured a wash
@@ -1217,6 +1225,11 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
         if ((rc = ensure(ctx, fs.dyn_desc, fs.dyn_desc_cap, n_regions))) return rc;
         if ((rc = ensure(ctx, fs.pairs, fs.pairs_cap, ctx->motion_pool))) return rc;
+        // the device fill plan (not for the transit layouts, whose tiles follow a host plan)
+        const bool dev_plan = ctx->device_fill && out.packed == 0u;
+        if (dev_plan && ((rc = ensure(ctx, fs.plan_desc, fs.plan_desc_cap, n_regions)) ||
+                         (rc = ensure(ctx, fs.plan_counts, fs.plan_counts_cap, (size_t)n_regions * kCounterStride))))
+            return rc;
         const uint32_t pool = (uint32_t)std::min<uint64_t>(ctx->motion_pool, 0xFFFFFFFFull);
         bins.tile_slots = n_regions;
         bins.split_slots = 0u;
@@ -1240,8 +1253,15 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         pf.dev_size.pool = pool;
         pf.dev_size.fixed = bins.desc;
         pf.dev_size.flag = flag;
+        pf.dev_size.counts = bins.counts;
+        pf.dev_size.plan_desc = dev_plan ? fs.plan_desc : nullptr;
+        pf.dev_size.plan_counts = dev_plan ? fs.plan_counts : nullptr;
         bins.list = list;
-        bins.desc = fs.dyn_desc;
+        bins.desc = dev_plan ? fs.plan_desc : fs.dyn_desc;
+        if (dev_plan) {                                // the render reads the plan's order
+            bins.counts = fs.plan_counts;
+            bins.dev_plan = 1u;
+        }
         bins.pairs = nullptr;
         bins.clear = nullptr;
     }
@@ -1432,8 +1452,8 @@ int launch_frame(xrt_context* ctx, PendingFrame& pf)
     }
     if (pf.dev_size.on) {                          // a device-sized frame's lists (prepare_frame)
         const PendingFrame::DevSize& d = pf.dev_size;
-        hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, stream, pf.bins.counts, d.fixed,
-                           fs.dyn_desc, d.n_slots, d.pool, bin_ctl);
+        hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, stream, d.counts, d.fixed,
+                           fs.dyn_desc, d.n_slots, d.pool, bin_ctl, d.plan_desc, d.plan_counts);
         XRT_HIP(ctx, hipGetLastError());
         const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((d.pool + 255u) / 256u, 2048u);
         hipLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, stream, (const uint4*)fs.pairs,
@@ -1796,6 +1816,7 @@ int xrt_create(int device, xrt_context** out)
     if (const char* sm = std::getenv("XRT_SPLIT_MIN")) ctx->split_min = (uint32_t)std::strtoul(sm, nullptr, 10);
     if (const char* mp = std::getenv("XRT_MOTION_POOL")) ctx->motion_pool_forced = std::strtoull(mp, nullptr, 10);
     if (const char* bm = std::getenv("XRT_BOX_MASKS")) ctx->box_masks = std::atoi(bm);
+    if (const char* df = std::getenv("XRT_DEVICE_FILL")) ctx->device_fill = std::atoi(df) != 0;
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
@@ -1881,6 +1902,10 @@ void xrt_destroy(xrt_context* ctx)
         (void)hipFree(fs.bin_list);
         (void)hipFree(fs.global_list);
         (void)hipFree(fs.times);
+        (void)hipFree(fs.dyn_desc);
+        (void)hipFree(fs.pairs);
+        (void)hipFree(fs.plan_desc);
+        (void)hipFree(fs.plan_counts);
         for (hipEvent_t e : {fs.ready, fs.done})
             if (e) (void)hipEventDestroy(e);
     }

@@ -472,14 +472,17 @@ def test_moving_camera_reuses_lists_exactly(dragon, W, H, r0, r1, degs):
     assert paths[still]["sizings"] == 1 and fills[still] > 0, (paths[still], fills[still])
 
 
-def test_moving_camera_pool_overflow_exact(dragon, monkeypatch):
+@pytest.mark.parametrize("device_fill", ["1", "0"])
+def test_moving_camera_pool_overflow_exact(dragon, monkeypatch, device_fill):
     """A moving camera's device-sized lists with a pool far too small
     (XRT_MOTION_POOL=300 entries): the lists that do not fit get what is left,
     their regions render from the whole mesh (exact), k_prep's flags report
     the overflows when the set is next used; every frame, through device planes
-    on two streams, equals a brute-force render of its camera."""
+    on two streams, equals a brute-force render of its camera -- over the
+    device fill plan (empty regions one fill workgroup each) and without it."""
     import torch
     monkeypatch.setenv("XRT_MOTION_POOL", "300")
+    monkeypatch.setenv("XRT_DEVICE_FILL", device_fill)
     W, H = 512, 384
     lo, hi = xrt.mesh_bbox(dragon)
     centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
