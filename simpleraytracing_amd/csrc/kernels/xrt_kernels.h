@@ -2389,12 +2389,13 @@ __device__ __forceinline__ void stage_survivor_records(RecStage& st, const TriRe
     }
 }
 
-__device__ __forceinline__ void test_staged_one(const RecStage& st, uint32_t k, float dx, float dy, float dz,
-                                                HitList& hl)
+#ifndef XRT_PUSH_BALLOT
+#define XRT_PUSH_BALLOT 1
+#endif
+// TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[3].x)
+__device__ __forceinline__ void test_rec(float4 a0, float4 a1, float4 a2, float tnum, float dx, float dy, float dz,
+                                         HitList& hl)
 {
-    // TriRec: e1 (a0.xyz), e2 (a0.w, a1.xy), tvec (a1.zw, a2.x), qvec (a2.yzw), tnum (q[3].x)
-    const float4 a0 = st.q[0][k], a1 = st.q[1][k], a2 = st.q[2][k];
-    const float tnum = st.q[3][k].x;
     float det, u, v;
     mt_numerators(dx, dy, dz, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w,
                   det, u, v);
@@ -2404,8 +2405,21 @@ __device__ __forceinline__ void test_staged_one(const RecStage& st, uint32_t k, 
     if (__builtin_expect(__ballot(!rcp_newton_exact_for(det)) != 0ull, 0)) inv = inv_det_of(det);
     bool h;
     const float t = mt_finish_inv(det, inv, u, v, tnum, h);
+#if XRT_PUSH_BALLOT
+    // a survivor of the conservative tile cull often hits none of the tile's
+    // rays: its insert (kMaxHits v_med3) skipped behind one wave-uniform branch
+    if (__ballot(h)) hl.push_if(h, t);
+#else
     hl.push_if(h, t);
+#endif
 }
+
+__device__ __forceinline__ void test_staged_one(const RecStage& st, uint32_t k, float dx, float dy, float dz,
+                                                HitList& hl)
+{
+    test_rec(st.q[0][k], st.q[1][k], st.q[2][k], st.q[3][k].x, dx, dy, dz, hl);
+}
+
 
 // The signed model's: the term's sign from the record's unit normal (pad0..2),
 // `id` the candidate's triangle id (wave-uniform).
