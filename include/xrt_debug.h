@@ -100,6 +100,16 @@ int xrt_debug_fill_regions(xrt_context* ctx, uint32_t* regions);
 int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4]);
 
 /*
+ * Diagnostics: counters[0] = host-buffer frames (xrt_render_rows) of a geometry
+ * seen for the first time that were sized on the device (the count pass, one
+ * 32-byte read-back of its pair
+ * total, the lists carved and filled by k_size_lists / k_scatter_pairs; no
+ * host plan, no second k_prep; XRT_DEVICE_FIRST=0 turns it off), [1] = those
+ * whose pool was too small for the pair total, grown and counted again.
+ */
+int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[2]);
+
+/*
  * Diagnostics: the frame pipeline since the context was created --
  * counters[0] frames rendered from a preparation made ahead of their call
  * (xrt_render_rows_device repeating its frame geometry), [1] preparations made

@@ -225,6 +225,12 @@ class Context:
         self._check(self._lib.xrt_debug_geometry_counters(self._ctx, c), "xrt_debug_geometry_counters")
         return dict(zip(("sizings", "reused", "plan_misses", "overflows"), (int(v) for v in c)))
 
+    def first_frames(self) -> dict:
+        """Frames of a new geometry sized on the device, and those whose pool was regrown (xrt_debug_first_frames)."""
+        c = (ctypes.c_uint64 * 2)()
+        self._check(self._lib.xrt_debug_first_frames(self._ctx, c), "xrt_debug_first_frames")
+        return {"device_sized": int(c[0]), "recounted": int(c[1])}
+
     def wave_times(self, frames_back: int = 0) -> np.ndarray:
         """Timing records of the render frames_back frames before the last (xrt_debug_wave_times):
         (n, 2) u32 s_memrealtime start / end (100 MHz, low 32 bits), one per statistics record."""

@@ -148,6 +148,7 @@ XRT_SYMBOLS = {
     "xrt_set_fill_plan": (ctypes.c_int, [_CtxP, ctypes.c_int]),
     "xrt_debug_fill_regions": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint32)]),
     "xrt_debug_geometry_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
+    "xrt_debug_first_frames": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_pipeline_counters": (ctypes.c_int, [_CtxP, ctypes.POINTER(ctypes.c_uint64)]),
     "xrt_debug_host_call_ms": (ctypes.c_int, [_CtxP, _dp]),
     "xrt_debug_destroy_ms": (ctypes.c_int, [_dp]),

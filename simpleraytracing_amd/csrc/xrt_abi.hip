@@ -333,6 +333,8 @@ struct xrt_context {
     uint64_t motion_pool = 0;          // entries of a device-sized (moving camera) frame's lists
     uint64_t motion_pool_forced = 0;   // test hook XRT_MOTION_POOL: that many entries, never grown
     bool device_fill = true;           // moving frames render over the device fill plan (XRT_DEVICE_FILL=0: off)
+    bool device_first = true;          // a geometry's first frame sized on the device (XRT_DEVICE_FIRST=0: off)
+    bool dev_geometry = false;         // bin_key's only frame was sized on the device (no compact lists)
     // Box tile masks (BinBuffers::box_masks; XRT_BOX_MASKS): 0 (default)
     // never, 1 in the host-sized frames of meshes under kPrepBigMesh
     // triangles, 2 in every binned frame.  Exact either way; measured a wash
@@ -498,6 +500,7 @@ struct xrt_context {
     BinKey call_key = {};              // the last device-pointer call's geometry
     uint64_t call_state_gen = ~0ull;
     uint64_t hp_ahead_used = 0, hp_ahead_dropped = 0, hp_launch_nowait = 0, hp_host_waits = 0;
+    uint64_t hp_dev_first = 0, hp_dev_first_recounts = 0;   // first frames sized on the device; pools regrown
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     uint32_t model = kModelAttenuation;   // xrt_set_model
     float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
@@ -951,14 +954,20 @@ int bin_buffers(xrt_context* ctx, FrameSet& fs, uint32_t n_regions, uint64_t lis
 // centred object does not start last and set the tail.
 std::vector<uint32_t> centre_first_order(uint32_t rx, uint32_t ry)
 {
+    // by squared distance from the grid's centre, ties in region order: keys
+    // (4 x the squared distance, exact in integers) beside the indices, sorted
+    // once (a comparator recomputing the distances took 0.37 ms at 64 x 64)
     const size_t n = (size_t)rx * ry;
+    std::vector<std::pair<uint64_t, uint32_t>> key(n);
+    for (uint32_t y = 0; y < ry; ++y)
+        for (uint32_t x = 0; x < rx; ++x) {
+            const int64_t dx = 2 * (int64_t)x - ((int64_t)rx - 1), dy = 2 * (int64_t)y - ((int64_t)ry - 1);
+            const size_t r = (size_t)y * rx + x;
+            key[r] = {(uint64_t)(dx * dx + dy * dy), (uint32_t)r};
+        }
+    std::sort(key.begin(), key.end());
     std::vector<uint32_t> order(n);
-    for (size_t r = 0; r < n; ++r) order[r] = (uint32_t)r;
-    const double cx = 0.5 * (rx - 1), cy = 0.5 * (ry - 1);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        const double ax = a % rx - cx, ay = a / rx - cy, bx = b % rx - cx, by = b / rx - cy;
-        return ax * ax + ay * ay < bx * bx + by * by;
-    });
+    for (size_t k = 0; k < n; ++k) order[k] = key[k].second;
     return order;
 }
 
@@ -1163,8 +1172,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     ctx->still_frames = key.same(ctx->last_key) ? ctx->still_frames + 1u : 0u;
     ctx->last_key = key;
     bool reuse = false;
-    if (binned && rows > 0 && fill_ok && ctx->bin_key_valid && ctx->compact && !ctx->bin_force_cap &&
-        !ctx->packed_cap && !ctx->hits_cap) {
+    if (binned && rows > 0 && fill_ok && ctx->bin_key_valid && (ctx->compact || ctx->dev_geometry) &&
+        !ctx->bin_force_cap && !ctx->packed_cap && !ctx->hits_cap) {
         if (ctx->reuse_cameras && !key.same(ctx->bin_key) && key.same_layout(ctx->bin_key) &&
             ctx->still_frames < kStillFrames) {
             reuse = true;
@@ -1176,14 +1185,36 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         }
     }
     if (!key.same_layout(ctx->bin_key)) ctx->moving = false;
-    const bool new_geometry = binned && rows > 0 && !reuse && (!ctx->bin_key_valid || !key.same(ctx->bin_key));
+    // (a geometry whose only frame was sized on the device has no compact
+    // lists: the same camera again is sized on the host)
+    const bool new_geometry = binned && rows > 0 && !reuse &&
+                              (!ctx->bin_key_valid || !key.same(ctx->bin_key) || ctx->dev_geometry);
     if (new_geometry) ctx->compact = false;
     const uint32_t fixed_cap = ctx->bin_force_cap ? (uint32_t)std::min<size_t>(kInitialRegionCap, ctx->bin_force_cap)
                                                   : kInitialRegionCap;
+    // A frame geometry seen for the first time -- a context's first frame, the
+    // reference's whole workload -- is sized on the device as a moving camera's
+    // frame is (below; one 32-byte read-back for the pool, no host plan and no
+    // second k_prep); the same geometry again is sized on the host (compact
+    // lists, fill plan, heaviest regions first) for the frames that follow.
+    // Host-buffer calls only (xrt_render_rows: the drop-in renderLoop's one
+    // frame into an Image): device-pointer callers -- pipelines, and strips
+    // whose transit plans (xrt_plan_region_map, xrt_plan_hit_layout) describe
+    // the host-sized layout of the frame before -- keep the host sizing.
+    const bool dev_first = new_geometry && !ctx->bin_force_cap && ctx->device_first && ctx->still_frames == 0u &&
+                           fill_ok && !ctx->packed_cap && !ctx->hits_cap && ctx->reuse_cameras &&
+                           stream == ctx->host_stream;
+    const bool device_sized = reuse || dev_first;
+    if (new_geometry) ctx->dev_geometry = false;
+    if (dev_first) {                               // later cameras over its region grid take the moving path
+        ctx->dev_geometry = true;
+        ctx->bin_key = key;
+        ctx->bin_key_valid = true;
+    }
     // A new geometry's first k_prep only counts its pairs (no lists): the
     // compact lists are sized from the counts and k_prep runs again into them.
-    const bool sizing = new_geometry && !ctx->bin_force_cap;
-    if (sizing && ctx->sizing_profile) {
+    const bool sizing = new_geometry && !ctx->bin_force_cap && !dev_first;
+    if ((sizing || dev_first) && ctx->sizing_profile) {
         ctx->prof_t = t_call;
         prof_mark(ctx, "set wait + buffers");
     }
@@ -1191,7 +1222,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.regions_x = rx;
         bins.regions_y = ry;
     }
-    if (binned && !reuse) {
+    if (binned && !device_sized) {
         const bool compact = ctx->compact && !ctx->bin_force_cap;
         bool cleared = false;
         const uint64_t entries = compact ? ctx->slot_pool : sizing ? 0u : (uint64_t)n_regions * fixed_cap;
@@ -1210,37 +1241,70 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     }
 
     hipEvent_t prep_done = fs.ready;
-    if (reuse) {
+    if (device_sized) {
         // A moving camera (DESIGN.md "Moving camera"): its lists sized on the
         // device, no host round trip -- k_prep counts its pairs per slot of the
         // region grid's base layout (centre first), k_size_lists carves each
         // slot's list from the set's pool, k_prep bins into them.  Every region
         // renders as tiles (no fill plan: the host never sees the counts).
         // k_prep's flags are read when the set is next used (lazy_flags).
+        // (a geometry's first frame: room for ~6 pairs a triangle, checked below)
+        const uint64_t first_guess = dev_first ? 6u * (uint64_t)T + 2u * n_regions : 0u;
         ctx->motion_pool = ctx->motion_pool_forced
                                ? ctx->motion_pool_forced
-                               : std::max<uint64_t>(ctx->motion_pool, std::max<uint64_t>(2 * ctx->slot_pool, 65536u));
+                               : std::max<uint64_t>(std::max<uint64_t>(ctx->motion_pool, first_guess),
+                                                    std::max<uint64_t>(2 * ctx->slot_pool, 65536u));
         bool cleared = false;
         if ((rc = bin_buffers(ctx, fs, n_regions, ctx->motion_pool, bins, bin_ctl, ps, cleared))) return rc;
+        if (dev_first) prof_mark(ctx, "device first: bin buffers");
         if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+        if (dev_first) prof_mark(ctx, "device first: fixed layout");
         if ((rc = ensure(ctx, fs.dyn_desc, fs.dyn_desc_cap, n_regions))) return rc;
         if ((rc = ensure(ctx, fs.pairs, fs.pairs_cap, ctx->motion_pool))) return rc;
         // the device fill plan (not for the transit layouts, whose tiles follow a host plan)
-        const bool dev_plan = ctx->device_fill && out.packed == 0u;
+        const bool dev_plan = ctx->device_fill && ctx->fill_plan != 0 && out.packed == 0u;
         if (dev_plan && ((rc = ensure(ctx, fs.plan_desc, fs.plan_desc_cap, n_regions)) ||
                          (rc = ensure(ctx, fs.plan_counts, fs.plan_counts_cap, (size_t)n_regions * kCounterStride))))
             return rc;
-        const uint32_t pool = (uint32_t)std::min<uint64_t>(ctx->motion_pool, 0xFFFFFFFFull);
+        uint32_t pool = (uint32_t)std::min<uint64_t>(ctx->motion_pool, 0xFFFFFFFFull);
         bins.tile_slots = n_regions;
         bins.split_slots = 0u;
         bins.tile_plan = 0u;
         bins.plan_miss = nullptr;
         bins.box_masks = ctx->box_masks == 2 ? 1u : 0u;
-        RegionEntry* const list = bins.list;
+        RegionEntry* list = bins.list;
         bins.list = nullptr;                           // the count-only pass, appending its pairs
         bins.pairs = fs.pairs;
         bins.pairs_cap = pool;
         if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+        if (dev_first) prof_mark(ctx, "device first: count pass (buffers before it)");
+        if (dev_first) {
+            // A first frame has no earlier pose to size its pool from: the count
+            // pass's pair total (32 bytes read back) checks it, and a pool too
+            // small grows and counts again -- never the whole-mesh fallback.
+            ++ctx->hp_dev_first;
+            uint8_t* hs = nullptr;
+            if ((rc = sizing_scratch(ctx, sizeof(BinState), hs))) return rc;
+            XRT_HIP(ctx, hipMemcpyAsync(hs, bin_ctl, sizeof(BinState), hipMemcpyDeviceToHost, ps));
+            XRT_HIP(ctx, hipStreamSynchronize(ps));
+            BinState st;
+            std::memcpy(&st, hs, sizeof st);
+            prof_mark(ctx, "device first: pair total read back");
+            if (st.pairs > pool && !ctx->motion_pool_forced) {
+                ++ctx->hp_dev_first_recounts;
+                ctx->motion_pool = std::min<uint64_t>((uint64_t)st.pairs + st.pairs / 4u + 65536u, 0xFFFFFFFFull);
+                pool = (uint32_t)ctx->motion_pool;
+                if ((rc = bin_buffers(ctx, fs, n_regions, ctx->motion_pool, bins, bin_ctl, ps, cleared, true)))
+                    return rc;                     // (clears this frame's counters)
+                if ((rc = fixed_layout(ctx, rx, ry, fixed_cap, bins))) return rc;
+                if ((rc = ensure(ctx, fs.pairs, fs.pairs_cap, ctx->motion_pool))) return rc;
+                list = bins.list;
+                bins.list = nullptr;
+                bins.pairs = fs.pairs;
+                bins.pairs_cap = pool;
+                if ((rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+            }
+        }
         uint32_t* const flag = fs.plan_flag ? const_cast<uint32_t*>(fs.plan_flag) : nullptr;
         if (flag) {                                    // [1]: a list past the pool, read lazily
             flag[0] = 0u;
@@ -1265,7 +1329,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         bins.pairs = nullptr;
         bins.clear = nullptr;
     }
-    if (rows > 0 && !reuse && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done))) return rc;
+    if (rows > 0 && !device_sized && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done)))
+        return rc;
     if (sizing) {
         // Size the compact region lists once per frame geometry (mesh, camera,
         // strip): a synchronous read of every region's count (the count-only
@@ -1367,7 +1432,7 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
     pf.hit_plan_ok = ctx->hit_valid && key.same(ctx->hit_key);
     pf.stream = stream;
     pf.prep_done = rows > 0 ? prep_done : nullptr;
-    pf.host_wait = bins.plan_miss != nullptr && !reuse;
+    pf.host_wait = bins.plan_miss != nullptr && !device_sized;
     pf.kernel = kernel;
     pf.binned = binned;
     pf.rows = rows;
@@ -1817,6 +1882,7 @@ int xrt_create(int device, xrt_context** out)
     if (const char* mp = std::getenv("XRT_MOTION_POOL")) ctx->motion_pool_forced = std::strtoull(mp, nullptr, 10);
     if (const char* bm = std::getenv("XRT_BOX_MASKS")) ctx->box_masks = std::atoi(bm);
     if (const char* df = std::getenv("XRT_DEVICE_FILL")) ctx->device_fill = std::atoi(df) != 0;
+    if (const char* dq = std::getenv("XRT_DEVICE_FIRST")) ctx->device_first = std::atoi(dq) != 0;
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
@@ -2334,6 +2400,14 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     counters[1] = ctx->hp_reused;
     counters[2] = ctx->hp_plan_miss;
     counters[3] = ctx->hp_overflow;
+    return XRT_OK;
+}
+
+int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[2])
+{
+    if (!ctx || !counters) return XRT_ERR_ARGUMENT;
+    counters[0] = ctx->hp_dev_first;
+    counters[1] = ctx->hp_dev_first_recounts;
     return XRT_OK;
 }
 
