@@ -105,9 +105,10 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4]);
  * 32-byte read-back of its pair
  * total, the lists carved and filled by k_size_lists / k_scatter_pairs; no
  * host plan, no second k_prep; XRT_DEVICE_FIRST=0 turns it off), [1] = those
- * whose pool was too small for the pair total, grown and counted again.
+ * whose pool was too small for the pair total, grown and counted again, [2] /
+ * [3] = the last such frame's pair total and the pool its count pass had.
  */
-int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[2]);
+int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[4]);
 
 /*
  * Diagnostics: the frame pipeline since the context was created --

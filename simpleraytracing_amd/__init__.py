@@ -227,9 +227,9 @@ class Context:
 
     def first_frames(self) -> dict:
         """Frames of a new geometry sized on the device, and those whose pool was regrown (xrt_debug_first_frames)."""
-        c = (ctypes.c_uint64 * 2)()
+        c = (ctypes.c_uint64 * 4)()
         self._check(self._lib.xrt_debug_first_frames(self._ctx, c), "xrt_debug_first_frames")
-        return {"device_sized": int(c[0]), "recounted": int(c[1])}
+        return {"device_sized": int(c[0]), "recounted": int(c[1]), "last_pairs": int(c[2]), "last_pool": int(c[3])}
 
     def wave_times(self, frames_back: int = 0) -> np.ndarray:
         """Timing records of the render frames_back frames before the last (xrt_debug_wave_times):

@@ -501,6 +501,7 @@ struct xrt_context {
     uint64_t call_state_gen = ~0ull;
     uint64_t hp_ahead_used = 0, hp_ahead_dropped = 0, hp_launch_nowait = 0, hp_host_waits = 0;
     uint64_t hp_dev_first = 0, hp_dev_first_recounts = 0;   // first frames sized on the device; pools regrown
+    uint64_t dev_first_pairs = 0, dev_first_pool = 0;       // the last one's pair total and first pool
     uint32_t miss_code = 0;            // L-buffer bits of a miss (0: +inf; xrt_set_miss_code)
     uint32_t model = kModelAttenuation;   // xrt_set_model
     float mu = 0.1037f;                // kModelSigned: mesh 0's attenuation coefficient
@@ -1290,6 +1291,8 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
             BinState st;
             std::memcpy(&st, hs, sizeof st);
             prof_mark(ctx, "device first: pair total read back");
+            ctx->dev_first_pairs = st.pairs;
+            ctx->dev_first_pool = pool;
             if (st.pairs > pool && !ctx->motion_pool_forced) {
                 ++ctx->hp_dev_first_recounts;
                 ctx->motion_pool = std::min<uint64_t>((uint64_t)st.pairs + st.pairs / 4u + 65536u, 0xFFFFFFFFull);
@@ -2403,11 +2406,13 @@ int xrt_debug_geometry_counters(xrt_context* ctx, uint64_t counters[4])
     return XRT_OK;
 }
 
-int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[2])
+int xrt_debug_first_frames(xrt_context* ctx, uint64_t counters[4])
 {
     if (!ctx || !counters) return XRT_ERR_ARGUMENT;
     counters[0] = ctx->hp_dev_first;
     counters[1] = ctx->hp_dev_first_recounts;
+    counters[2] = ctx->dev_first_pairs;
+    counters[3] = ctx->dev_first_pool;
     return XRT_OK;
 }
 

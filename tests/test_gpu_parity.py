@@ -559,6 +559,55 @@ def test_box_masks_exact(dragon, monkeypatch, name, model):
                 assert getattr(got[3], f) == getattr(ref[3], f), (mode, k, f)
 
 
+@pytest.mark.parametrize("case", ["dragon-strip", "planes-recount", "soup"])
+def test_first_frame_device_sized_exact(dragon, case):
+    """A geometry's first host-buffer frame is sized on the device (the count
+    pass, one read-back of its pair total, k_size_lists / k_scatter_pairs, the
+    device fill plan): equal to brute force bit for bit, statistics included --
+    a strip starting off the region grid; planes each covering every region, so
+    the first pool (6 pairs a triangle, at least 65,536) is too small and the
+    pass counts again; a random soup.  The same camera again is sized on the host, a new
+    one takes the moving path, every frame exact."""
+    from scene_kit import plane_stack
+    if case == "dragon-strip":
+        tris, W, H, r0, r1 = dragon, 1000, 777, 13, 700
+    elif case == "planes-recount":
+        tris, W, H, r0, r1 = plane_stack(20, spacing=0.05), 2048, 2048, 0, None
+    else:
+        tris, W, H, r0, r1 = synthetic_soup(seed=5, n=4000), 400, 300, 0, None
+    cam = xrt.camera_for_mesh(tris, W, H)
+    if case == "planes-recount":
+        cam.pixel_spacing *= 0.25          # the squares fill the frame: ~2,000 regions a triangle
+    lo, hi = xrt.mesh_bbox(tris)
+    centre = 0.5 * (np.asarray(lo, np.float64) + np.asarray(hi, np.float64))
+    cams = [cam, cam, orbit_camera(cam, centre, 3.0)]
+    with xrt.Context(0) as brute:
+        brute.set_kernel(xrt.XRT_KERNEL_BRUTE)
+        brute.upload_mesh(tris)
+        refs = [brute.render_rows(c, r0, r1) for c in cams]
+    with xrt.Context(0) as c:
+        c.set_kernel(xrt.XRT_KERNEL_BINNED)
+        c.upload_mesh(tris)
+        paths = []
+        for k, cm in enumerate(cams):
+            g0, f0 = c.geometry_counters(), c.first_frames()
+            got = c.render_rows(cm, r0, r1)
+            g1, f1 = c.geometry_counters(), c.first_frames()
+            if k == 0:
+                ff = f1
+            paths.append((f1["device_sized"] - f0["device_sized"], f1["recounted"] - f0["recounted"],
+                          g1["sizings"] - g0["sizings"], g1["reused"] - g0["reused"]))
+            for x, y in zip(got[:3], refs[k][:3]):
+                assert np.array_equal(bits(x), bits(y)), (case, k)
+            for f in ("rays", "hits", "hit_rays", "odd_rays", "max_hits"):
+                assert getattr(got[3], f) == getattr(refs[k][3], f), (case, k, f)
+    assert paths[0][0] == 1 and paths[0][2] == 0, paths       # device-sized, no host sizing
+    assert paths[1][2] == 1 and paths[1][0] == 0, paths       # the same camera: sized on the host
+    assert paths[2][3] == 1, paths                            # a new camera: the moving path
+    if case == "planes-recount":
+        assert paths[0][1] == 1, (paths, ff)
+
+
 def test_contexts_share_device_streams_exact(dragon):
     """Contexts of one device share its prep and host streams (acquire_streams):
     two contexts interleaving frames in flight on two caller streams -- one
