@@ -63,6 +63,9 @@ constexpr double kTicksPerMs = 1e5;
 #define XRT_FRAME_SETS 4
 #endif
 constexpr int kFrameSets = XRT_FRAME_SETS;
+#ifndef XRT_DEV_SIZE_ON_PREP
+#define XRT_DEV_SIZE_ON_PREP 0   // a device-sized frame's k_size_lists / k_scatter_pairs on the prep stream
+#endif
 // LDS a k_prep workgroup holds (its own + dynamic padding): the CU's LDS left
 // beside a render at full occupancy (XRT_RENDER_WAVES waves per SIMD, each
 // with its record stage), split over kPrepPerCu workgroups, so no more of
@@ -1331,6 +1334,24 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         }
         bins.pairs = nullptr;
         bins.clear = nullptr;
+#if XRT_DEV_SIZE_ON_PREP
+        // k_size_lists and k_scatter_pairs behind the count pass on the prep
+        // stream (on a render stream they queue behind that stream's previous
+        // render), the preparation's event after them
+        {
+            const PendingFrame::DevSize& d = pf.dev_size;
+            hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, ps, d.counts, d.fixed,
+                               fs.dyn_desc, d.n_slots, d.pool, bin_ctl, d.plan_desc, d.plan_counts);
+            XRT_HIP(ctx, hipGetLastError());
+            const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((d.pool + 255u) / 256u, 2048u);
+            hipLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, ps, (const uint4*)fs.pairs,
+                               (const BinState*)bin_ctl, d.pool, (const SlotDesc*)fs.dyn_desc,
+                               (const float4*)fs.cull, (uint32_t)ctx->num_tris, bins.list, d.flag);
+            XRT_HIP(ctx, hipGetLastError());
+            XRT_HIP(ctx, hipEventRecord(prep_done, ps));
+            pf.dev_size.on = false;
+        }
+#endif
     }
     if (rows > 0 && !device_sized && (rc = launch_prep(ctx, fs, p, cp, culled, bins, bin_ctl, ps, prep_done)))
         return rc;
