@@ -64,7 +64,12 @@ constexpr double kTicksPerMs = 1e5;
 #endif
 constexpr int kFrameSets = XRT_FRAME_SETS;
 #ifndef XRT_DEV_SIZE_ON_PREP
-#define XRT_DEV_SIZE_ON_PREP 0   // a device-sized frame's k_size_lists / k_scatter_pairs on the prep stream
+// Where a device-sized frame's k_size_lists / k_scatter_pairs run: 0 on the
+// render's stream (behind that stream's previous render), 1 on the prep stream
+// (behind the count pass: the prep chain grows), 2 on the device's host stream
+// after the count pass's event (idle in a device-pointer pipeline; no extra
+// queue): 2048^2 moving frames 47.0 / 57.5 / 41.1 us (profiles/r06ac, r06ae).
+#define XRT_DEV_SIZE_ON_PREP 2
 #endif
 // LDS a k_prep workgroup holds (its own + dynamic padding): the CU's LDS left
 // beside a render at full occupancy (XRT_RENDER_WAVES waves per SIMD, each
@@ -1339,16 +1344,20 @@ int prepare_frame(xrt_context* ctx, const xrt_camera* cam, uint32_t row_begin, u
         // stream (on a render stream they queue behind that stream's previous
         // render), the preparation's event after them
         {
+            // (2: on the device's host stream -- idle in a device-pointer
+            // pipeline, no extra queue -- after the count pass's event)
+            const hipStream_t ss = XRT_DEV_SIZE_ON_PREP == 2 ? ctx->host_stream : ps;
+            if (ss != ps) XRT_HIP(ctx, hipStreamWaitEvent(ss, prep_done, 0));
             const PendingFrame::DevSize& d = pf.dev_size;
-            hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, ps, d.counts, d.fixed,
+            hipLaunchKernelGGL(k_size_lists, dim3((d.n_slots + 255) / 256), dim3(256), 0, ss, d.counts, d.fixed,
                                fs.dyn_desc, d.n_slots, d.pool, bin_ctl, d.plan_desc, d.plan_counts);
             XRT_HIP(ctx, hipGetLastError());
             const uint32_t scatter_blocks = (uint32_t)std::min<uint64_t>((d.pool + 255u) / 256u, 2048u);
-            hipLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, ps, (const uint4*)fs.pairs,
+            hipLaunchKernelGGL(k_scatter_pairs, dim3(scatter_blocks), dim3(256), 0, ss, (const uint4*)fs.pairs,
                                (const BinState*)bin_ctl, d.pool, (const SlotDesc*)fs.dyn_desc,
                                (const float4*)fs.cull, (uint32_t)ctx->num_tris, bins.list, d.flag);
             XRT_HIP(ctx, hipGetLastError());
-            XRT_HIP(ctx, hipEventRecord(prep_done, ps));
+            XRT_HIP(ctx, hipEventRecord(prep_done, ss));
             pf.dev_size.on = false;
         }
 #endif
